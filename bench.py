@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark: env steps/s (= full BPR user-equilibrium assignments/s) of N
+vectorised Sioux Falls repair envs per MI355X (BASELINE.json configs[1]:
+4096 envs, MSA 30 iterations).
+
+One "step" = RepairEnv.step for every env of the batch (src/env/repair_env.py:
+207-237): repair the chosen link, re-run the 30-iteration assignment, reward,
+done, and the get_state observation (751-819) -- one trx_step + one
+trx_observe launch.  Actions: uniform over each env's damaged links (device
+RNG).  Damage: fixed_damage_seed=42 for all envs (the trainer's config);
+episodes are 22 steps, all envs auto-reset together (the reset assignment is
+inside the timed region but not counted as a step).
+
+Multi-GPU: one process per GPU (torchrun), envs sharded with no data-path
+collective (weak scaling); max elapsed over ranks; value = all ranks' steps /
+that time.
+
+Prints ONE JSON line on rank 0 (driver contract), with
+  roofline:     algorithmic bytes per env_kernel launch (SURVEY.md §8(d):
+                bytes(assign) x envs) / the kernel's mean duration measured
+                with HIP events on its stream, vs 8 TB/s HBM peak;
+  cpu_baseline: the C restatement (oracle/, kind "port") timed on host cores
+                on a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "env steps/sec (full BPR assigns/sec), N vectorised Sioux Falls envs, 1/2/4/8 GPU"
+HBM_PEAK = 8.0e12  # MI355X_MICROARCH.md: HBM3E peak 8.0 TB/s (spec)
+
+
+def bytes_per_assign(N, E, Z, P, K):
+    """SURVEY.md §8(d) algorithmic bytes of one full assignment (4-byte elements)."""
+    return (K + 1) * 20 * E + K * (Z * (8 * E + 12 * N) + 4 * P + 4 * E + 12 * E) + 8 * E
+
+
+def fixed_damage_mask(E, seed=42, ratio=0.3):
+    from trafficrl.data import sioux_falls
+    from trafficrl.graph import DamageSampler
+
+    g = sioux_falls()
+
+    class _G:
+        num_edges = len(g.edges)
+        num_nodes = g.num_nodes
+        src = np.array([e.u - 1 for e in g.edges], np.int32)
+        dst = np.array([e.v - 1 for e in g.edges], np.int32)
+
+    return DamageSampler(_G, 0, fixed_damage=True, fixed_damage_seed=seed).sample(ratio)
+
+
+def cpu_baseline(method, iters, seconds=12.0):
+    """Time the oracle's C restatement (same algorithm: scipy-order Dijkstra,
+    predecessor path walk, fp32 MSA/FW) on the host cores, warm-started
+    steps of the fixed-damage env (one assignment each)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test/baseline infrastructure only
+
+    og = O.OracleGraph.from_npz(os.path.join(ROOT, "tests", "golden", "sf_graph.npz"))
+    gr = np.load(os.path.join(ROOT, "tests", "golden", "sf_graph.npz"))
+    E = og.E
+    dmg = fixed_damage_mask(E)
+    cap = np.where(dmg > 0, np.float32(1e-3), gr["cap0"]).astype(np.float32)
+    f0, _, _, _ = og.assign(cap, dmg, np.zeros(E, np.float32), method=method, iters=iters)
+    threads = max(1, min(16, os.cpu_count() or 1, O.max_threads()))
+    # repair one random damaged link per row, warm start from the reset flow
+    rng = np.random.default_rng(7)
+    B = 64 * threads
+    cand = np.where(dmg > 0)[0]
+    C = np.repeat(cap[None], B, 0)
+    D = np.repeat(dmg[None], B, 0)
+    a = rng.choice(cand, B)
+    C[np.arange(B), a] = gr["cap0"][a]
+    D[np.arange(B), a] = 0.0
+    F = np.repeat(f0[None], B, 0)
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        og.assign(C, D, F, method=method, iters=iters, nthreads=threads)
+        done += B
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "env steps/s", "cores": threads, "kind": "port",
+            "sample": f"{done} warm-started {method.upper()}-{iters} steps (SF, fixed damage seed 42, one repaired "
+                      f"link each) in {dt:.1f}s on {threads} host threads; oracle/trx_oracle.c"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=66)
+    ap.add_argument("--warmup", type=int, default=22)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--method", default="msa", choices=["msa", "fw", "cfw"])
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--no-observe", action="store_true", help="skip get_state (assignment-only steps)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from trafficrl.data import sioux_falls
+    from trafficrl.env import VecRepairEnv
+
+    B = args.envs
+    gd = sioux_falls()
+    env = VecRepairEnv(gd, B, device=dev, assignment_method=args.method, assignment_iters=args.iters,
+                       reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0, reward_gamma=0.0,
+                       reward_clip=2.0, capacity_damage=1e-3, unassigned_penalty=1e4, reset=False)
+    E, N = env.num_edges, env.num_nodes
+    dmg0 = torch.from_numpy(fixed_damage_mask(E)).to(dev)
+    dmg_all = dmg0[None].expand(B, E).contiguous()
+    ep_len = int(dmg0.sum().item())
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    observe = not args.no_observe
+
+    ev_pairs = []
+
+    def timed_kernel(fn):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        ev_pairs.append((s, e))
+
+    state = {"t": 0}
+
+    def reset():
+        timed_kernel(lambda: env.reset(damaged=dmg_all, observe=False))
+        if observe:
+            env.observe()
+        state["t"] = 0
+
+    def one_step():
+        scores = torch.rand(B, E, device=dev, generator=gen) * env.damaged
+        actions = scores.argmax(dim=1).to(torch.int32)
+        timed_kernel(lambda: env.step(actions, observe=False, check=False))
+        if observe:
+            env.observe()
+        state["t"] += 1
+        if state["t"] == ep_len:
+            reset()
+
+    reset()
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    ev_pairs.clear()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [s.elapsed_time(e) for s, e in ev_pairs]
+    mean_kernel_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = torch.tensor([mean_kernel_s], device=dev, dtype=torch.float64)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        mean_kernel_s = float(k.item())
+
+    total_steps = args.steps * B * world
+    value = total_steps / elapsed
+    Z = env.graph.num_origins
+    P = len(env.graph.od_o)
+    bpa = bytes_per_assign(N, E, Z, P, args.iters)
+    achieved = bpa * B / mean_kernel_s
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(args.method, args.iters, args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (link flows/costs) + f64 (path labels)",
+            "data": "synthetic: Sioux Falls TNTP, fixed_damage_seed=42, uniform random valid repair actions",
+            "config": {
+                "workload": f"SF {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment per step"
+                            + (", get_state included" if observe else ""),
+                "envs_per_gpu": B, "global_envs": B * world, "network": "SiouxFalls (24 nodes, 76 links, 528 OD)",
+                "method": args.method, "assignment_iters": args.iters, "episode_len": ep_len,
+                "parallelism": f"env-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": None,
+                "kernel": "trx::env_kernel<24>", "kernel_mean_ms": mean_kernel_s * 1e3,
+                "bytes_per_assign": bpa, "assigns_per_launch": B,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

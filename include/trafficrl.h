@@ -1,0 +1,151 @@
+/*
+ * trafficrl.h -- C ABI of libtrafficrl.so, the MI355X (gfx950) implementation
+ * of the reference's per-step user-equilibrium hot path.
+ *
+ * The reference's boundary is Python (pop-pop-pOp-dev/SAC-GAT-HER_transportationRL,
+ * src/env/repair_env.py); every entry point below names the reference
+ * function/statement range it replaces.  INTEGRATION.md shows the ctypes
+ * binding the reference side would add; trafficrl/_lib.py is that binding.
+ *
+ * Conventions
+ *  - All buffers are CALLER-OWNED DEVICE pointers (e.g. torch tensors'
+ *    data_ptr()), row-major [B, E] / [B] unless noted.  Graph inputs to
+ *    trx_graph_create are HOST pointers (copied to the device).
+ *  - Every call is stream-ordered and asynchronous on `stream` (a
+ *    hipStream_t passed as void*; NULL = the null stream).  No call
+ *    allocates, frees or synchronises (hipGraph-capturable), except
+ *    trx_graph_create/destroy.
+ *  - A graph handle is bound to the device current at creation.  Handles are
+ *    immutable after creation and may be shared by threads; one stream per
+ *    host thread.
+ *  - Return 0 on success, <0 on error; trx_last_error() gives a thread-local
+ *    message.  No C++ exception crosses this boundary.
+ */
+#ifndef TRAFFICRL_H
+#define TRAFFICRL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRX_ABI_VERSION 1
+
+/* error codes */
+#define TRX_OK 0
+#define TRX_EINVAL (-1)   /* bad argument (ValueError on the Python side)   */
+#define TRX_EHIP (-2)     /* HIP runtime failure (RuntimeError)             */
+#define TRX_EUNSUP (-3)   /* input outside what a kernel supports           */
+
+/* assignment methods: RepairEnv(assignment_method=...) repair_env.py:55,304-335 */
+#define TRX_METHOD_MSA 0
+#define TRX_METHOD_FW 1
+#define TRX_METHOD_CFW 2
+
+/* reward modes: RepairEnv.compute_reward_with_goal repair_env.py:244-291 */
+#define TRX_REWARD_DELTA 0
+#define TRX_REWARD_LOG_DELTA 1
+#define TRX_REWARD_NEG_TSTT 2
+#define TRX_REWARD_MINIMIZE_TSTT 3
+#define TRX_REWARD_REL_IMPROVE 4
+
+typedef struct trx_graph trx_graph;
+
+/* Env constants of RepairEnv.__init__ (repair_env.py:23-50). */
+typedef struct trx_params {
+    int32_t method;             /* TRX_METHOD_*                      assignment_method   */
+    int32_t iters;              /* K > 0                             assignment_iters    */
+    float bpr_alpha;            /* 0.15                              bpr_alpha           */
+    float bpr_beta;             /* 4.0                               bpr_beta            */
+    float capacity_damage;      /* 1e-3                              capacity_damage     */
+    float _pad0;
+    double unassigned_penalty;  /* 2e7 (yaml: 1e4)                   unassigned_penalty  */
+    int32_t reward_mode;        /* TRX_REWARD_*                      reward_mode         */
+    int32_t _pad1;
+    double reward_alpha, reward_beta, reward_gamma, reward_clip;
+} trx_params;
+
+/* Per-env state of B vectorised envs: device pointers, caller-owned.
+ * Mirrors RepairEnv attributes (repair_env.py:167-205):
+ *   flow          [B,E] f32  self.flow          (warm start in, result out)
+ *   capacity      [B,E] f32  self.capacities
+ *   damaged       [B,E] f32  self.is_damaged    (0/1)
+ *   goal          [B,E] f32  self.goal_mask     (0/1)
+ *   t             [B,E] f32  BPR(final flow)    (may be NULL)
+ *   tstt          [B]   f64  self.tstt
+ *   initial_tstt  [B]   f64  self.initial_tstt
+ *   unassigned    [B]   f64  self.unassigned_demand                          */
+typedef struct trx_state {
+    float* flow;
+    float* capacity;
+    float* damaged;
+    float* goal;
+    float* t;
+    double* tstt;
+    double* initial_tstt;
+    double* unassigned;
+} trx_state;
+
+/* ---------------------------------------------------------------- misc */
+int32_t trx_abi_version(void);
+const char* trx_last_error(void);
+
+/* ----------------------------------------------------------------- graph
+ * Replaces RepairEnv.__init__ array setup (repair_env.py:85-96, 106-109) over
+ * GraphData from src/data/tntp_parser.py:102-105.
+ *   src,dst   [E] 0-based node ids (file order = edge id order)
+ *   t0,cap0   [E] free-flow time, capacity (float32, like repair_env.py:89-91)
+ *   od_o,od_d,od_v [P] OD entries in dict order (0-based), demand > 0
+ * Fails (TRX_EUNSUP) on parallel links (scipy's csr_matrix would sum them)
+ * or on non-integral / >= 2^24 total demand (the exact fp32 AON contract). */
+int trx_graph_create(int32_t num_nodes, int32_t num_edges, const int32_t* src, const int32_t* dst,
+                     const float* t0, const float* cap0, int32_t num_od, const int32_t* od_o,
+                     const int32_t* od_d, const double* od_v, trx_graph** out);
+int trx_graph_destroy(trx_graph* g);
+/* num_nodes, num_edges, num_origins (zones with demand), total_demand */
+int trx_graph_info(const trx_graph* g, int32_t* num_nodes, int32_t* num_edges, int32_t* num_origins,
+                   double* total_demand);
+/* Device scratch bytes needed by trx_reset/step/assign for B envs. */
+int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs);
+
+/* ----------------------------------------------------------- hot path
+ * trx_assign: RepairEnv.compute_flow_assignment (repair_env.py:299-345) for
+ * every env b with env_mask[b] != 0 (env_mask NULL = all): warm start from
+ * state.flow, K iterations of BPR (667-677) -> all-or-nothing over every OD
+ * pair (scipy branch 481-503, 707-722) -> MSA/FW/CFW averaging (315-343),
+ * then TSTT (724-735).  Writes flow, t, tstt, unassigned.  Used by the
+ * greedy baseline's what-if batches (src/baselines/__init__.py:51-67). */
+int trx_assign(const trx_graph* g, const trx_params* p, int32_t num_envs, trx_state* s, const uint8_t* env_mask,
+               void* workspace, void* stream);
+
+/* trx_reset: RepairEnv.reset (repair_env.py:167-205) after damage sampling.
+ * The caller writes the sampled 0/1 mask into state.damaged (numpy PCG64
+ * sampling + strong-connectivity retries stay on the host, 168-192).  Sets
+ * capacity (cap0 or capacity_damage), goal = damaged, flow = 0, runs the
+ * assignment and sets tstt = initial_tstt.  env_mask as in trx_assign. */
+int trx_reset(const trx_graph* g, const trx_params* p, int32_t num_envs, trx_state* s, const uint8_t* env_mask,
+              void* workspace, void* stream);
+
+/* trx_step: RepairEnv.step (repair_env.py:207-237) for all B envs.
+ *   action [B] int32 edge ids; must be in [0,E) (the host checks the range
+ *   and raises ValueError, 208-209).  An already-repaired edge gives
+ *   reward -1, done 0 and no assignment (210-212); otherwise the edge is
+ *   repaired, the assignment runs, reward = compute_reward_with_goal
+ *   (220-230), done = is_goal_complete (236).
+ *   reward [B] f64, done [B] u8, valid [B] u8 (1 if an assignment ran). */
+int trx_step(const trx_graph* g, const trx_params* p, int32_t num_envs, trx_state* s, const int32_t* action,
+             double* reward, uint8_t* done, uint8_t* valid, void* workspace, void* stream);
+
+/* trx_observe: RepairEnv.get_state (repair_env.py:751-819) for B envs.
+ *   node_x [B,N,4] f32: betweenness of the active subgraph / its max,
+ *                      remaining goal ratio, avg undamaged flow norm, log10 tstt
+ *   edge_x [B,E,6] f32: t0_norm, cap_norm, clip(log1p(v/c)), damaged, goal, id/(E-1)
+ *   mask   [B,E]   f32: action_mask = damaged (may be NULL)                     */
+int trx_observe(const trx_graph* g, int32_t num_envs, const trx_state* s, float* node_x, float* edge_x,
+                float* mask, void* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRAFFICRL_H */

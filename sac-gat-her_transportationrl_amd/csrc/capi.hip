@@ -1,0 +1,278 @@
+// capi.hip -- C ABI of libtrafficrl.so (declared in include/trafficrl.h).
+//
+// Host-side runtime: validates inputs the way the reference raises, builds the
+// immutable device graph (scipy-ordered CSR, dense demand table, edge-id
+// table) once, and launches the stream-ordered gfx950 kernels.  No call but
+// trx_graph_create/destroy allocates or synchronises.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "trx_internal.h"
+
+using trx::DevGraph;
+
+struct trx_graph {
+    DevGraph dg;
+    int device;
+    std::vector<void*> allocs;
+};
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+template <typename T>
+int upload(trx_graph* g, const std::vector<T>& host, const T** out) {
+    void* d = nullptr;
+    size_t bytes = host.size() * sizeof(T);
+    if (bytes == 0) bytes = sizeof(T);
+    hipError_t e = hipMalloc(&d, bytes);
+    if (e != hipSuccess) return fail(TRX_EHIP, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    g->allocs.push_back(d);
+    if (!host.empty()) {
+        e = hipMemcpy(d, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return fail(TRX_EHIP, "hipMemcpy: %s", hipGetErrorString(e));
+    }
+    *out = static_cast<const T*>(d);
+    return TRX_OK;
+}
+
+int check_params(const trx_params* p) {
+    if (!p) return fail(TRX_EINVAL, "params is NULL");
+    if (p->iters <= 0) return fail(TRX_EINVAL, "assignment_iters must be > 0 to update TSTT.");  // repair_env.py:300-301
+    if (p->method < TRX_METHOD_MSA || p->method > TRX_METHOD_CFW)
+        return fail(TRX_EINVAL, "unsupported assignment_method %d", p->method);
+    if (p->reward_mode < TRX_REWARD_DELTA || p->reward_mode > TRX_REWARD_REL_IMPROVE)
+        return fail(TRX_EINVAL, "unsupported reward_mode %d", p->reward_mode);
+    return TRX_OK;
+}
+
+int check_state(const trx_state* s, bool need_initial) {
+    if (!s) return fail(TRX_EINVAL, "state is NULL");
+    if (!s->flow || !s->capacity || !s->damaged || !s->goal || !s->tstt || !s->unassigned)
+        return fail(TRX_EINVAL, "state has a NULL required buffer");
+    if (need_initial && !s->initial_tstt) return fail(TRX_EINVAL, "state.initial_tstt is NULL");
+    return TRX_OK;
+}
+
+int check_small(const trx_graph* g) {
+    if (!g) return fail(TRX_EINVAL, "graph is NULL");
+    if (g->dg.N > trx::kSmallMaxNodes)
+        return fail(TRX_EUNSUP, "graph has %d nodes; the register-resident kernel supports <= %d", g->dg.N,
+                    trx::kSmallMaxNodes);
+    return TRX_OK;
+}
+
+int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mode, const int32_t* action,
+        double* reward, uint8_t* done, uint8_t* valid, const uint8_t* env_mask, void* ws, void* stream) {
+    int rc;
+    if ((rc = check_small(g)) || (rc = check_params(p)) || (rc = check_state(s, mode != trx::kModeAssign))) return rc;
+    if (B < 0) return fail(TRX_EINVAL, "num_envs < 0");
+    if (B == 0) return TRX_OK;
+    if (!ws) return fail(TRX_EINVAL, "workspace is NULL (size it with trx_workspace_bytes)");
+    hipError_t e = hipSetDevice(g->device);
+    if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
+    e = trx::launch_env_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws,
+                               static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "kernel launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t trx_abi_version(void) { return TRX_ABI_VERSION; }
+
+const char* trx_last_error(void) { return g_err; }
+
+int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* dst, const float* t0,
+                     const float* cap0, int32_t P, const int32_t* od_o, const int32_t* od_d, const double* od_v,
+                     trx_graph** out) {
+    if (!out) return fail(TRX_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (N <= 0 || E < 0 || P < 0) return fail(TRX_EINVAL, "bad sizes N=%d E=%d P=%d", N, E, P);
+    if (E > 0 && (!src || !dst || !t0 || !cap0)) return fail(TRX_EINVAL, "NULL edge array");
+    if (P > 0 && (!od_o || !od_d || !od_v)) return fail(TRX_EINVAL, "NULL OD array");
+    if (N > trx::kSmallMaxNodes)
+        return fail(TRX_EUNSUP, "graph has %d nodes; this build supports <= %d (register-resident kernel)", N,
+                    trx::kSmallMaxNodes);
+    const int NP = N <= 8 ? 8 : N <= 16 ? 16 : N <= 24 ? 24 : 32;
+
+    std::vector<int16_t> eid_of((size_t)NP * NP, -1);
+    for (int e = 0; e < E; ++e) {
+        if (src[e] < 0 || src[e] >= N || dst[e] < 0 || dst[e] >= N)
+            return fail(TRX_EINVAL, "edge %d endpoint out of range", e);
+        if (!(t0[e] > 0.0f) || !std::isfinite(t0[e]))
+            return fail(TRX_EUNSUP, "edge %d has non-positive free-flow time %g", e, (double)t0[e]);
+        int16_t& slot = eid_of[(size_t)src[e] * NP + dst[e]];
+        if (slot >= 0) return fail(TRX_EUNSUP, "parallel links %d->%d (scipy csr_matrix would sum them)", src[e], dst[e]);
+        slot = (int16_t)e;
+    }
+    // scipy CSR: rows by source, columns ascending
+    std::vector<int32_t> indptr(N + 1, 0), indices, csr_eid;
+    for (int u = 0; u < N; ++u) {
+        for (int v = 0; v < N; ++v) {
+            int e = eid_of[(size_t)u * NP + v];
+            if (e >= 0) {
+                indices.push_back(v);
+                csr_eid.push_back(e);
+            }
+        }
+        indptr[u + 1] = (int32_t)indices.size();
+    }
+    // origins = nodes with at least one OD entry (repair_env.py:490-493)
+    std::vector<int> has(N, 0);
+    double total = 0.0;
+    for (int k = 0; k < P; ++k) {
+        if (od_o[k] < 0 || od_o[k] >= N || od_d[k] < 0 || od_d[k] >= N)
+            return fail(TRX_EINVAL, "OD entry %d out of range", k);
+        double v = od_v[k];
+        if (!(v > 0.0) || v != std::floor(v))
+            return fail(TRX_EUNSUP, "OD demand %g is not a positive integer (exact fp32 AON contract)", v);
+        has[od_o[k]] = 1;
+        total += v;
+    }
+    if (total >= 16777216.0) return fail(TRX_EUNSUP, "total demand %g >= 2^24 (exact fp32 AON contract)", total);
+    std::vector<int32_t> origins;
+    std::vector<int> zone_of(N, -1);
+    for (int u = 0; u < N; ++u)
+        if (has[u]) {
+            zone_of[u] = (int)origins.size();
+            origins.push_back(u);
+        }
+    const int Z = (int)origins.size();
+    if (Z == 0) return fail(TRX_EUNSUP, "no OD demand");
+    std::vector<float> dem((size_t)Z * N, 0.0f);
+    for (int k = 0; k < P; ++k) dem[(size_t)zone_of[od_o[k]] * N + od_d[k]] = (float)od_v[k];
+    // networkx node insertion order (repair_env.py:106-109)
+    std::vector<int32_t> nx_order;
+    std::vector<int> seen(N, 0);
+    for (int e = 0; e < E; ++e)
+        for (int n : {src[e], dst[e]})
+            if (!seen[n]) {
+                seen[n] = 1;
+                nx_order.push_back(n);
+            }
+    for (int n = 0; n < N; ++n)
+        if (!seen[n]) nx_order.push_back(n);
+    // adjacency views for the observation kernel
+    std::vector<int32_t> out_ptr(N + 1, 0), out_dst, out_eid, in_ptr(N + 1, 0), in_src, in_eid;
+    for (int u = 0; u < N; ++u) {
+        for (int e = 0; e < E; ++e)
+            if (src[e] == u) {
+                out_dst.push_back(dst[e]);
+                out_eid.push_back(e);
+            }
+        out_ptr[u + 1] = (int32_t)out_dst.size();
+        for (int e = 0; e < E; ++e)
+            if (dst[e] == u) {
+                in_src.push_back(src[e]);
+                in_eid.push_back(e);
+            }
+        in_ptr[u + 1] = (int32_t)in_src.size();
+    }
+
+    trx_graph* g = new trx_graph();
+    hipError_t he = hipGetDevice(&g->device);
+    if (he != hipSuccess) {
+        delete g;
+        return fail(TRX_EHIP, "hipGetDevice: %s", hipGetErrorString(he));
+    }
+    DevGraph& d = g->dg;
+    d.N = N;
+    d.E = E;
+    d.Z = Z;
+    d.NP = NP;
+    d.total_demand = total;
+    float mt = 0.f, mc = 0.f;
+    for (int e = 0; e < E; ++e) {
+        mt = std::max(mt, t0[e]);
+        mc = std::max(mc, cap0[e]);
+    }
+    d.max_t0 = E > 0 ? mt : 1.0f;
+    d.max_cap = E > 0 ? mc : 1.0f;
+    int rc = TRX_OK;
+    std::vector<int32_t> vsrc(src, src + E), vdst(dst, dst + E);
+    std::vector<float> vt0(t0, t0 + E), vcap(cap0, cap0 + E);
+    if ((rc = upload(g, vsrc, &d.src)) || (rc = upload(g, vdst, &d.dst)) || (rc = upload(g, vt0, &d.t0)) ||
+        (rc = upload(g, vcap, &d.cap0)) || (rc = upload(g, indptr, &d.indptr)) ||
+        (rc = upload(g, indices, &d.indices)) || (rc = upload(g, csr_eid, &d.csr_eid)) ||
+        (rc = upload(g, eid_of, &d.eid_of)) || (rc = upload(g, dem, &d.dem)) ||
+        (rc = upload(g, origins, &d.origins)) || (rc = upload(g, nx_order, &d.nx_order)) ||
+        (rc = upload(g, out_ptr, &d.out_ptr)) || (rc = upload(g, out_dst, &d.out_dst)) ||
+        (rc = upload(g, out_eid, &d.out_eid)) || (rc = upload(g, in_ptr, &d.in_ptr)) ||
+        (rc = upload(g, in_src, &d.in_src)) || (rc = upload(g, in_eid, &d.in_eid))) {
+        trx_graph_destroy(g);
+        return rc;
+    }
+    *out = g;
+    return TRX_OK;
+}
+
+int trx_graph_destroy(trx_graph* g) {
+    if (!g) return TRX_OK;
+    for (void* p : g->allocs) (void)hipFree(p);
+    delete g;
+    return TRX_OK;
+}
+
+int trx_graph_info(const trx_graph* g, int32_t* num_nodes, int32_t* num_edges, int32_t* num_origins,
+                   double* total_demand) {
+    if (!g) return fail(TRX_EINVAL, "graph is NULL");
+    if (num_nodes) *num_nodes = g->dg.N;
+    if (num_edges) *num_edges = g->dg.E;
+    if (num_origins) *num_origins = g->dg.Z;
+    if (total_demand) *total_demand = g->dg.total_demand;
+    return TRX_OK;
+}
+
+int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs) {
+    if (!g || num_envs < 0) return fail(TRX_EINVAL, "bad arguments");
+    return (int64_t)trx::small_workspace_bytes(g->dg, num_envs) + 256;
+}
+
+int trx_assign(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, const uint8_t* env_mask, void* ws,
+               void* stream) {
+    return run(g, p, B, s, trx::kModeAssign, nullptr, nullptr, nullptr, nullptr, env_mask, ws, stream);
+}
+
+int trx_reset(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, const uint8_t* env_mask, void* ws,
+              void* stream) {
+    return run(g, p, B, s, trx::kModeReset, nullptr, nullptr, nullptr, nullptr, env_mask, ws, stream);
+}
+
+int trx_step(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, const int32_t* action,
+             double* reward, uint8_t* done, uint8_t* valid, void* ws, void* stream) {
+    if (!action || !reward || !done || !valid) return fail(TRX_EINVAL, "step output/action buffer is NULL");
+    return run(g, p, B, s, trx::kModeStep, action, reward, done, valid, nullptr, ws, stream);
+}
+
+int trx_observe(const trx_graph* g, int32_t B, const trx_state* s, float* node_x, float* edge_x, float* mask,
+                void* ws, void* stream) {
+    (void)ws;
+    int rc;
+    if ((rc = check_small(g)) || (rc = check_state(s, false))) return rc;
+    if (!node_x || !edge_x) return fail(TRX_EINVAL, "observation buffers are NULL");
+    if (B <= 0) return B == 0 ? TRX_OK : fail(TRX_EINVAL, "num_envs < 0");
+    hipError_t e = hipSetDevice(g->device);
+    if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
+    e = trx::launch_observe_kernel(g->dg, B, *s, node_x, edge_x, mask, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "observe launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+}  // extern "C"

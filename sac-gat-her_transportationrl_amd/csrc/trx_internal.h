@@ -1,0 +1,67 @@
+// trx_internal.h -- shared declarations between the C-ABI host code and the
+// gfx950 kernels of libtrafficrl.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/trafficrl.h"
+
+namespace trx {
+
+// Largest node count handled by the register-resident small-graph kernel
+// (dist labels live in VGPRs, one lane per (env, origin) SSSP).
+constexpr int kSmallMaxNodes = 32;
+
+// Device-resident, immutable graph description (built by trx_graph_create).
+struct DevGraph {
+    int N, E, Z, NP;            // nodes, edges, origins (zones with demand), padded nodes
+    const int32_t* src;         // [E]
+    const int32_t* dst;         // [E]
+    const float* t0;            // [E]
+    const float* cap0;          // [E]
+    const int32_t* indptr;      // [N+1]  CSR rows sorted by column (scipy order)
+    const int32_t* indices;     // [E]
+    const int32_t* csr_eid;     // [E]
+    const int16_t* eid_of;      // [NP*NP] (u,v) -> edge id, -1 = no edge
+    const float* dem;           // [Z*N]  demand origin zone zi -> node v (fp32, exact ints)
+    const int32_t* origins;     // [Z]    node id of origin zone zi
+    const int32_t* nx_order;    // [N]    networkx node insertion order (observation)
+    const int32_t* out_ptr;     // [N+1]  successors in networkx adjacency (file) order
+    const int32_t* out_dst;     // [E]
+    const int32_t* out_eid;     // [E]
+    const int32_t* in_ptr;      // [N+1]  predecessors (any order: distinct tails)
+    const int32_t* in_src;      // [E]
+    const int32_t* in_eid;      // [E]
+    double total_demand;        // float(np.sum(list(od_demand.values())))
+    float max_t0, max_cap;      // RepairEnv.max_t0 / max_capacity
+};
+
+// Per-lane Fibonacci-heap state for the exact (scipy-order) SSSP fallback.
+struct FibLane {
+    double val[kSmallMaxNodes];
+    int8_t parent[kSmallMaxNodes], left[kSmallMaxNodes], right[kSmallMaxNodes], child[kSmallMaxNodes];
+    uint8_t rank[kSmallMaxNodes], state[kSmallMaxNodes];
+    int8_t roots[32];
+};
+
+enum RunMode { kModeAssign = 0, kModeReset = 1, kModeStep = 2 };
+
+struct LaunchCfg {
+    int np;        // template node padding
+    int epw;       // envs per workgroup
+    int threads;   // block size
+    size_t smem;   // dynamic LDS bytes
+    int blocks;    // grid
+};
+
+LaunchCfg small_launch_cfg(const DevGraph& g, int num_envs);
+size_t small_workspace_bytes(const DevGraph& g, int num_envs);
+
+hipError_t launch_env_kernel(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
+                             const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                             const uint8_t* env_mask, void* workspace, hipStream_t stream);
+
+hipError_t launch_observe_kernel(const DevGraph& g, int num_envs, const trx_state& s, float* node_x, float* edge_x,
+                                 float* mask, hipStream_t stream);
+
+}  // namespace trx

@@ -1,0 +1,102 @@
+"""ctypes binding of libtrafficrl.so (C ABI: include/trafficrl.h).
+
+This is the binding the reference side would add: plain
+pointers and sizes, torch tensors passed by data_ptr(), the current HIP stream
+passed as a void*.  There is no CPU fallback: if the library is missing or no
+HIP device is present, the env raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
+
+TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
+METHODS = {"msa": 0, "fw": 1, "cfw": 2}
+REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
+
+# Every symbol include/trafficrl.h declares (tests check the export table).
+EXPORTS = (
+    "trx_abi_version", "trx_last_error", "trx_graph_create", "trx_graph_destroy", "trx_graph_info",
+    "trx_workspace_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe",
+)
+
+
+class TrxParams(ctypes.Structure):
+    _fields_ = [
+        ("method", ctypes.c_int32), ("iters", ctypes.c_int32),
+        ("bpr_alpha", ctypes.c_float), ("bpr_beta", ctypes.c_float),
+        ("capacity_damage", ctypes.c_float), ("_pad0", ctypes.c_float),
+        ("unassigned_penalty", ctypes.c_double),
+        ("reward_mode", ctypes.c_int32), ("_pad1", ctypes.c_int32),
+        ("reward_alpha", ctypes.c_double), ("reward_beta", ctypes.c_double),
+        ("reward_gamma", ctypes.c_double), ("reward_clip", ctypes.c_double),
+    ]
+
+
+class TrxState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ("flow", "capacity", "damaged", "goal", "t", "tstt", "initial_tstt", "unassigned")]
+
+
+_vp = ctypes.c_void_p
+_lib = None
+
+
+class TrafficRLError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libtrafficrl.so (importing torch first so both share one HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- torch's libamdhip64.so.7 must be the one resolved
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is not built. Build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    L.trx_abi_version.restype = ctypes.c_int32
+    L.trx_last_error.restype = ctypes.c_char_p
+    L.trx_graph_create.argtypes = [ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp,
+                                   ctypes.POINTER(_vp)]
+    L.trx_graph_destroy.argtypes = [_vp]
+    L.trx_graph_info.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                 ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
+    L.trx_workspace_bytes.argtypes = [_vp, ctypes.c_int32]
+    L.trx_workspace_bytes.restype = ctypes.c_int64
+    L.trx_assign.argtypes = [_vp, ctypes.POINTER(TrxParams), ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp]
+    L.trx_reset.argtypes = [_vp, ctypes.POINTER(TrxParams), ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp]
+    L.trx_step.argtypes = [_vp, ctypes.POINTER(TrxParams), ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp,
+                           _vp, _vp, _vp]
+    L.trx_observe.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp, _vp, _vp]
+    for name in ("trx_graph_create", "trx_graph_destroy", "trx_graph_info", "trx_assign", "trx_reset", "trx_step",
+                 "trx_observe"):
+        getattr(L, name).restype = ctypes.c_int
+    if L.trx_abi_version() != 1:
+        raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != 1")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    """Map C return codes to the reference's exception types."""
+    if rc == TRX_OK:
+        return
+    msg = load().trx_last_error().decode(errors="replace")
+    if rc == TRX_EINVAL:
+        raise ValueError(f"{what}: {msg}")
+    raise TrafficRLError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def stream_ptr(device=None) -> ctypes.c_void_p:
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

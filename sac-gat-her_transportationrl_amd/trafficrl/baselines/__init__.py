@@ -1,0 +1,159 @@
+"""Baseline repair policies (src/baselines/__init__.py:11-113).
+
+The greedy one-step policy (35-69) runs one warm-started assignment per
+damaged candidate; here all candidates are ONE batched trx_assign launch
+(candidate rows of a what-if batch) instead of 22 serial assignments.  The
+choice rule is the reference's: first candidate (in link order) with the
+strictly smallest TSTT.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List
+
+import numpy as np
+import torch
+
+from ..env.repair_env import EnvState, RepairEnv
+from ..env.vec_env import VecRepairEnv
+
+
+def select_random(state: EnvState) -> int:
+    candidates = np.where(state.action_mask > 0)[0]
+    return int(np.random.choice(candidates))
+
+
+def select_max_vc(state: EnvState) -> int:
+    return int(np.argmax(state.edge_features[:, 2] * state.action_mask))
+
+
+def select_max_flow(state: EnvState) -> int:
+    return int(np.argmax(state.edge_features[:, 2] * state.edge_features[:, 1] * state.action_mask))
+
+
+def select_max_betweenness(state: EnvState, node_betweenness: np.ndarray, edge_index: np.ndarray) -> int:
+    src, dst = edge_index
+    edge_bw = (node_betweenness[src] + node_betweenness[dst]) / 2.0
+    return int(np.argmax(edge_bw * state.action_mask))
+
+
+class WhatIfBatch:
+    """Reusable device batch of what-if rows sharing one graph."""
+
+    def __init__(self, graph, params, device, rows: int):
+        self.rows = 0
+        self.graph, self.params, self.device = graph, params, device
+        self._vec = None
+        self.ensure(rows)
+
+    def ensure(self, rows: int):
+        if self._vec is not None and rows <= self.rows:
+            return
+        self.rows = max(rows, 1)
+        # shares the graph handle and params; only state tensors are allocated
+        v = VecRepairEnv(self.graph.graph_data, self.rows, device=self.device, graph=self.graph, reset=False,
+                         assignment_iters=self.params.iters,
+                         assignment_method={0: "msa", 1: "fw", 2: "cfw"}[self.params.method])
+        v.params = self.params
+        self._vec = v
+
+    def tstt(self, cap: torch.Tensor, dmg: torch.Tensor, flow: torch.Tensor) -> torch.Tensor:
+        """Run warm-started assignments for rows [R,E]; return tstt[R] (f64)."""
+        R = cap.shape[0]
+        self.ensure(R)
+        v = self._vec
+        v.capacity[:R].copy_(cap)
+        v.damaged[:R].copy_(dmg)
+        v.flow[:R].copy_(flow)
+        mask = torch.zeros(v.num_envs, dtype=torch.uint8, device=v.device)
+        mask[:R] = 1
+        v.assign(mask)
+        return v.tstt[:R]
+
+
+_batches: Dict[int, WhatIfBatch] = {}
+
+
+def select_greedy_one_step(env: RepairEnv, state: EnvState) -> int:
+    candidates = np.where(state.action_mask > 0)[0]
+    if candidates.size == 0:
+        return int(np.argmax(state.action_mask))
+    candidates = candidates[env.is_damaged[candidates] != 0]
+    if candidates.size == 0:
+        return int(np.where(state.action_mask > 0)[0][0])
+    dev = env.device
+    D = candidates.size
+    cap = torch.from_numpy(np.repeat(env.capacities[None], D, 0)).to(dev)
+    dmg = torch.from_numpy(np.repeat(env.is_damaged[None], D, 0)).to(dev)
+    flow = torch.from_numpy(np.repeat(env.flow[None], D, 0)).to(dev)
+    idx = torch.arange(D, device=dev)
+    cand = torch.from_numpy(candidates).to(dev)
+    cap[idx, cand] = torch.from_numpy(env.initial_capacities[candidates]).to(dev)
+    dmg[idx, cand] = 0.0
+    key = id(env)
+    wb = _batches.get(key)
+    if wb is None or wb.graph is not env.graph:
+        wb = _batches[key] = WhatIfBatch(env.graph, env._vec.params, dev, max(D, 32))
+    ts = wb.tstt(cap, dmg, flow).cpu().numpy()
+    return int(candidates[int(np.argmin(ts))])  # first strict minimum, like `if env.tstt < best_tstt`
+
+
+def greedy_actions(venv: VecRepairEnv, batch: WhatIfBatch | None = None) -> torch.Tensor:
+    """Greedy one-step action for every env of a VecRepairEnv at once: B x E
+    what-if rows (non-damaged links masked out) in one trx_assign launch."""
+    B, E = venv.num_envs, venv.num_edges
+    dev = venv.device
+    rows = B * E
+    if batch is None:
+        batch = WhatIfBatch(venv.graph, venv.params, dev, rows)
+    eye = torch.eye(E, device=dev, dtype=torch.bool)
+    cap = venv.capacity[:, None, :].expand(B, E, E).clone()
+    dmg = venv.damaged[:, None, :].expand(B, E, E).clone()
+    cap0 = torch.as_tensor(venv.graph.cap0, device=dev)
+    cap = torch.where(eye[None], cap0[None, None, :].expand(B, E, E), cap)
+    dmg = torch.where(eye[None], torch.zeros((), device=dev), dmg)
+    flow = venv.flow[:, None, :].expand(B, E, E).reshape(rows, E)
+    cand = venv.damaged > 0  # [B,E]
+    batch.ensure(rows)
+    v = batch._vec
+    v.capacity[:rows].copy_(cap.reshape(rows, E))
+    v.damaged[:rows].copy_(dmg.reshape(rows, E))
+    v.flow[:rows].copy_(flow)
+    mask = torch.zeros(v.num_envs, dtype=torch.uint8, device=dev)
+    mask[:rows] = cand.reshape(-1).to(torch.uint8)
+    v.assign(mask)
+    ts = torch.where(cand, v.tstt[:rows].view(B, E), torch.full((), float("inf"), dtype=torch.float64, device=dev))
+    return torch.argmin(ts, dim=1).to(torch.int32)  # first minimum in link order
+
+
+def run_episode(env: RepairEnv, policy: Callable[[EnvState], int], reward_scale: float = 1.0,
+                max_steps: int = 0) -> Dict:
+    tstt_curve: List[float] = []
+    state = env.reset()
+    done = False
+    steps = 0
+    total_reward = 0.0
+    while not done:
+        action = policy(state)
+        state, reward, done, info = env.step(action)
+        total_reward += reward * reward_scale
+        tstt_curve.append(info.get("tstt", env.tstt))
+        steps += 1
+        if max_steps > 0 and steps >= max_steps and not done:
+            break
+    tstt_last = float(tstt_curve[-1]) if tstt_curve else env.tstt
+    tstt_mean = float(np.mean(tstt_curve)) if tstt_curve else env.tstt
+    tstt_auc = float(np.trapezoid(tstt_curve)) if tstt_curve else env.tstt
+    return {"tstt_curve": tstt_curve, "reward": total_reward, "tstt_last": tstt_last, "tstt_mean": tstt_mean,
+            "tstt_auc": tstt_auc, "auc": tstt_auc}
+
+
+def get_baseline_policies(env: RepairEnv) -> Dict[str, Callable[[EnvState], int]]:
+    node_bw = env.betweenness_vec
+    edge_index = env.edge_index
+    return {
+        "random": select_random,
+        "max_vc": select_max_vc,
+        "max_flow": select_max_flow,
+        "max_betweenness": lambda s: select_max_betweenness(s, node_bw, edge_index),
+        "greedy": lambda s: select_greedy_one_step(env, s),
+    }

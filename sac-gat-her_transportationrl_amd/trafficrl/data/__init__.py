@@ -1,0 +1,1 @@
+from .tntp_parser import EdgeData, GraphData, load_graph_data, parse_net_tntp, parse_trips_tntp, sioux_falls  # noqa: F401

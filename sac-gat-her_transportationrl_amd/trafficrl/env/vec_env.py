@@ -1,0 +1,189 @@
+"""VecRepairEnv: B Sioux-Falls-sized repair envs stepping in lockstep on one
+MI355X.  The batched form of RepairEnv (src/env/repair_env.py:22-819).
+
+State lives in device tensors (structure of arrays, [B, E] row-major, float32
+per link, float64 per env), every hot operation is one gfx950 kernel launch
+through libtrafficrl.so:
+
+  reset   -> trx_reset    (repair_env.py:167-205, damage draw on the host RNG)
+  step    -> trx_step     (repair_env.py:207-237, assignment fused in)
+  observe -> trx_observe  (repair_env.py:751-819)
+  assign  -> trx_assign   (repair_env.py:299-345, what-if batches)
+
+Nothing here falls back to the CPU: without libtrafficrl.so or a HIP device
+the constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _lib
+from ..graph import DamageSampler, TrafficGraph
+
+
+@dataclass
+class VecObs:
+    node_x: torch.Tensor     # [B, N, 4]
+    edge_x: torch.Tensor     # [B, E, 6]
+    action_mask: torch.Tensor  # [B, E]
+    log_tstt: torch.Tensor   # [B] float64
+
+
+class VecRepairEnv:
+    def __init__(
+        self,
+        graph_data,
+        num_envs: int,
+        device="cuda",
+        damaged_ratio: float = 0.3,
+        bpr_alpha: float = 0.15,
+        bpr_beta: float = 4.0,
+        assignment_iters: int = 20,
+        assignment_method: str = "msa",
+        reward_mode: str = "log_delta",
+        reward_alpha: float = 1.0,
+        reward_beta: float = 10.0,
+        reward_gamma: float = 0.1,
+        reward_clip: float = 0.0,
+        capacity_damage: float = 1e-3,
+        unassigned_penalty: float = 2e7,
+        fixed_damage: bool = False,
+        fixed_damage_seed: Optional[int] = None,
+        seed: int = 0,
+        seeds: Optional[Sequence[int]] = None,
+        graph: Optional[TrafficGraph] = None,
+        reset: bool = True,
+    ):
+        if assignment_method.lower() not in _lib.METHODS:
+            raise ValueError(f"assignment_method {assignment_method!r} not supported (msa, fw, cfw)")
+        if int(assignment_iters) <= 0:
+            raise ValueError("assignment_iters must be > 0 to update TSTT.")
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("VecRepairEnv runs on a HIP device only (device='cuda[:i]')")
+        torch.cuda.set_device(self.device)
+        self.graph = graph if graph is not None else TrafficGraph(graph_data, self.device)
+        self.graph_data = self.graph.graph_data
+        self.num_envs = B = int(num_envs)
+        self.num_nodes = N = self.graph.num_nodes
+        self.num_edges = E = self.graph.num_edges
+        self.damaged_ratio = damaged_ratio
+        self.assignment_method = assignment_method.lower()
+        self.assignment_iters = int(assignment_iters)
+        self.reward_mode = reward_mode
+        self.params = _lib.TrxParams(
+            method=_lib.METHODS[self.assignment_method], iters=self.assignment_iters, bpr_alpha=bpr_alpha,
+            bpr_beta=bpr_beta, capacity_damage=capacity_damage, unassigned_penalty=unassigned_penalty,
+            reward_mode=_lib.REWARD_MODES[reward_mode], reward_alpha=reward_alpha, reward_beta=reward_beta,
+            reward_gamma=reward_gamma, reward_clip=reward_clip)
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.flow = torch.zeros(B, E, **f32)
+        self.capacity = torch.zeros(B, E, **f32)
+        self.damaged = torch.zeros(B, E, **f32)
+        self.goal = torch.zeros(B, E, **f32)
+        self.t = torch.zeros(B, E, **f32)
+        self.tstt = torch.zeros(B, **f64)
+        self.initial_tstt = torch.zeros(B, **f64)
+        self.unassigned = torch.zeros(B, **f64)
+        self.reward = torch.zeros(B, **f64)
+        self.done = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.valid = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self._obs_bufs = None
+        self.workspace = torch.empty(self.graph.workspace_bytes(B), dtype=torch.uint8, device=dev)
+        self._state = _lib.TrxState(
+            flow=self.flow.data_ptr(), capacity=self.capacity.data_ptr(), damaged=self.damaged.data_ptr(),
+            goal=self.goal.data_ptr(), t=self.t.data_ptr(), tstt=self.tstt.data_ptr(),
+            initial_tstt=self.initial_tstt.data_ptr(), unassigned=self.unassigned.data_ptr())
+        self.edge_index = torch.as_tensor(self.graph.edge_index, device=dev)
+        self._seeds = list(seeds) if seeds is not None else [seed + i for i in range(B)]
+        self._fixed = (fixed_damage, fixed_damage_seed)
+        self._samplers = None
+        if reset:
+            self.reset()
+
+    @property
+    def samplers(self):
+        if self._samplers is None:
+            fd, fds = self._fixed
+            self._samplers = [DamageSampler(self.graph, int(s), fd, fds) for s in self._seeds]
+        return self._samplers
+
+    def _obs_buffers(self):
+        if self._obs_bufs is None:
+            B, N, E = self.num_envs, self.num_nodes, self.num_edges
+            f32 = dict(dtype=torch.float32, device=self.device)
+            self._obs_bufs = (torch.zeros(B, N, 4, **f32), torch.zeros(B, E, 6, **f32), torch.zeros(B, E, **f32))
+        return self._obs_bufs
+
+    # ------------------------------------------------------------ kernels
+    def _stream(self):
+        return _lib.stream_ptr(self.device)
+
+    def assign(self, env_mask: Optional[torch.Tensor] = None):
+        """compute_flow_assignment for the envs in env_mask (uint8 [B]); warm
+        start from self.flow with the current capacities/damage."""
+        L = _lib.load()
+        m = None if env_mask is None else env_mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        _lib.check(L.trx_assign(self.graph.handle, ctypes.byref(self.params), self.num_envs, ctypes.byref(self._state),
+                                _lib.ptr(m), _lib.ptr(self.workspace), self._stream()), "trx_assign")
+
+    def reset(self, env_ids=None, damaged: Optional[torch.Tensor] = None, damaged_ratio: Optional[float] = None,
+              observe: bool = True):
+        """Reset all envs (or env_ids).  Damage masks come from each env's
+        host RNG unless `damaged` [B,E] (or [len(env_ids),E]) is given."""
+        ratio = self.damaged_ratio if damaged_ratio is None else damaged_ratio
+        B = self.num_envs
+        ids = list(range(B)) if env_ids is None else [int(i) for i in (env_ids.tolist() if torch.is_tensor(env_ids)
+                                                                       else env_ids)]
+        if damaged is None:
+            masks = np.stack([self.samplers[i].sample(ratio) for i in ids])
+            damaged = torch.from_numpy(masks)
+        damaged = damaged.to(device=self.device, dtype=torch.float32)
+        env_mask = None
+        if env_ids is None:
+            self.damaged.copy_(damaged)
+        else:
+            idx = torch.as_tensor(ids, device=self.device, dtype=torch.long)
+            self.damaged.index_copy_(0, idx, damaged)
+            env_mask = torch.zeros(B, dtype=torch.uint8, device=self.device)
+            env_mask[idx] = 1
+        L = _lib.load()
+        _lib.check(L.trx_reset(self.graph.handle, ctypes.byref(self.params), B, ctypes.byref(self._state),
+                               _lib.ptr(env_mask), _lib.ptr(self.workspace), self._stream()), "trx_reset")
+        return self.observe() if observe else None
+
+    def step(self, actions: torch.Tensor, observe: bool = True, check: bool = True):
+        """Batched RepairEnv.step.  Returns (obs, reward[B] f64, done[B] bool, info)."""
+        a = actions.to(device=self.device, dtype=torch.int32).contiguous()
+        if a.numel() != self.num_envs:
+            raise ValueError(f"expected {self.num_envs} actions, got {a.numel()}")
+        if check:
+            lo, hi = int(a.min()), int(a.max())
+            if lo < 0 or hi >= self.num_edges:
+                bad = lo if lo < 0 else hi
+                raise ValueError(f"action_edge_id {bad} out of range (0..{self.num_edges - 1})")
+        L = _lib.load()
+        _lib.check(L.trx_step(self.graph.handle, ctypes.byref(self.params), self.num_envs, ctypes.byref(self._state),
+                              _lib.ptr(a), _lib.ptr(self.reward), _lib.ptr(self.done), _lib.ptr(self.valid),
+                              _lib.ptr(self.workspace), self._stream()), "trx_step")
+        obs = self.observe() if observe else None
+        return obs, self.reward, self.done.bool(), {"tstt": self.tstt, "valid": self.valid.bool()}
+
+    def observe(self) -> VecObs:
+        L = _lib.load()
+        node_x, edge_x, mask = self._obs_buffers()
+        _lib.check(L.trx_observe(self.graph.handle, self.num_envs, ctypes.byref(self._state), _lib.ptr(node_x),
+                                 _lib.ptr(edge_x), _lib.ptr(mask), _lib.ptr(self.workspace), self._stream()),
+                   "trx_observe")
+        log_tstt = torch.log10(torch.clamp(self.tstt, min=1.0))
+        return VecObs(node_x, edge_x, mask, log_tstt)
+
+    def is_goal_complete(self) -> torch.Tensor:
+        return (self.goal * self.damaged).sum(dim=1) == 0
