@@ -63,9 +63,14 @@ class VecRepairEnv:
             raise ValueError(f"assignment_method {assignment_method!r} not supported (msa, fw, cfw)")
         if int(assignment_iters) <= 0:
             raise ValueError("assignment_iters must be > 0 to update TSTT.")
-        self.device = torch.device(device)
-        if self.device.type != "cuda":
+        dev = torch.device(device)
+        if dev.type != "cuda":
             raise RuntimeError("VecRepairEnv runs on a HIP device only (device='cuda[:i]')")
+        if not torch.cuda.is_available():
+            raise RuntimeError("VecRepairEnv needs a HIP device (MI355X); there is no CPU fallback")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         torch.cuda.set_device(self.device)
         self.graph = graph if graph is not None else TrafficGraph(graph_data, self.device)
         self.graph_data = self.graph.graph_data
