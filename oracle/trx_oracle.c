@@ -111,8 +111,10 @@ void orc_bpr(int E, const float* flow, const float* cap, const float* t0, const 
         if (beta == 4.0f) {
             double v = (double)vc, v2 = v * v;
             p = (float)(v2 * v2);
-        } else {
-            p = (float)pow((double)vc, (double)beta);
+        } else {  /* integer beta: left-to-right float64 product (same as the HIP kernel) */
+            double v = (double)vc, acc = 1.0;
+            for (int i = 0; i < (int)beta; i++) acc = acc * v;
+            p = (float)acc;
         }
         float a = alpha * p;
         float s = 1.0f + a;

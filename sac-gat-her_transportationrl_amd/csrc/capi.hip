@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -55,6 +56,9 @@ int check_params(const trx_params* p) {
     if (p->iters <= 0) return fail(TRX_EINVAL, "assignment_iters must be > 0 to update TSTT.");  // repair_env.py:300-301
     if (p->method < TRX_METHOD_MSA || p->method > TRX_METHOD_CFW)
         return fail(TRX_EINVAL, "unsupported assignment_method %d", p->method);
+    if (!(p->bpr_beta >= 0.0f && p->bpr_beta <= 16.0f) || p->bpr_beta != std::floor(p->bpr_beta))
+        return fail(TRX_EUNSUP, "bpr_beta %g: only integer BPR powers 0..16 are supported (the reference uses 4)",
+                    (double)p->bpr_beta);
     if (p->reward_mode < TRX_REWARD_DELTA || p->reward_mode > TRX_REWARD_REL_IMPROVE)
         return fail(TRX_EINVAL, "unsupported reward_mode %d", p->reward_mode);
     return TRX_OK;
@@ -85,8 +89,16 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
     if (!ws) return fail(TRX_EINVAL, "workspace is NULL (size it with trx_workspace_bytes)");
     hipError_t e = hipSetDevice(g->device);
     if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
-    e = trx::launch_env_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws,
-                               static_cast<hipStream_t>(stream));
+    static const bool use_lane_kernel = [] {
+        const char* k = getenv("TRX_KERNEL");
+        return k && strcmp(k, "lane") == 0;
+    }();
+    if (use_lane_kernel)  // v1: one lane per shortest-path tree (kept for A/B)
+        e = trx::launch_env_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws,
+                                   static_cast<hipStream_t>(stream));
+    else  // v2: one quad of lanes per tree
+        e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
+                                        static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }

@@ -1,0 +1,268 @@
+// device_common.h -- device helpers shared by the gfx950 env kernels:
+// BPR cost, numpy pairwise float32 sum, the exact scipy Fibonacci-heap SSSP
+// replay, and the reward formula.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "trx_internal.h"
+
+namespace trx {
+namespace {  // internal linkage: each kernel TU gets its own copy
+
+constexpr float kInfF = __builtin_huge_valf();
+constexpr double kInfD = __builtin_huge_val();
+constexpr uint8_t kNoPred = 0xFF;
+
+__device__ __forceinline__ float bpr_cost(float flow, float cap, float t0, float dmg, float alpha, float beta) {
+    // repair_env.py:670-677
+    const float floor6 = 1e-6f;
+    float c = cap > floor6 ? cap : floor6;
+    float vc = __fdiv_rn(flow, c);
+    vc = vc < 0.0f ? 0.0f : (vc > 10.0f ? 10.0f : vc);
+    float pw;
+    if (beta == 4.0f) {
+        double v = (double)vc;
+        double v2 = __dmul_rn(v, v);
+        pw = (float)__dmul_rn(v2, v2);
+    } else {  // integer beta (checked by the host): left-to-right float64 product
+        double v = (double)vc, acc = 1.0;
+        const int n = (int)beta;
+        for (int i = 0; i < n; ++i) acc = __dmul_rn(acc, v);
+        pw = (float)acc;
+    }
+    float t = __fmul_rn(t0, __fadd_rn(1.0f, __fmul_rn(alpha, pw)));
+    return dmg > 0.5f ? 1e6f : t;
+}
+
+// numpy pairwise_sum (float32) over a[0..n) with stride-1 LDS reads.
+__device__ float pairwise_block(const float* a, int n) {
+    if (n < 8) {
+        float r = 0.0f;
+        for (int i = 0; i < n; ++i) r = __fadd_rn(r, a[i]);
+        return r;
+    }
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], a[i + j]);
+    }
+    float res = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                          __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+    for (; i < n; ++i) res = __fadd_rn(res, a[i]);
+    return res;
+}
+
+// numpy's recursive pairwise_sum for n > 128, unrolled to a fixed depth
+// (n <= 128 * 2^D); no stack arrays, so it costs no VGPRs for the kernel.
+template <int D>
+__device__ __forceinline__ float pairwise_rec(const float* a, int n) {
+    if constexpr (D == 0) {
+        return pairwise_block(a, n);
+    } else {
+        if (n <= 128) return pairwise_block(a, n);
+        int n2 = n / 2;
+        n2 -= n2 % 8;
+        return __fadd_rn(pairwise_rec<D - 1>(a, n2), pairwise_rec<D - 1>(a + n2, n - n2));
+    }
+}
+__device__ __forceinline__ float pairwise_sum(const float* a, int n) { return pairwise_rec<4>(a, n); }
+
+// ------------------------------------------- exact scipy heap (rare path)
+// Restates scipy 1.15.3 _shortest_path.pyx FibonacciHeap on index links.
+struct Heap {
+    FibLane* h;
+    int min;
+};
+
+__device__ void fh_add_sibling(FibLane* h, int node, int ns) {
+    int r = h->right[node];
+    if (r >= 0) h->left[r] = (int8_t)ns;
+    h->right[ns] = (int8_t)r;
+    h->left[ns] = (int8_t)node;
+    h->right[node] = (int8_t)ns;
+    int par = h->parent[node];
+    h->parent[ns] = (int8_t)par;
+    if (par >= 0) h->rank[par] += 1;
+}
+__device__ void fh_add_child(FibLane* h, int node, int c) {
+    h->parent[c] = (int8_t)node;
+    int ch = h->child[node];
+    if (ch >= 0) {
+        fh_add_sibling(h, ch, c);
+    } else {
+        h->child[node] = (int8_t)c;
+        h->right[c] = -1;
+        h->left[c] = -1;
+        h->rank[node] = 1;
+    }
+}
+__device__ void fh_remove(FibLane* h, int node) {
+    int par = h->parent[node];
+    if (par >= 0) {
+        h->rank[par] -= 1;
+        if (h->child[par] == node) h->child[par] = h->right[node];
+    }
+    int l = h->left[node], r = h->right[node];
+    if (l >= 0) h->right[l] = (int8_t)r;
+    if (r >= 0) h->left[r] = (int8_t)l;
+    h->left[node] = -1;
+    h->right[node] = -1;
+    h->parent[node] = -1;
+}
+__device__ void fh_insert(Heap& H, int node) {
+    FibLane* h = H.h;
+    if (H.min >= 0) {
+        if (h->val[node] < h->val[H.min]) {
+            h->left[node] = -1;
+            h->right[node] = (int8_t)H.min;
+            h->left[H.min] = (int8_t)node;
+            H.min = node;
+        } else {
+            fh_add_sibling(h, H.min, node);
+        }
+    } else {
+        H.min = node;
+    }
+}
+__device__ void fh_decrease(Heap& H, int node, double nv) {
+    FibLane* h = H.h;
+    h->val[node] = nv;
+    int par = h->parent[node];
+    if (par >= 0 && h->val[par] >= nv) {
+        fh_remove(h, node);
+        fh_insert(H, node);
+    } else if (h->val[H.min] > nv) {
+        fh_remove(h, node);
+        h->right[node] = (int8_t)H.min;
+        h->left[H.min] = (int8_t)node;
+        H.min = node;
+    }
+}
+__device__ void fh_link(Heap& H, int node) {
+    FibLane* h = H.h;
+    for (;;) {
+        int rk = h->rank[node];
+        int ln = h->roots[rk];
+        if (ln < 0) {
+            h->roots[rk] = (int8_t)node;
+            return;
+        }
+        h->roots[rk] = -1;
+        if (h->val[node] < h->val[ln] || node == H.min) {
+            fh_remove(h, ln);
+            fh_add_child(h, node, ln);
+        } else {
+            fh_remove(h, node);
+            fh_add_child(h, ln, node);
+            node = ln;
+        }
+    }
+}
+__device__ int fh_remove_min(Heap& H) {
+    FibLane* h = H.h;
+    int temp = h->child[H.min];
+    while (temp >= 0) {
+        int tr = h->right[temp];
+        fh_remove(h, temp);
+        fh_add_sibling(h, H.min, temp);
+        temp = tr;
+    }
+    int out = H.min;
+    temp = h->right[H.min];
+    fh_remove(h, H.min);
+    H.min = temp;
+    if (temp < 0) return out;
+    for (int i = 0; i < 32; ++i) h->roots[i] = -1;
+    while (temp >= 0) {
+        if (h->val[temp] < h->val[H.min]) H.min = temp;
+        int tr = h->right[temp];
+        fh_link(H, temp);
+        temp = tr;
+    }
+    temp = H.min;
+    while (h->left[temp] >= 0) temp = h->left[temp];
+    if (H.min != temp) {
+        fh_remove(h, H.min);
+        h->right[H.min] = (int8_t)temp;
+        h->left[temp] = (int8_t)H.min;
+    }
+    return out;
+}
+
+// Exact scipy-order SSSP for one lane; writes scan order and predecessors
+// (node-major [v][L] LDS layout) and returns the number of scanned nodes.
+template <typename CostFn>
+__device__ int exact_sssp(const DevGraph& g, CostFn cost, int origin, FibLane* h, uint8_t* ord, uint8_t* pred,
+                          int L, int lane) {
+    const int N = g.N;
+    for (int k = 0; k < N; ++k) {
+        h->val[k] = 0.0;
+        h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
+        h->rank[k] = 0;
+        h->state[k] = 0;
+        pred[k * L + lane] = kNoPred;
+    }
+    Heap H{h, -1};
+    fh_insert(H, origin);
+    int k = 0;
+    while (H.min >= 0) {
+        int v = fh_remove_min(H);
+        h->state[v] = 2;
+        if (ord) ord[k * L + lane] = (uint8_t)v;
+        ++k;
+        double vv = h->val[v];
+        for (int j = g.indptr[v]; j < g.indptr[v + 1]; ++j) {
+            int jc = g.indices[j];
+            int st = h->state[jc];
+            if (st != 2) {
+                double nv = vv + (double)cost(v, jc);
+                if (st == 0) {
+                    h->state[jc] = 1;
+                    h->val[jc] = nv;
+                    fh_insert(H, jc);
+                    pred[jc * L + lane] = (uint8_t)v;
+                } else if (h->val[jc] > nv) {
+                    fh_decrease(H, jc, nv);
+                    pred[jc * L + lane] = (uint8_t)v;
+                }
+            }
+        }
+    }
+    return k;
+}
+
+// compute_reward_with_goal (repair_env.py:244-291)
+__device__ double reward_fn(const trx_params& p, double prev, double curr, double init, bool complete) {
+    double bonus = complete ? p.reward_beta : 0.0;
+    double r;
+    if (p.reward_mode == TRX_REWARD_MINIMIZE_TSTT || p.reward_mode == TRX_REWARD_REL_IMPROVE) {
+        double base = init;
+        double bb = base > 1.0 ? base : 1.0;
+        if (p.reward_mode == TRX_REWARD_MINIMIZE_TSTT) {
+            r = -p.reward_alpha * (curr / bb);
+        } else {
+            double delta_pct = ((prev - curr) / bb) * 100.0;
+            double ratio = curr / bb;
+            r = p.reward_alpha * delta_pct - 1.0 * ratio;
+        }
+        r = r + bonus;
+    } else {
+        double delta;
+        if (p.reward_mode == TRX_REWARD_NEG_TSTT) {
+            delta = -curr;
+        } else if (p.reward_mode == TRX_REWARD_LOG_DELTA) {
+            delta = log10(prev > 1.0 ? prev : 1.0) - log10(curr > 1.0 ? curr : 1.0);
+        } else {
+            delta = prev - curr;
+        }
+        r = p.reward_alpha * delta + bonus - p.reward_gamma;
+    }
+    if (p.reward_clip > 0) r = r < -p.reward_clip ? -p.reward_clip : (r > p.reward_clip ? p.reward_clip : r);
+    return r;
+}
+
+}  // namespace
+}  // namespace trx

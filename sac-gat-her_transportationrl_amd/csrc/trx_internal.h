@@ -4,7 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/trafficrl.h"
+#include "trafficrl.h"
 
 namespace trx {
 
@@ -60,6 +60,11 @@ size_t small_workspace_bytes(const DevGraph& g, int num_envs);
 hipError_t launch_env_kernel(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                              const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                              const uint8_t* env_mask, void* workspace, hipStream_t stream);
+
+LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs);
+hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
+                                  const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                                  const uint8_t* env_mask, hipStream_t stream);
 
 hipError_t launch_observe_kernel(const DevGraph& g, int num_envs, const trx_state& s, float* node_x, float* edge_x,
                                  float* mask, hipStream_t stream);

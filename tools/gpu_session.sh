@@ -23,6 +23,8 @@ for s in "$@"; do
         bench) step bench 600 python bench.py ;;
         benchq) step bench 400 python bench.py --steps 44 --warmup 22 --cpu-seconds 5 ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 44 --warmup 22 --no-cpu ;;
+        benchab) step bench_lane 300 env TRX_KERNEL=lane python bench.py --steps 44 --warmup 22 --no-cpu
+                 step bench_quad 300 python bench.py --steps 44 --warmup 22 --no-cpu ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
