@@ -19,8 +19,38 @@
 // order-independent (integral demands, total < 2^24, checked on the host).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device_common.h"
 #include "trx_internal.h"
+
+#ifdef TRX_PHASE_STAMPS
+// Diagnostic build only: per-phase cycle totals (thread 0 of each workgroup,
+// summed over workgroups).  Never compiled into the shipped library.
+__device__ unsigned long long trx_phase_cycles[8];
+#define TRX_STAMP(slot)                                                     \
+    do {                                                                    \
+        if (threadIdx.x == 0) {                                             \
+            unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
+            atomicAdd(&trx_phase_cycles[slot], now_ - stamp_prev_);          \
+            stamp_prev_ = now_;                                             \
+        }                                                                   \
+    } while (0)
+extern "C" int trx_debug_phase_cycles(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_phase_cycles), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -2;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(trx_phase_cycles), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#else
+#define TRX_STAMP(slot) \
+    do {                \
+    } while (0)
+#endif
 
 namespace trx {
 
@@ -28,47 +58,59 @@ namespace {
 
 constexpr int kQuad = 4;
 
+// Byte offsets of the LDS regions (plain integers: the kernel derives typed
+// LDS pointers from them, so no pointer table is ever materialised).
 struct SmemQ {
-    float *flow, *cap, *dmg, *goal, *t, *aux, *dprev;  // [EPW*E]
-    float* w;          // [EPW][NP(u)][4(j)][NP/4(i)]  cost of u -> 4i+j
-    uint8_t* pred;     // [EPW*Z][NP]  per tree
-    int16_t* eid;      // [NP*NP]
-    float* dem;        // [Z*N]
-    float* unas;       // [L]
-    int* act;          // [EPW]
-    double* red;       // [EPW*2]
-    FibLane* heap;     // [L/64]
+    uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [EPW*E] f32
+    uint32_t w;      // [EPW][NP(u)][4(j)][NP/4(i)] f32: cost of u -> 4i+j
+    uint32_t pred;   // [EPW*Z][NP] u8 per tree
+    uint32_t ord;    // [EPW*Z][NP] u8 scan order per tree
+    uint32_t dist;   // [EPW*Z][NP] f64 labels per tree (tie post-pass)
+    uint32_t nscan;  // [EPW*Z] i32
+    uint32_t inptr;  // [N+1] i16 in-edge CSR
+    uint32_t insrc;  // [E] u8
+    uint32_t eid;    // [NP*NP] i16
+    uint32_t dem;    // [Z*N] f32
+    uint32_t unas;   // [L] f32
+    uint32_t act;    // [EPW] i32
+    uint32_t red;    // [EPW*2] f64
+    uint32_t heap;   // [L/64] FibLane
+    uint32_t total;
 };
 
-__host__ __device__ inline size_t align16q(size_t x) { return (x + 15) & ~size_t(15); }
+__host__ __device__ inline uint32_t align16q(uint32_t x) { return (x + 15u) & ~15u; }
 
-__host__ __device__ inline size_t smemq_layout(int E, int N, int Z, int NP, int EPW, int L, SmemQ* s,
-                                               unsigned char* base) {
-    size_t off = 0;
-    size_t el = (size_t)EPW * E * sizeof(float);
-    float** arrs[7] = {s ? &s->flow : nullptr, s ? &s->cap : nullptr, s ? &s->dmg : nullptr, s ? &s->goal : nullptr,
-                       s ? &s->t : nullptr,    s ? &s->aux : nullptr, s ? &s->dprev : nullptr};
-    for (int i = 0; i < 7; ++i) {
-        if (s) *arrs[i] = (float*)(base + off);
-        off = align16q(off + el);
-    }
-    if (s) s->w = (float*)(base + off);
-    off = align16q(off + (size_t)EPW * NP * NP * sizeof(float));
-    if (s) s->pred = base + off;
-    off = align16q(off + (size_t)EPW * Z * NP);
-    if (s) s->eid = (int16_t*)(base + off);
-    off = align16q(off + (size_t)NP * NP * sizeof(int16_t));
-    if (s) s->dem = (float*)(base + off);
-    off = align16q(off + (size_t)Z * N * sizeof(float));
-    if (s) s->unas = (float*)(base + off);
-    off = align16q(off + (size_t)L * sizeof(float));
-    if (s) s->act = (int*)(base + off);
-    off = align16q(off + (size_t)EPW * sizeof(int));
-    if (s) s->red = (double*)(base + off);
-    off = align16q(off + (size_t)EPW * 2 * sizeof(double));
-    if (s) s->heap = (FibLane*)(base + off);
-    off = align16q(off + (size_t)((L + 63) / 64) * sizeof(FibLane));
-    return off;
+__host__ __device__ inline SmemQ smemq_layout(int E, int N, int Z, int NP, int EPW, int L) {
+    SmemQ o{};
+    uint32_t off = 0;
+    auto take = [&off](uint32_t bytes) {
+        uint32_t r = off;
+        off = align16q(off + bytes);
+        return r;
+    };
+    const uint32_t el = (uint32_t)(EPW * E * 4);
+    o.flow = take(el);
+    o.cap = take(el);
+    o.dmg = take(el);
+    o.goal = take(el);
+    o.t = take(el);
+    o.aux = take(el);
+    o.dprev = take(el);
+    o.w = take((uint32_t)(EPW * NP * NP * 4));
+    o.pred = take((uint32_t)(EPW * Z * NP));
+    o.ord = take((uint32_t)(EPW * Z * NP));
+    o.dist = take((uint32_t)(EPW * Z * NP * 8));
+    o.nscan = take((uint32_t)(EPW * Z * 4));
+    o.inptr = take((uint32_t)((N + 1) * 2));
+    o.insrc = take((uint32_t)E);
+    o.eid = take((uint32_t)(NP * NP * 2));
+    o.dem = take((uint32_t)(Z * N * 4));
+    o.unas = take((uint32_t)(L * 4));
+    o.act = take((uint32_t)(EPW * 4));
+    o.red = take((uint32_t)(EPW * 2 * 8));
+    o.heap = take((uint32_t)(((L + 63) / 64) * sizeof(FibLane)));
+    o.total = off;
+    return o;
 }
 
 // DPP quad_perm controls: xor 1 = [1,0,3,2], xor 2 = [2,3,0,1]
@@ -93,7 +135,7 @@ __device__ __forceinline__ void quad_min_step(double& best, int& bu) {
 }  // namespace
 
 template <int NP>
-__global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_params p, const trx_state s, int B,
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))) env_kernel_q(const DevGraph g, const trx_params p, const trx_state s, int B,
                                                     int EPW, int mode, const int32_t* __restrict__ action,
                                                     double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                                                     uint8_t* __restrict__ valid_out,
@@ -105,8 +147,24 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
     const int tid = threadIdx.x;
     const int EL = EPW * E;
     const int env0 = blockIdx.x * EPW;
-    SmemQ S;
-    smemq_layout(E, N, Z, NP, EPW, L, &S, smem_raw);
+    const SmemQ O = smemq_layout(E, N, Z, NP, EPW, L);
+    struct {
+        float *flow, *cap, *dmg, *goal, *t, *aux, *dprev, *w, *dem, *unas;
+        uint8_t *pred, *ord, *insrc;
+        double *dist, *red;
+        int *nscan, *act;
+        int16_t *inptr, *eid;
+        FibLane* heap;
+    } S = {(float*)(smem_raw + O.flow), (float*)(smem_raw + O.cap),   (float*)(smem_raw + O.dmg),
+           (float*)(smem_raw + O.goal), (float*)(smem_raw + O.t),     (float*)(smem_raw + O.aux),
+           (float*)(smem_raw + O.dprev), (float*)(smem_raw + O.w),    (float*)(smem_raw + O.dem),
+           (float*)(smem_raw + O.unas), smem_raw + O.pred,            smem_raw + O.ord,
+           smem_raw + O.insrc,          (double*)(smem_raw + O.dist), (double*)(smem_raw + O.red),
+           (int*)(smem_raw + O.nscan),  (int*)(smem_raw + O.act),     (int16_t*)(smem_raw + O.inptr),
+           (int16_t*)(smem_raw + O.eid), (FibLane*)(smem_raw + O.heap)};
+#ifdef TRX_PHASE_STAMPS
+    unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
 
     // ------------------------------------------------ per-env activation
     if (tid < EPW) {
@@ -129,6 +187,8 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
     }
     for (int i = tid; i < NP * NP; i += L) S.eid[i] = g.eid_of[i];
     for (int i = tid; i < Z * N; i += L) S.dem[i] = g.dem[i];
+    for (int i = tid; i <= N; i += L) S.inptr[i] = (int16_t)g.in_ptr[i];
+    for (int i = tid; i < E; i += L) S.insrc[i] = (uint8_t)g.in_src[i];
     __syncthreads();
 
     // ------------------------------------------------------- load state
@@ -162,6 +222,7 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
         S.t[i] = S.act[el] ? bpr_cost(fl, cp, g.t0[e], dm, p.bpr_alpha, p.bpr_beta) : 0.0f;
     }
     __syncthreads();
+    TRX_STAMP(0);
 
     // thread -> (tree = (env, origin zone), lane j of its quad)
     const int tree = tid / kQuad;
@@ -182,21 +243,23 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
             S.w[x] = e >= 0 ? S.t[el * E + e] : kInfF;
         }
         __syncthreads();
+        TRX_STAMP(1);
 
-        // ---------------- shortest-path tree per quad
-        double d[NPL];
+        // ---------------- shortest-path tree per quad (Dijkstra, float64 labels)
         bool amb_tree = false;
         if (tree_on) {
             const float* Wl = S.w + lenv * NP * NP;
-            uint32_t info[NPL];  // pred | level << 8
+            uint8_t* ord = S.ord + tree * NP;
+            double d[NPL];
+            uint32_t pr[NPL];  // predecessor node id, kNoPred = none
 #pragma unroll
             for (int i = 0; i < NPL; ++i) {
                 d[i] = (kQuad * i + j == origin) ? 0.0 : kInfD;
-                info[i] = kNoPred;
+                pr[i] = kNoPred;
             }
-            uint32_t scanned = 0u, amb = 0u, lev = 0u;
-            double last = -1.0;
-            for (int k = 0; k < N; ++k) {
+            uint32_t scanned = 0u;
+            int k = 0;
+            for (; k < N; ++k) {
                 double best = kInfD;
                 int bu = 0x7fffffff;
 #pragma unroll
@@ -210,10 +273,7 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
                 if (!(best < kInfD)) break;  // quad-uniform
                 const int u = bu;
                 if ((u & (kQuad - 1)) == j) scanned |= 1u << (u >> 2);
-                if (best > last) {
-                    ++lev;
-                    last = best;
-                }
+                if (j == 0) ord[k] = (uint8_t)u;
                 const float* row = Wl + u * NP + j * NPL;
                 float wv[NPL];
                 if constexpr (NPL % 4 == 0) {
@@ -229,69 +289,129 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
                         wv[2 * q] = w2.x; wv[2 * q + 1] = w2.y;
                     }
                 }
+                // strict improvement (scipy `current_node.val > next_val`); scanned
+                // labels never improve since costs are > 0
 #pragma unroll
                 for (int i = 0; i < NPL; ++i) {
                     double nd = __dadd_rn(best, (double)wv[i]);
-                    bool uns = !((scanned >> i) & 1u) && (wv[i] < kInfF);
-                    bool better = uns && nd < d[i];
-                    bool tie = uns && !better && nd == d[i] && ((info[i] >> 8) == lev);
+                    bool better = nd < d[i];
                     d[i] = better ? nd : d[i];
-                    info[i] = better ? ((uint32_t)u | (lev << 8)) : info[i];
-                    amb = better ? (amb & ~(1u << i)) : (tie ? (amb | (1u << i)) : amb);
+                    pr[i] = better ? (uint32_t)u : pr[i];
                 }
             }
-            uint8_t* pr = S.pred + tree * NP;
+            if (j == 0) S.nscan[tree] = k;
+            double* dl = S.dist + tree * NP;
+            uint8_t* pl = S.pred + tree * NP;
 #pragma unroll
-            for (int i = 0; i < NPL; ++i) pr[kQuad * i + j] = (uint8_t)(info[i] & 0xFF);
-            int a = amb != 0u;
-            a |= qperm<0xB1>(a);
-            a |= qperm<0x4E>(a);
-            amb_tree = a != 0;
+            for (int i = 0; i < NPL; ++i) {
+                dl[kQuad * i + j] = d[i];
+                pl[kQuad * i + j] = (uint8_t)pr[i];
+            }
+            // tie post-pass: ambiguous iff some node has >= 2 equal-cost tails at
+            // the smallest tail label (scipy's heap order then picks the pred).
+            // Labels of other lanes are read back from LDS (same wave: in order).
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int amb = 0;
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int v = kQuad * i + j;
+                if (v < N && v != origin && d[i] < kInfD) {
+                    double m = kInfD;
+                    int cnt = 0;
+                    for (int q = S.inptr[v]; q < S.inptr[v + 1]; ++q) {
+                        int u = S.insrc[q];
+                        double du = dl[u];
+                        double nd = __dadd_rn(du, (double)Wl[u * NP + j * NPL + i]);
+                        if (nd == d[i]) {
+                            cnt = du < m ? 1 : (du == m ? cnt + 1 : cnt);
+                            m = du < m ? du : m;
+                        }
+                    }
+                    amb |= cnt > 1;
+                }
+            }
+            amb |= qperm<0xB1>(amb);
+            amb |= qperm<0x4E>(amb);
+            amb_tree = amb != 0;
         }
+        TRX_STAMP(2);
         {
-            // trees whose predecessor choice depends on scipy's heap order are
-            // replayed exactly, one at a time per wave, by the quad's lane 0
             uint64_t pending = __ballot(tree_on && amb_tree && j == 0);
             FibLane* h = S.heap + (tid >> 6);
             while (pending) {
                 int leader = __ffsll((unsigned long long)pending) - 1;
                 if ((tid & 63) == leader) {
                     const float* Wl = S.w + lenv * NP * NP;
-                    exact_sssp(
-                        g, [&](int a_, int b_) { return Wl[a_ * NP + (b_ & 3) * NPL + (b_ >> 2)]; }, origin, h,
-                        nullptr, S.pred + tree * NP, 1, 0);
+                    S.nscan[tree] = exact_sssp(
+                        N, g.indptr, g.indices,
+                        [Wl](int a_, int b_) { return Wl[a_ * NP + (b_ & 3) * NPL + (b_ >> 2)]; }, origin, h,
+                        S.ord + tree * NP, S.pred + tree * NP, 1, 0);
                 }
                 pending &= pending - 1;
             }
         }
         __syncthreads();
+        TRX_STAMP(3);
 
-        // ---------------- all-or-nothing: walk predecessor paths (repair_env.py:495-502)
+        // ---------------- all-or-nothing: subtree accumulation in reverse scan
+        // order (repair_env.py:490-502 summed per tree; integer demands make
+        // the float sums exact in any order).  Reachable <=> has a predecessor.
         if (tree_on) {
-            const uint8_t* pr = S.pred + tree * NP;
+            uint32_t pr[NPL];
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) pr[i] = S.pred[tree * NP + kQuad * i + j];
+            const int nscan = S.nscan[tree];
             const float* dm = S.dem + zi * N;
-            float* aux = S.aux + lenv * E;
+            float acc[NPL];
             float un = 0.0f;
 #pragma unroll
             for (int i = 0; i < NPL; ++i) {
                 const int v = kQuad * i + j;
-                if (v < N) {
-                    float dv = dm[v];
-                    bool reach = d[i] < kInfD && v != origin;
-                    un += reach ? 0.0f : dv;  // unreachable or intrazonal (repair_env.py:708)
-                    if (reach && dv != 0.0f) {
-                        int cur = v;
-                        for (int hop = 0; hop < N && cur != origin; ++hop) {
-                            int pu = pr[cur];
-                            atomicAdd(&aux[S.eid[pu * NP + cur]], dv);
-                            cur = pu;
-                        }
+                float dv = v < N ? dm[v] : 0.0f;
+                bool reach = pr[i] != kNoPred;
+                acc[i] = reach ? dv : 0.0f;
+                un += reach ? 0.0f : dv;  // unreachable or intrazonal (repair_env.py:708)
+            }
+            unassigned_lane = un;
+            uint32_t ow[NP / 4];
+            const uint32_t* ordw = reinterpret_cast<const uint32_t*>(S.ord + tree * NP);
+#pragma unroll
+            for (int q = 0; q < NP / 4; ++q) ow[q] = ordw[q];
+            float* aux = S.aux + lenv * E;
+#pragma unroll
+            for (int k = NP - 1; k >= 1; --k) {
+                if (k < nscan) {  // quad-uniform
+                    const int v = (ow[k >> 2] >> (8 * (k & 3))) & 0xFF;
+                    const int slot = v >> 2;
+                    float av = 0.0f;
+                    int pv = 0;
+#pragma unroll
+                    for (int i = 0; i < NPL; ++i) {
+                        av = (i == slot) ? acc[i] : av;
+                        pv = (i == slot) ? (int)pr[i] : pv;
+                    }
+                    const bool mine = (v & (kQuad - 1)) == j;
+                    av = mine ? av : 0.0f;
+                    pv = mine ? pv : 0;
+                    // exactly one lane holds the values: quad sums broadcast them
+                    av += __int_as_float(qperm<0xB1>(__float_as_int(av)));
+                    av += __int_as_float(qperm<0x4E>(__float_as_int(av)));
+                    pv |= qperm<0xB1>(pv);
+                    pv |= qperm<0x4E>(pv);
+                    if (av != 0.0f) {
+                        const bool pmine = (pv & (kQuad - 1)) == j;
+                        const int ps = pv >> 2;
+#pragma unroll
+                        for (int i = 0; i < NPL; ++i) acc[i] = (pmine && i == ps) ? acc[i] + av : acc[i];
+                        if (pmine) atomicAdd(&aux[S.eid[pv * NP + v]], av);
                     }
                 }
             }
-            unassigned_lane = un;
         }
         __syncthreads();
+        TRX_STAMP(4);
 
         // ---------------- flow update + BPR (repair_env.py:317-342)
         if (p.method == TRX_METHOD_CFW) {
@@ -342,6 +462,7 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
             S.t[i] = bpr_cost(nf, S.cap[i], g.t0[e], S.dmg[i], p.bpr_alpha, p.bpr_beta);
         }
         __syncthreads();
+        TRX_STAMP(5);
     }
 
     // ---------------- per-env unassigned (tree order, exact integers)
@@ -382,6 +503,8 @@ __global__ void __launch_bounds__(512) env_kernel_q(const DevGraph g, const trx_
             s.goal[gi] = S.goal[i];
         }
     }
+    __syncthreads();
+    TRX_STAMP(6);
 }
 
 LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs) {
@@ -389,12 +512,15 @@ LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs) {
     c.np = g.NP;
     // envs per workgroup: fill up to 512 threads with whole envs (Z quads each)
     int per_env = g.Z * kQuad;
-    int epw = 512 / per_env;
-    if (epw < 1) epw = 1;
-    if (epw > 4) epw = 4;  // 384 threads for SF: ~28 KB LDS, 5 workgroups/CU
+    static const int epw_env = [] {
+        const char* e = getenv("TRX_EPW");  // tuning knob (A/B runs)
+        return e ? atoi(e) : 0;
+    }();
+    int epw = epw_env > 0 ? epw_env : 2;  // SF: 2 envs = 192 threads, 6 workgroups/CU at 96 VGPRs
+    while (epw > 1 && epw * per_env > 512) --epw;
     c.epw = epw;
     c.threads = ((epw * per_env + 63) / 64) * 64;
-    c.smem = smemq_layout(g.E, g.N, g.Z, c.np, c.epw, c.threads, nullptr, nullptr);
+    c.smem = smemq_layout(g.E, g.N, g.Z, c.np, c.epw, c.threads).total;
     c.blocks = (num_envs + c.epw - 1) / c.epw;
     return c;
 }

@@ -89,16 +89,9 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
     if (!ws) return fail(TRX_EINVAL, "workspace is NULL (size it with trx_workspace_bytes)");
     hipError_t e = hipSetDevice(g->device);
     if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
-    static const bool use_lane_kernel = [] {
-        const char* k = getenv("TRX_KERNEL");
-        return k && strcmp(k, "lane") == 0;
-    }();
-    if (use_lane_kernel)  // v1: one lane per shortest-path tree (kept for A/B)
-        e = trx::launch_env_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws,
-                                   static_cast<hipStream_t>(stream));
-    else  // v2: one quad of lanes per tree
-        e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
-                                        static_cast<hipStream_t>(stream));
+    (void)ws;
+    e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
+                                    static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
@@ -254,7 +247,7 @@ int trx_graph_info(const trx_graph* g, int32_t* num_nodes, int32_t* num_edges, i
 
 int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs) {
     if (!g || num_envs < 0) return fail(TRX_EINVAL, "bad arguments");
-    return (int64_t)trx::small_workspace_bytes(g->dg, num_envs) + 256;
+    return 256;  // all per-env work lives in LDS; kept in the ABI for larger-graph kernels
 }
 
 int trx_assign(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, const uint8_t* env_mask, void* ws,

@@ -195,9 +195,8 @@ __device__ int fh_remove_min(Heap& H) {
 // Exact scipy-order SSSP for one lane; writes scan order and predecessors
 // (node-major [v][L] LDS layout) and returns the number of scanned nodes.
 template <typename CostFn>
-__device__ int exact_sssp(const DevGraph& g, CostFn cost, int origin, FibLane* h, uint8_t* ord, uint8_t* pred,
-                          int L, int lane) {
-    const int N = g.N;
+__device__ int exact_sssp(const int N, const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                          CostFn cost, int origin, FibLane* h, uint8_t* ord, uint8_t* pred, int L, int lane) {
     for (int k = 0; k < N; ++k) {
         h->val[k] = 0.0;
         h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
@@ -214,8 +213,8 @@ __device__ int exact_sssp(const DevGraph& g, CostFn cost, int origin, FibLane* h
         if (ord) ord[k * L + lane] = (uint8_t)v;
         ++k;
         double vv = h->val[v];
-        for (int j = g.indptr[v]; j < g.indptr[v + 1]; ++j) {
-            int jc = g.indices[j];
+        for (int j = indptr[v]; j < indptr[v + 1]; ++j) {
+            int jc = indices[j];
             int st = h->state[jc];
             if (st != 2) {
                 double nv = vv + (double)cost(v, jc);

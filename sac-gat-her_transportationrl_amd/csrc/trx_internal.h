@@ -54,13 +54,6 @@ struct LaunchCfg {
     int blocks;    // grid
 };
 
-LaunchCfg small_launch_cfg(const DevGraph& g, int num_envs);
-size_t small_workspace_bytes(const DevGraph& g, int num_envs);
-
-hipError_t launch_env_kernel(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
-                             const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
-                             const uint8_t* env_mask, void* workspace, hipStream_t stream);
-
 LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs);
 hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,

@@ -1,0 +1,34 @@
+"""Diagnostic: per-phase cycle shares of the v2 env kernel (stamps build).
+
+Loads trafficrl/libtrafficrl_stamps.so INSTEAD of the shipped library (make
+stamps), runs a few steps of the bench workload, prints cycle shares.  Read
+the shares, not the absolute time (stamps serialise thread 0).
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
+import torch  # noqa: E402
+from trafficrl import _lib  # noqa: E402
+
+_lib.LIB_PATH = os.path.join(ROOT, "sac-gat-her_transportationrl_amd", "trafficrl", "libtrafficrl_stamps.so")
+L = _lib.load()
+L.trx_debug_phase_cycles.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+from trafficrl.data import sioux_falls  # noqa: E402
+from trafficrl.env import VecRepairEnv  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=True, fixed_damage_seed=42)
+buf = (ctypes.c_ulonglong * 8)()
+L.trx_debug_phase_cycles(buf, 1)
+gen = torch.Generator(device="cuda").manual_seed(0)
+for _ in range(5):
+    a = (torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32)
+    env.step(a, observe=False)
+L.trx_debug_phase_cycles(buf, 1)
+names = ["load", "cost build", "dijkstra", "tie check+replay", "aon", "update+bpr", "tstt+store"]
+tot = sum(buf[i] for i in range(7))
+for i, n in enumerate(names):
+    print(f"{n:>14}: {buf[i] / tot * 100:6.2f} %  ({buf[i] / 5 / (B / 4) / 30:.0f} cycles/WG/iter)")
