@@ -95,6 +95,21 @@ def cpu_baseline(method, iters, seconds=12.0):
                       f"link each) in {dt:.1f}s on {threads} host threads; oracle/trx_oracle.c"}
 
 
+def measured_traffic():
+    """HBM bytes per env_kernel launch from the latest committed rocprofv3 PMC
+    summary (profiles/*_pmc.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes of this bench's workload)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        return d.get("hbm_bytes_per_launch_raw"), os.path.relpath(files[-1], ROOT)
+    except (OSError, ValueError):
+        return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -194,6 +209,9 @@ def main():
     P = len(env.graph.od_o)
     bpa = bytes_per_assign(N, E, Z, P, args.iters)
     achieved = bpa * B / mean_kernel_s
+    traffic, traffic_src = measured_traffic()
+    if (args.envs, args.iters, args.method) != (4096, 30, "msa"):
+        traffic, traffic_src = None, None  # the committed PMC pass is for the default workload
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
@@ -220,7 +238,9 @@ def main():
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK, "traffic": None,
+                "frac": achieved / HBM_PEAK, "traffic": traffic,
+                "traffic_note": (f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {traffic_src} "
+                                 "(raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic else None,
                 "kernel": "trx::env_kernel<24>", "kernel_mean_ms": mean_kernel_s * 1e3,
                 "bytes_per_assign": bpa, "assigns_per_launch": B,
             },

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (gpurun_out/pmc1..4) for the env kernel
+into profiles/<tag>_pmc.json.
+
+HBM traffic per launch = (FETCH_SIZE + WRITE_SIZE) x 1024 B (rocprofv3 reports
+KB).  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reads exactly half the
+bytes of a wide (16 B/lane) coalesced stream; other widths are uncalibrated.
+This kernel's loads are 4-byte per lane (SoA link arrays), so the raw value is
+reported and the x2 wide-stream correction is given as an upper bound.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+agg = defaultdict(list)
+for f in sorted(glob.glob(os.path.join(root, "gpurun_out", "pmc*", "run_counter_collection.csv"))):
+    for r in csv.DictReader(open(f)):
+        if "env_kernel" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+mean = {k: sum(v) / len(v) for k, v in agg.items()}
+out = {"kernel": "trx::env_kernel_q<24>", "dispatches": {k: len(v) for k, v in agg.items()},
+       "per_dispatch_mean": mean}
+if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+    raw = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
+    out["hbm_bytes_per_launch_raw"] = raw
+    out["hbm_bytes_per_launch_fetch_x2_upper"] = (2 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
+if "SQ_WAVE_CYCLES" in mean:
+    w = mean["SQ_WAVE_CYCLES"]
+    out["wait_any_frac"] = mean.get("SQ_WAIT_ANY", 0) / w
+    out["active_inst_any_frac"] = mean.get("SQ_ACTIVE_INST_ANY", 0) / w
+    out["wait_inst_any_frac"] = mean.get("SQ_WAIT_INST_ANY", 0) / w
+path = os.path.join(root, "profiles", f"{tag}_pmc.json")
+json.dump(out, open(path, "w"), indent=1)
+print(json.dumps(out, indent=1))
