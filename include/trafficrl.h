@@ -145,6 +145,30 @@ int trx_step(const trx_graph* g, const trx_params* p, int32_t num_envs, trx_stat
 int trx_observe(const trx_graph* g, int32_t num_envs, const trx_state* s, float* node_x, float* edge_x,
                 float* mask, void* workspace, void* stream);
 
+/* ------------------------------------------------------------------ GAT
+ * Edge softmax + neighbour aggregation of torch_geometric GATConv as used by
+ * GATEncoder (src/models/gat_encoder.py:22-25, 36-42; PyG GATConv.forward
+ * after `lin`): over a graph in CSR-by-destination form (self loops included)
+ *   logit[e,h] = leaky_relu(a_src[src[e],h] + a_dst[i,h] + a_edge[e,h], negative_slope)
+ *   alpha[e,h] = softmax over the in-edges of i (max-shifted, +1e-16 denominator)
+ *   out[i,h*C:(h+1)*C] = sum_e alpha[e,h] * xh[src[e], h*C:(h+1)*C]  (+ bias, may be NULL)
+ * xh [N, heads*channels] float32 (xh_bf16=0) or bfloat16 (1); a_src/a_dst
+ * [N,heads], a_edge/alpha [num_edges,heads] in CSR order, out [N,heads*channels].
+ * Constraints: heads <= 8, channels % 4 == 0, heads*channels <= 2048,
+ * channels divides 256 or is a multiple of 256. */
+int trx_gat_forward(int32_t num_nodes, int32_t heads, int32_t channels, const int32_t* rowptr, const int32_t* src,
+                    const void* xh, int32_t xh_bf16, const float* a_src, const float* a_dst, const float* a_edge,
+                    float negative_slope, const float* bias, float* out, float* alpha, void* stream);
+/* Backward of trx_gat_forward (without bias).  (sptr, spos, sdst) is the same
+ * graph in CSR by SOURCE: for node j, entries sptr[j]..sptr[j+1] give the
+ * dst-CSR position and destination of each out-edge (fixed order =>
+ * deterministic, no float atomics).  grad_xh [N,heads*channels] float32. */
+int trx_gat_backward(int32_t num_nodes, int32_t heads, int32_t channels, const int32_t* rowptr, const int32_t* src,
+                     const int32_t* sptr, const int32_t* spos, const int32_t* sdst, const void* xh, int32_t xh_bf16,
+                     const float* a_src, const float* a_dst, const float* a_edge, float negative_slope,
+                     const float* alpha, const float* grad_out, float* grad_xh, float* grad_a_src, float* grad_a_dst,
+                     float* grad_a_edge, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -280,4 +280,43 @@ int trx_observe(const trx_graph* g, int32_t B, const trx_state* s, float* node_x
     return TRX_OK;
 }
 
+int trx_gat_forward(int32_t num_nodes, int32_t heads, int32_t channels, const int32_t* rowptr, const int32_t* src,
+                    const void* xh, int32_t xh_bf16, const float* a_src, const float* a_dst, const float* a_edge,
+                    float negative_slope, const float* bias, float* out, float* alpha, void* stream) {
+    if (num_nodes < 0 || heads <= 0 || heads > 8 || channels <= 0 || channels % 4 != 0 || heads * channels > 2048)
+        return fail(TRX_EUNSUP, "gat: need 1<=heads<=8, channels%%4==0, heads*channels<=2048 (got %d x %d)", heads,
+                    channels);
+    if (channels < 256 && (256 % channels) != 0)
+        return fail(TRX_EUNSUP, "gat: channels < 256 must divide 256 (got %d)", channels);
+    if (channels > 256 && channels % 256 != 0) return fail(TRX_EUNSUP, "gat: channels > 256 must be a multiple of 256");
+    if (num_nodes == 0) return TRX_OK;
+    if (!rowptr || !src || !xh || !a_src || !a_dst || !a_edge || !out || !alpha)
+        return fail(TRX_EINVAL, "gat_forward: NULL buffer");
+    hipError_t e = trx::launch_gat_forward(num_nodes, heads, channels, rowptr, src, xh, xh_bf16, a_src, a_dst, a_edge,
+                                           negative_slope, bias, out, alpha, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_forward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_gat_backward(int32_t num_nodes, int32_t heads, int32_t channels, const int32_t* rowptr, const int32_t* src,
+                     const int32_t* sptr, const int32_t* spos, const int32_t* sdst, const void* xh, int32_t xh_bf16,
+                     const float* a_src, const float* a_dst, const float* a_edge, float negative_slope,
+                     const float* alpha, const float* grad_out, float* grad_xh, float* grad_a_src, float* grad_a_dst,
+                     float* grad_a_edge, void* stream) {
+    if (num_nodes < 0 || heads <= 0 || heads > 8 || channels <= 0 || channels % 4 != 0 || heads * channels > 2048)
+        return fail(TRX_EUNSUP, "gat: unsupported heads/channels");
+    if (channels < 256 && (256 % channels) != 0)
+        return fail(TRX_EUNSUP, "gat: channels < 256 must divide 256 (got %d)", channels);
+    if (channels > 256 && channels % 256 != 0) return fail(TRX_EUNSUP, "gat: channels > 256 must be a multiple of 256");
+    if (num_nodes == 0) return TRX_OK;
+    if (!rowptr || !src || !sptr || !spos || !sdst || !xh || !alpha || !grad_out || !grad_xh || !grad_a_src ||
+        !grad_a_dst || !grad_a_edge)
+        return fail(TRX_EINVAL, "gat_backward: NULL buffer");
+    hipError_t e = trx::launch_gat_backward(num_nodes, heads, channels, rowptr, src, sptr, spos, sdst, xh, xh_bf16,
+                                            a_src, a_dst, a_edge, negative_slope, alpha, grad_out, grad_xh, grad_a_src,
+                                            grad_a_dst, grad_a_edge, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 }  // extern "C"

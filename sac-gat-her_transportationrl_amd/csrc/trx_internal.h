@@ -62,4 +62,13 @@ hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const 
 hipError_t launch_observe_kernel(const DevGraph& g, int num_envs, const trx_state& s, float* node_x, float* edge_x,
                                  float* mask, hipStream_t stream);
 
+hipError_t launch_gat_forward(int Nt, int H, int C, const int32_t* rowptr, const int32_t* src, const void* xh,
+                              int bf16, const float* a_src, const float* a_dst, const float* a_edge, float slope,
+                              const float* bias, float* out, float* alpha, hipStream_t stream);
+hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, const int32_t* src, const int32_t* sptr,
+                               const int32_t* spos, const int32_t* sdst, const void* xh, int bf16, const float* a_src,
+                               const float* a_dst, const float* a_edge, float slope, const float* alpha,
+                               const float* gout, float* gxh, float* ga_src, float* ga_dst, float* ga_edge,
+                               hipStream_t stream);
+
 }  // namespace trx

@@ -20,7 +20,8 @@ REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "
 # Every symbol include/trafficrl.h declares (tests check the export table).
 EXPORTS = (
     "trx_abi_version", "trx_last_error", "trx_graph_create", "trx_graph_destroy", "trx_graph_info",
-    "trx_workspace_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe",
+    "trx_workspace_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe", "trx_gat_forward",
+    "trx_gat_backward",
 )
 
 
@@ -74,8 +75,12 @@ def load():
     L.trx_step.argtypes = [_vp, ctypes.POINTER(TrxParams), ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp,
                            _vp, _vp, _vp]
     L.trx_observe.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp, _vp, _vp]
+    L.trx_gat_forward.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, ctypes.c_int32,
+                                  _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _vp]
+    L.trx_gat_backward.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   ctypes.c_int32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     for name in ("trx_graph_create", "trx_graph_destroy", "trx_graph_info", "trx_assign", "trx_reset", "trx_step",
-                 "trx_observe"):
+                 "trx_observe", "trx_gat_forward", "trx_gat_backward"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != 1:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != 1")

@@ -1,0 +1,270 @@
+"""GAT encoder (src/models/gat_encoder.py:9-53) on gfx950 kernels.
+
+`GATConv` keeps torch_geometric's GATConv parameter layout and state_dict keys
+(lin.weight [H*C,in], lin_edge.weight [H*C,edge_dim], att_src/att_dst/att_edge
+[1,H,C], bias) and its forward semantics (PyG 2.5 defaults used by the
+reference: add_self_loops=True with fill_value='mean' edge attributes,
+negative_slope=0.2, softmax over each destination's in-edges with a +1e-16
+denominator, concat or head-mean, bias).  The reference's checkpoints
+(history-data/outputs1/*.pt) load into these modules.
+
+Split of work:
+  * dense projections (lin, the per-head attention dot products, the edge
+    logits) -- torch GEMMs (hipBLASLt, bf16 MFMA under autocast);
+  * edge softmax + neighbour aggregation (+ bias), forward and backward --
+    trx_gat_forward / trx_gat_backward HIP kernels (csrc/gat_kernel.hip) over a
+    cached CSR-by-destination of the batch graph.
+The edge logits use a_edge = edge_attr @ M^T with M[h] = sum_c W_edge[h,c,:] *
+att_edge[h,c] -- algebraically PyG's (lin_edge(edge_attr) * att_edge).sum(-1)
+without materialising the [E, H*C] edge embedding.
+
+torch_geometric is not importable in this environment, so GAT numerics are
+pinned only against tests/test_gat.py's plain-torch restatement of PyG
+semantics ("parity unpinned" w.r.t. the reference's own outputs).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from .. import _lib
+
+
+# --------------------------------------------------------------- graph CSR
+@dataclass
+class GraphCSR:
+    num_nodes: int
+    keep: torch.Tensor      # [E0] bool: non-self-loop input edges (PyG remove_self_loops)
+    src_all: torch.Tensor   # [Et] source of each edge in PyG order (kept edges, then loops)
+    dst_all: torch.Tensor   # [Et]
+    perm: torch.Tensor      # [Et] CSR position -> PyG-order edge id
+    rowptr: torch.Tensor    # [N+1] int32 CSR by destination
+    col: torch.Tensor       # [Et]  int32 source per CSR position
+    sptr: torch.Tensor      # [N+1] int32 CSR by source
+    spos: torch.Tensor      # [Et]  int32 dst-CSR position per source-CSR entry
+    sdst: torch.Tensor      # [Et]  int32 destination per source-CSR entry
+    deg_in: torch.Tensor    # [N] float in-degree of kept edges (for the mean loop attr)
+
+
+_csr_cache: Dict[Tuple, GraphCSR] = {}
+
+
+def build_csr(edge_index: torch.Tensor, num_nodes: int) -> GraphCSR:
+    key = (edge_index.data_ptr(), edge_index.shape[1], edge_index._version, num_nodes, edge_index.device)
+    g = _csr_cache.get(key)
+    if g is not None:
+        return g
+    dev = edge_index.device
+    src0, dst0 = edge_index[0].long(), edge_index[1].long()
+    keep = src0 != dst0
+    loops = torch.arange(num_nodes, device=dev)
+    src_all = torch.cat([src0[keep], loops])
+    dst_all = torch.cat([dst0[keep], loops])
+    Et = src_all.numel()
+    # stable sort by destination -> CSR by destination
+    perm = torch.argsort(dst_all * (Et + 1) + torch.arange(Et, device=dev))
+    counts = torch.bincount(dst_all, minlength=num_nodes)
+    rowptr = torch.zeros(num_nodes + 1, dtype=torch.int64, device=dev)
+    rowptr[1:] = torch.cumsum(counts, 0)
+    col = src_all[perm]
+    # CSR by source over dst-CSR positions
+    sperm = torch.argsort(col * (Et + 1) + torch.arange(Et, device=dev))
+    scounts = torch.bincount(col, minlength=num_nodes)
+    sptr = torch.zeros(num_nodes + 1, dtype=torch.int64, device=dev)
+    sptr[1:] = torch.cumsum(scounts, 0)
+    sdst = dst_all[perm][sperm]
+    deg_in = torch.bincount(dst0[keep], minlength=num_nodes).to(torch.float32)
+    g = GraphCSR(num_nodes, keep, src_all, dst_all, perm, rowptr.to(torch.int32), col.to(torch.int32),
+                 sptr.to(torch.int32), sperm.to(torch.int32), sdst.to(torch.int32), deg_in)
+    if len(_csr_cache) > 64:
+        _csr_cache.clear()
+    _csr_cache[key] = g
+    return g
+
+
+# ---------------------------------------------------- HIP aggregation op
+class _GATAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xh, a_src, a_dst, a_edge, g: GraphCSR, heads: int, channels: int, slope: float):
+        L = _lib.load()
+        N = g.num_nodes
+        xh = xh.contiguous()
+        bf16 = 1 if xh.dtype == torch.bfloat16 else 0
+        if not bf16 and xh.dtype != torch.float32:
+            xh = xh.float()
+        a_src = a_src.float().contiguous()
+        a_dst = a_dst.float().contiguous()
+        a_edge = a_edge.float().contiguous()
+        out = torch.empty(N, heads * channels, device=xh.device, dtype=torch.float32)
+        alpha = torch.empty(a_edge.shape[0], heads, device=xh.device, dtype=torch.float32)
+        _lib.check(L.trx_gat_forward(N, heads, channels, _lib.ptr(g.rowptr), _lib.ptr(g.col), _lib.ptr(xh), bf16,
+                                     _lib.ptr(a_src), _lib.ptr(a_dst), _lib.ptr(a_edge), float(slope), None,
+                                     _lib.ptr(out), _lib.ptr(alpha), _lib.stream_ptr(xh.device)), "trx_gat_forward")
+        ctx.save_for_backward(xh, a_src, a_dst, a_edge, alpha)
+        ctx.g, ctx.heads, ctx.channels, ctx.slope, ctx.bf16 = g, heads, channels, slope, bf16
+        ctx.xh_dtype = xh.dtype
+        ctx.mark_non_differentiable(alpha)
+        return out, alpha
+
+    @staticmethod
+    def backward(ctx, gout, _galpha):
+        L = _lib.load()
+        xh, a_src, a_dst, a_edge, alpha = ctx.saved_tensors
+        g = ctx.g
+        N = g.num_nodes
+        gout = gout.float().contiguous()
+        gxh = torch.empty(N, ctx.heads * ctx.channels, device=gout.device, dtype=torch.float32)
+        ga_src = torch.empty_like(a_src)
+        ga_dst = torch.empty_like(a_dst)
+        ga_edge = torch.empty_like(a_edge)
+        _lib.check(L.trx_gat_backward(N, ctx.heads, ctx.channels, _lib.ptr(g.rowptr), _lib.ptr(g.col),
+                                      _lib.ptr(g.sptr), _lib.ptr(g.spos), _lib.ptr(g.sdst), _lib.ptr(xh), ctx.bf16,
+                                      _lib.ptr(a_src), _lib.ptr(a_dst), _lib.ptr(a_edge), float(ctx.slope),
+                                      _lib.ptr(alpha), _lib.ptr(gout), _lib.ptr(gxh), _lib.ptr(ga_src),
+                                      _lib.ptr(ga_dst), _lib.ptr(ga_edge), _lib.stream_ptr(gout.device)),
+                   "trx_gat_backward")
+        return gxh.to(ctx.xh_dtype), ga_src, ga_dst, ga_edge, None, None, None, None
+
+
+def gat_aggregate(xh, a_src, a_dst, a_edge_csr, g: GraphCSR, heads, channels, slope=0.2):
+    return _GATAggregate.apply(xh, a_src, a_dst, a_edge_csr, g, heads, channels, slope)
+
+
+# ------------------------------------------------------------- modules
+def _glorot_(t: torch.Tensor):
+    # PyG inits.glorot on a [1,H,C] attention vector / [out,in] weight
+    fan = t.size(-2) + t.size(-1)
+    a = math.sqrt(6.0 / fan)
+    with torch.no_grad():
+        t.uniform_(-a, a)
+
+
+class _Lin(nn.Module):
+    """PyG Linear without bias: state_dict key `weight` [out, in]."""
+
+    def __init__(self, in_ch, out_ch):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(out_ch, in_ch))
+        _glorot_(self.weight)
+
+    def forward(self, x):
+        return F.linear(x, self.weight)
+
+
+class GATConv(nn.Module):
+    def __init__(self, in_channels: int, out_channels: int, heads: int = 1, concat: bool = True,
+                 negative_slope: float = 0.2, dropout: float = 0.0, add_self_loops: bool = True,
+                 edge_dim: Optional[int] = None, fill_value: str = "mean", bias: bool = True):
+        super().__init__()
+        if not add_self_loops or fill_value != "mean" or dropout != 0.0:
+            raise NotImplementedError("only the reference's GATConv configuration is ported "
+                                      "(add_self_loops=True, fill_value='mean', dropout=0)")
+        self.in_channels, self.out_channels, self.heads, self.concat = in_channels, out_channels, heads, concat
+        self.negative_slope = negative_slope
+        self.edge_dim = edge_dim
+        self.lin = _Lin(in_channels, heads * out_channels)
+        self.att_src = nn.Parameter(torch.empty(1, heads, out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, heads, out_channels))
+        if edge_dim is not None:
+            self.lin_edge = _Lin(edge_dim, heads * out_channels)
+            self.att_edge = nn.Parameter(torch.empty(1, heads, out_channels))
+        else:
+            self.lin_edge = None
+            self.register_parameter("att_edge", None)
+        self.bias = nn.Parameter(torch.zeros(heads * out_channels if concat else out_channels)) if bias else None
+        _glorot_(self.att_src)
+        _glorot_(self.att_dst)
+        if self.att_edge is not None:
+            _glorot_(self.att_edge)
+
+    def forward(self, x, edge_index, edge_attr=None, return_attention_weights=None):
+        H, C = self.heads, self.out_channels
+        N = x.size(0)
+        g = build_csr(edge_index, N)
+        xh = self.lin(x)                                   # [N, H*C]  (MFMA GEMM)
+        xh3 = xh.view(N, H, C).float()
+        a_src = (xh3 * self.att_src).sum(-1)               # [N, H]
+        a_dst = (xh3 * self.att_dst).sum(-1)
+        if self.lin_edge is not None and edge_attr is not None:
+            ea = edge_attr[g.keep].float()
+            # fill_value='mean': loop attr = mean of the node's incoming edge attrs
+            loop = torch.zeros(N, ea.size(1), device=ea.device, dtype=ea.dtype)
+            loop.index_add_(0, edge_index[1][g.keep].long(), ea)
+            loop = loop / g.deg_in.clamp(min=1.0).unsqueeze(1)
+            full = torch.cat([ea, loop], 0)
+            M = (self.lin_edge.weight.view(H, C, -1).float() * self.att_edge.view(H, C, 1).float()).sum(1)
+            a_edge = full @ M.t()                          # [Et, H]
+        else:
+            a_edge = torch.zeros(g.src_all.numel(), H, device=x.device)
+        out, alpha = gat_aggregate(xh, a_src, a_dst, a_edge[g.perm], g, H, C, self.negative_slope)
+        if not self.concat:
+            out = out.view(N, H, C).mean(1)
+        if self.bias is not None:
+            out = out + self.bias
+        if return_attention_weights:
+            a_pyg = torch.empty_like(alpha)
+            a_pyg[g.perm] = alpha
+            ei = torch.stack([g.src_all, g.dst_all])
+            return out, (ei, a_pyg)
+        return out
+
+
+def global_mean_pool(x, batch, num_graphs: Optional[int] = None):
+    B = int(batch.max()) + 1 if num_graphs is None else num_graphs
+    out = torch.zeros(B, x.size(1), device=x.device, dtype=x.dtype)
+    out.index_add_(0, batch, x)
+    cnt = torch.bincount(batch, minlength=B).clamp(min=1).to(x.dtype).unsqueeze(1)
+    return out / cnt
+
+
+def global_max_pool(x, batch, num_graphs: Optional[int] = None):
+    B = int(batch.max()) + 1 if num_graphs is None else num_graphs
+    out = torch.full((B, x.size(1)), float("-inf"), device=x.device, dtype=x.dtype)
+    return out.scatter_reduce(0, batch.unsqueeze(1).expand_as(x), x, reduce="amax", include_self=True)
+
+
+class GATEncoder(nn.Module):
+    """src/models/gat_encoder.py:9-53, same submodule names and forward."""
+
+    def __init__(self, in_dim: int, hidden_dim: int, out_dim: int, edge_dim: int, heads: int = 4,
+                 num_layers: int = 3):
+        super().__init__()
+        self.num_layers = max(2, num_layers)
+        self.layers = nn.ModuleList()
+        self.layers.append(GATConv(in_dim, hidden_dim, heads=heads, concat=True, edge_dim=edge_dim))
+        for _ in range(self.num_layers - 2):
+            self.layers.append(GATConv(hidden_dim * heads, hidden_dim, heads=heads, concat=True, edge_dim=edge_dim))
+        self.layers.append(GATConv(hidden_dim * heads, out_dim, heads=1, concat=False, edge_dim=edge_dim))
+        self.input_proj = nn.Linear(in_dim, hidden_dim * heads)
+        self.norms = nn.ModuleList()
+        for i in range(self.num_layers):
+            self.norms.append(nn.LayerNorm(out_dim if i == self.num_layers - 1 else hidden_dim * heads))
+
+    def forward(self, x, edge_index, edge_attr, batch, return_attention: bool = False,
+                num_graphs: Optional[int] = None):
+        attn = None
+        for i, layer in enumerate(self.layers):
+            last = i == len(self.layers) - 1
+            if last and return_attention:
+                x, attn_info = layer(x, edge_index, edge_attr=edge_attr, return_attention_weights=True)
+                attn = attn_info[1]
+            elif last:
+                x = layer(x, edge_index, edge_attr=edge_attr)
+            else:
+                x_in = x
+                x = layer(x, edge_index, edge_attr=edge_attr)
+                if i == 0:
+                    x_in = self.input_proj(x_in)
+                x = self.norms[i](x)
+                x = torch.relu(x + x_in)
+                continue
+            x = self.norms[i](x)
+            x = F.elu(x)
+        g_mean = global_mean_pool(x, batch, num_graphs)
+        g_max = global_max_pool(x, batch, num_graphs)
+        return x, torch.cat([g_mean, g_max], dim=1), attn

@@ -1,0 +1,323 @@
+"""Discrete SAC with GAT encoders (src/rl/sac.py:23-291).
+
+Same classes, constructor arguments, forward signatures, update() batch tuple,
+returned metrics and checkpoint dict keys as the reference, so
+src/train.py-style callers and old checkpoints keep working.  Changes are in
+how the work maps to MI355X:
+
+* the edge MLP's first layer on cat([h_src, h_dst, e, ctx]) (sac.py:42-43,
+  1030 -> hidden) is evaluated as h @ W_src^T gathered at src + h @ W_dst^T at
+  dst + e @ W_e^T + (ctx @ W_ctx^T)[graph]: algebraically identical, but the
+  big GEMM runs per NODE (B*N rows) instead of per EDGE (B*E rows) -- 6x fewer
+  FLOPs on Sioux Falls, all in MFMA GEMMs;
+* PyG softmax / torch_scatter.scatter_sum over edge_batch become segment ops
+  (index_add / dense [B,E] reshapes when every graph has the same links);
+* update() runs the three independent backward passes (critic, actor, alpha:
+  none depends on another's optimizer step, sac.py:204-243) before any step,
+  so multi-GPU data parallelism needs ONE bucketed all-reduce of all
+  gradients per update (`grad_sync`, RCCL over xGMI) instead of three.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from ..models.gat_encoder import GATEncoder
+
+
+@dataclass
+class SACOutput:
+    action: int
+    log_prob: torch.Tensor
+    probs: torch.Tensor
+
+
+def scatter_sum(src: torch.Tensor, index: torch.Tensor, num: int) -> torch.Tensor:
+    out = torch.zeros(num, *src.shape[1:], device=src.device, dtype=src.dtype)
+    return out.index_add_(0, index, src)
+
+
+def segment_softmax(logits: torch.Tensor, index: torch.Tensor, num: int, per_segment: Optional[int] = None):
+    """torch_geometric.utils.softmax: exp(x - max_seg) / (sum_seg + 1e-16)."""
+    if per_segment is not None and logits.numel() == num * per_segment:
+        x = logits.view(num, per_segment)
+        ex = torch.exp(x - x.amax(dim=1, keepdim=True))
+        return (ex / (ex.sum(dim=1, keepdim=True) + 1e-16)).view(-1)
+    mx = torch.full((num,), float("-inf"), device=logits.device, dtype=logits.dtype)
+    mx = mx.scatter_reduce(0, index, logits, reduce="amax", include_self=True)
+    ex = torch.exp(logits - mx[index])
+    return ex / (scatter_sum(ex, index, num)[index] + 1e-16)
+
+
+class _EdgeHead(nn.Module):
+    """Owner of edge_mlp (state_dict keys edge_mlp.0.*, edge_mlp.2.*)."""
+
+    def __init__(self, embed: int, edge_in: int, hidden: int):
+        super().__init__()
+        self.embed, self.edge_in = embed, edge_in
+        self.edge_mlp = nn.Sequential(nn.Linear(embed * 4 + edge_in, hidden), nn.ReLU(), nn.Linear(hidden, 1))
+
+    def edge_scores(self, node_emb, global_ctx, edge_attr, src, dst, edge_batch):
+        W1, b1 = self.edge_mlp[0].weight, self.edge_mlp[0].bias
+        d, k = self.embed, self.edge_in
+        w_nodes = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)          # [2H, embed]
+        p = node_emb @ w_nodes.t()                                    # per-node projections
+        hdim = W1.shape[0]
+        z = p[src, :hdim] + p[dst, hdim:]
+        z = z + edge_attr @ W1[:, 2 * d:2 * d + k].t()
+        z = z + (global_ctx @ W1[:, 2 * d + k:].t() + b1)[edge_batch]
+        return self.edge_mlp[2](torch.relu(z)).squeeze(-1)
+
+
+class Actor(_EdgeHead):
+    def __init__(self, node_in: int, edge_in: int, hidden: int, embed: int, num_layers: int = 3):
+        super().__init__(embed, edge_in, hidden)
+        self.node_norm = nn.LayerNorm(node_in)
+        self.edge_norm = nn.LayerNorm(edge_in)
+        self.encoder = GATEncoder(node_in, hidden, embed, edge_dim=edge_in, num_layers=num_layers)
+
+    def forward(self, node_x, edge_index, edge_attr, action_mask, batch, return_attention: bool = False,
+                num_graphs: Optional[int] = None):
+        node_x = self.node_norm(node_x)
+        edge_attr = self.edge_norm(edge_attr)
+        B = num_graphs if num_graphs is not None else int(batch.max()) + 1
+        node_emb, global_ctx, attn = self.encoder(node_x, edge_index, edge_attr, batch,
+                                                  return_attention=return_attention, num_graphs=B)
+        src, dst = edge_index
+        edge_batch = batch[src]
+        logits = self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, edge_batch).float()
+        logits = logits.masked_fill(action_mask <= 0, -1e9)
+        probs = segment_softmax(logits, edge_batch, B, logits.numel() // B if logits.numel() % B == 0 else None)
+        return logits, probs, attn
+
+
+class Critic(_EdgeHead):
+    def __init__(self, node_in: int, edge_in: int, hidden: int, embed: int, num_layers: int = 3,
+                 encoder: GATEncoder | None = None):
+        super().__init__(embed, edge_in, hidden)
+        self.node_norm = nn.LayerNorm(node_in)
+        self.edge_norm = nn.LayerNorm(edge_in)
+        self.encoder = encoder if encoder is not None else GATEncoder(node_in, hidden, embed, edge_dim=edge_in,
+                                                                      num_layers=num_layers)
+
+    def forward(self, node_x, edge_index, edge_attr, batch, num_graphs: Optional[int] = None):
+        node_x = self.node_norm(node_x)
+        edge_attr = self.edge_norm(edge_attr)
+        B = num_graphs if num_graphs is not None else int(batch.max()) + 1
+        node_emb, global_ctx, _ = self.encoder(node_x, edge_index, edge_attr, batch, num_graphs=B)
+        src, dst = edge_index
+        return self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, batch[src]).float()
+
+
+class DiscreteSAC:
+    def __init__(self, node_in: int, edge_in: int, hidden: int, embed: int, num_layers: int = 3, lr: float = 3e-4,
+                 actor_lr: float | None = None, critic_lr: float | None = None, alpha_lr: float | None = None,
+                 grad_clip: float | None = None, gamma: float = 0.99, target_tau: float = 0.005,
+                 target_entropy: float = None, target_entropy_ratio: float = 0.1, alpha_init: float = 0.1,
+                 share_critic_encoder: bool = True, device=None, amp_dtype: Optional[torch.dtype] = None):
+        self.actor = Actor(node_in, edge_in, hidden, embed, num_layers=num_layers)
+        self.share_critic_encoder = share_critic_encoder
+        if share_critic_encoder:
+            self.critic_encoder = GATEncoder(node_in, hidden, embed, edge_dim=edge_in, num_layers=num_layers)
+            self.target_encoder = GATEncoder(node_in, hidden, embed, edge_dim=edge_in, num_layers=num_layers)
+            self.critic1 = Critic(node_in, edge_in, hidden, embed, num_layers, encoder=self.critic_encoder)
+            self.critic2 = Critic(node_in, edge_in, hidden, embed, num_layers, encoder=self.critic_encoder)
+            self.target1 = Critic(node_in, edge_in, hidden, embed, num_layers, encoder=self.target_encoder)
+            self.target2 = Critic(node_in, edge_in, hidden, embed, num_layers, encoder=self.target_encoder)
+            self.target_encoder.load_state_dict(self.critic_encoder.state_dict())
+        else:
+            self.critic1 = Critic(node_in, edge_in, hidden, embed, num_layers)
+            self.critic2 = Critic(node_in, edge_in, hidden, embed, num_layers)
+            self.target1 = Critic(node_in, edge_in, hidden, embed, num_layers)
+            self.target2 = Critic(node_in, edge_in, hidden, embed, num_layers)
+            self.target1.load_state_dict(self.critic1.state_dict())
+            self.target2.load_state_dict(self.critic2.state_dict())
+        if device is not None:
+            for m in (self.actor, self.critic1, self.critic2, self.target1, self.target2):
+                m.to(device)
+        actor_lr = lr if actor_lr is None else actor_lr
+        critic_lr = lr if critic_lr is None else critic_lr
+        alpha_lr = lr if alpha_lr is None else alpha_lr
+        self.actor_opt = torch.optim.Adam(self.actor.parameters(), lr=actor_lr)
+        if share_critic_encoder:
+            critic_params = (list(self.critic_encoder.parameters()) + list(self.critic1.edge_mlp.parameters())
+                             + list(self.critic2.edge_mlp.parameters()))
+        else:
+            critic_params = list(self.critic1.parameters()) + list(self.critic2.parameters())
+        self.critic_params = critic_params
+        self.critic_opt = torch.optim.Adam(critic_params, lr=critic_lr)
+        dev = device if device is not None else "cpu"
+        self.log_alpha = torch.tensor(float(np.log(max(alpha_init, 1e-8))), requires_grad=True, device=dev)
+        self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=alpha_lr)
+        self.gamma = gamma
+        self.target_tau = target_tau
+        self.target_entropy = target_entropy
+        self.target_entropy_ratio = target_entropy_ratio
+        self.grad_clip = grad_clip
+        self.amp_dtype = amp_dtype
+        # data-parallel hook: called once per update with every gradient tensor
+        self.grad_sync: Optional[Callable[[list], None]] = None
+
+    @property
+    def alpha(self):
+        return self.log_alpha.exp()
+
+    def _amp(self):
+        if self.amp_dtype is None:
+            return torch.autocast("cuda", enabled=False)
+        return torch.autocast("cuda", dtype=self.amp_dtype)
+
+    # ------------------------------------------------------------ acting
+    def select_action(self, node_x, edge_index, edge_attr, action_mask, deterministic: bool = False) -> SACOutput:
+        batch = torch.zeros(node_x.size(0), dtype=torch.long, device=node_x.device)
+        with torch.no_grad(), self._amp():
+            _, probs, _ = self.actor(node_x, edge_index, edge_attr, action_mask, batch, num_graphs=1)
+        if deterministic:
+            action = torch.argmax(probs).item()
+        else:
+            action = torch.multinomial(probs, 1).item()
+        log_prob = torch.log(probs[action] + 1e-8)
+        return SACOutput(action=action, log_prob=log_prob, probs=probs)
+
+    def select_actions(self, node_x, edge_index, edge_attr, action_mask, batch, num_graphs: int,
+                       deterministic: bool = False, generator=None) -> torch.Tensor:
+        """Batched acting for B graphs with identical link counts (VecRepairEnv):
+        one actor forward, one multinomial draw per graph, no host sync."""
+        with torch.no_grad(), self._amp():
+            _, probs, _ = self.actor(node_x, edge_index, edge_attr, action_mask, batch, num_graphs=num_graphs)
+        p = probs.view(num_graphs, -1)
+        if deterministic:
+            return p.argmax(dim=1)
+        return torch.multinomial(p, 1, generator=generator).squeeze(1)
+
+    # ------------------------------------------------------------ update
+    def update(self, batch, weights=None, alpha_max: float = None, sync_metrics: bool = True):
+        """sac.py:157-263.  sync_metrics=True returns python floats and a
+        td_errors list like the reference; False keeps them as device tensors
+        (no host synchronisation, for the vectorised trainer)."""
+        if isinstance(batch, list) and len(batch) == 1:
+            batch = batch[0]
+        (node_x, edge_index, edge_attr, action_mask, batch_vec, action, reward, next_node_x, next_edge_attr,
+         next_action_mask, next_batch_vec, done) = batch
+        B = reward.shape[0]
+        if weights is None:
+            weights_tensor = torch.ones_like(reward)
+        else:
+            weights_tensor = torch.as_tensor(weights, device=reward.device, dtype=reward.dtype)
+            if weights_tensor.dim() == 0:
+                weights_tensor = weights_tensor.unsqueeze(0).expand_as(reward)
+        edge_batch = batch_vec[edge_index[0]]
+        with self._amp():
+            with torch.no_grad():
+                _, next_probs, _ = self.actor(next_node_x, edge_index, next_edge_attr, next_action_mask,
+                                              next_batch_vec, num_graphs=B)
+                q_next = torch.min(self.target1(next_node_x, edge_index, next_edge_attr, next_batch_vec, B),
+                                   self.target2(next_node_x, edge_index, next_edge_attr, next_batch_vec, B))
+                v_next = scatter_sum(next_probs * (q_next - self.alpha * torch.log(next_probs + 1e-8)), edge_batch, B)
+                target = reward + (1.0 - done) * self.gamma * v_next
+            q1_all = self.critic1(node_x, edge_index, edge_attr, batch_vec, B)
+            q2_all = self.critic2(node_x, edge_index, edge_attr, batch_vec, B)
+            q1 = q1_all[action]
+            q2 = q2_all[action]
+            td_error = (target - q1).detach().abs()
+            loss1 = F.mse_loss(q1, target, reduction="none")
+            loss2 = F.mse_loss(q2, target, reduction="none")
+            critic_loss = (weights_tensor * (loss1 + loss2)).mean()
+            logits, probs, _ = self.actor(node_x, edge_index, edge_attr, action_mask, batch_vec, num_graphs=B)
+        q_all = torch.min(q1_all, q2_all).detach()
+        # alpha detached: the reference zeroes log_alpha.grad (alpha_opt.zero_grad,
+        # sac.py:236) after actor_loss.backward, so this term never reaches it
+        actor_terms = probs * (self.alpha.detach() * torch.log(probs + 1e-8) - q_all)
+        actor_loss = scatter_sum(actor_terms, edge_batch, B).mean()
+        if self.target_entropy is None:
+            valid = scatter_sum((action_mask > 0).float(), edge_batch, B)
+            target_entropy = (self.target_entropy_ratio * torch.log(valid + 1e-8)).mean()
+        else:
+            target_entropy = self.target_entropy
+        log_probs = torch.log(probs + 1e-8).detach()
+        alpha_term = scatter_sum(probs.detach() * (log_probs + target_entropy), edge_batch, B)
+        alpha_loss = -(self.log_alpha * alpha_term).mean()
+        entropy = scatter_sum(-(probs.detach() * log_probs), edge_batch, B).mean()
+        q_taken = torch.min(q1, q2).detach()
+        logp_mean = scatter_sum(probs.detach() * log_probs, edge_batch, B).mean().detach()
+
+        # three independent backward passes, then (multi-GPU) ONE bucketed all-reduce
+        self.critic_opt.zero_grad(set_to_none=False)
+        self.actor_opt.zero_grad(set_to_none=False)
+        self.alpha_opt.zero_grad(set_to_none=False)
+        critic_loss.backward()
+        actor_loss.backward()
+        alpha_loss.backward()
+        if self.grad_sync is not None:
+            grads = [p.grad for p in self._all_params() if p.grad is not None]
+            self.grad_sync(grads)
+        clip = self.grad_clip is not None and self.grad_clip > 0
+        if clip:
+            torch.nn.utils.clip_grad_norm_(list(self.critic1.parameters()) + list(self.critic2.parameters()),
+                                           max_norm=self.grad_clip)
+        self.critic_opt.step()
+        if clip:
+            torch.nn.utils.clip_grad_norm_(self.actor.parameters(), max_norm=self.grad_clip)
+        self.actor_opt.step()
+        if clip:
+            torch.nn.utils.clip_grad_norm_([self.log_alpha], max_norm=self.grad_clip)
+        self.alpha_opt.step()
+        with torch.no_grad():
+            if alpha_max is not None:
+                self.log_alpha.clamp_(max=float(np.log(alpha_max)))
+            self.log_alpha.clamp_(min=float(np.log(0.01)))
+        if self.share_critic_encoder:
+            self._soft_update(self.critic_encoder, self.target_encoder)
+            self._soft_update(self.critic1.edge_mlp, self.target1.edge_mlp)
+            self._soft_update(self.critic2.edge_mlp, self.target2.edge_mlp)
+        else:
+            self._soft_update(self.critic1, self.target1)
+            self._soft_update(self.critic2, self.target2)
+        out = {
+            "critic_loss": critic_loss.detach(),
+            "actor_loss": actor_loss.detach(),
+            "alpha": self.alpha.detach(),
+            "alpha_loss": alpha_loss.detach(),
+            "policy_entropy": entropy,
+            "q_taken": q_taken.mean(),
+            "q_mean": q_all.mean(),
+            "logp_mean": logp_mean,
+            "td_errors": td_error,
+        }
+        if sync_metrics:
+            out = {k: (v.cpu().numpy().tolist() if k == "td_errors" else float(v)) for k, v in out.items()}
+        return out
+
+    def _all_params(self):
+        seen, out = set(), []
+        for p in list(self.critic_params) + list(self.actor.parameters()) + [self.log_alpha]:
+            if id(p) not in seen:
+                seen.add(id(p))
+                out.append(p)
+        return out
+
+    def save(self, path: str):
+        torch.save({"actor": self.actor.state_dict(), "critic1": self.critic1.state_dict(),
+                    "critic2": self.critic2.state_dict(), "target1": self.target1.state_dict(),
+                    "target2": self.target2.state_dict(), "log_alpha": self.log_alpha.detach().cpu()}, path)
+
+    def load(self, path: str, map_location: str = "cpu"):
+        state = torch.load(path, map_location=map_location, weights_only=True)
+        self.actor.load_state_dict(state["actor"])
+        self.critic1.load_state_dict(state["critic1"])
+        self.critic2.load_state_dict(state["critic2"])
+        self.target1.load_state_dict(state["target1"])
+        self.target2.load_state_dict(state["target2"])
+        self.log_alpha = state["log_alpha"].to(map_location).requires_grad_()
+        lr = self.alpha_opt.param_groups[0]["lr"]
+        self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=lr)
+
+    @torch.no_grad()
+    def _soft_update(self, src, tgt):
+        for p, tp in zip(src.parameters(), tgt.parameters()):
+            tp.data.copy_(tp.data * (1.0 - self.target_tau) + p.data * self.target_tau)
