@@ -54,6 +54,30 @@ def segment_softmax(logits: torch.Tensor, index: torch.Tensor, num: int, per_seg
     return ex / (scatter_sum(ex, index, num)[index] + 1e-16)
 
 
+@torch.no_grad()
+def clip_grad_norm_listwise_(params, max_norm: float):
+    """torch.nn.utils.clip_grad_norm_ with the reference's list semantics made
+    deterministic.  The reference clips list(critic1.parameters()) +
+    list(critic2.parameters()) (sac.py:224-227); with a shared critic encoder
+    that list holds the encoder's gradients twice.  Sequentially (torch's
+    per-tensor loop) each duplicate is counted twice in the norm and scaled
+    twice; torch's fused CUDA path instead scales the same tensor from two
+    workgroups at once (a read-modify-write race: g*c or g*c^2).  This helper
+    always applies the sequential semantics."""
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return torch.zeros(())
+    total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g, 2.0) for g in grads]), 2.0)
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    mult = {}
+    for p in params:
+        if p.grad is not None:
+            mult[id(p)] = (p, mult.get(id(p), (p, 0))[1] + 1)
+    for p, n in mult.values():
+        p.grad.mul_(coef if n == 1 else coef ** n)
+    return total
+
+
 class _EdgeHead(nn.Module):
     """Owner of edge_mlp (state_dict keys edge_mlp.0.*, edge_mlp.2.*)."""
 
@@ -258,14 +282,13 @@ class DiscreteSAC:
             self.grad_sync(grads)
         clip = self.grad_clip is not None and self.grad_clip > 0
         if clip:
-            torch.nn.utils.clip_grad_norm_(list(self.critic1.parameters()) + list(self.critic2.parameters()),
-                                           max_norm=self.grad_clip)
+            clip_grad_norm_listwise_(list(self.critic1.parameters()) + list(self.critic2.parameters()), self.grad_clip)
         self.critic_opt.step()
         if clip:
-            torch.nn.utils.clip_grad_norm_(self.actor.parameters(), max_norm=self.grad_clip)
+            clip_grad_norm_listwise_(list(self.actor.parameters()), self.grad_clip)
         self.actor_opt.step()
         if clip:
-            torch.nn.utils.clip_grad_norm_([self.log_alpha], max_norm=self.grad_clip)
+            clip_grad_norm_listwise_([self.log_alpha], self.grad_clip)
         self.alpha_opt.step()
         with torch.no_grad():
             if alpha_max is not None:
