@@ -169,6 +169,20 @@ int trx_gat_backward(int32_t num_nodes, int32_t heads, int32_t channels, const i
                      const float* alpha, const float* grad_out, float* grad_xh, float* grad_a_src, float* grad_a_dst,
                      float* grad_a_edge, void* stream);
 
+/* ------------------------------------------------- prioritized replay
+ * Sum tree of src/train.py:27-91 (ReplayBuffer) on the device: tree[1] is the
+ * root, leaf i is tree[capacity + i], children of k are 2k, 2k+1; float64.
+ * trx_per_update: tree[capacity + idx[k]] = priority[k] (priority already
+ *   raised to alpha; idx distinct -- the caller keeps the last of duplicates)
+ *   and every ancestor recomputed as the sum of its children.
+ * trx_per_sample: for each u[k] in [0,1): r = u[k]*tree[1], descend with
+ *   `r <= tree[left] ? left : (r -= tree[left], right)` (train.py:67-79);
+ *   out_idx[k] = leaf - capacity, out_priority[k] = tree[leaf]. */
+int trx_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* priority, int32_t n,
+                   void* stream);
+int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
+                   double* out_priority, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

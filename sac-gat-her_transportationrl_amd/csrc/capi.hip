@@ -319,4 +319,21 @@ int trx_gat_backward(int32_t num_nodes, int32_t heads, int32_t channels, const i
     return TRX_OK;
 }
 
+int trx_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* priority, int32_t n,
+                   void* stream) {
+    if (!tree || capacity <= 0 || n < 0 || (n > 0 && (!idx || !priority))) return fail(TRX_EINVAL, "per_update args");
+    hipError_t e = trx::launch_per_update(tree, capacity, idx, priority, n, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "per_update launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
+                   double* out_priority, void* stream) {
+    if (!tree || capacity <= 0 || n < 0 || (n > 0 && (!u || !out_idx || !out_priority)))
+        return fail(TRX_EINVAL, "per_sample args");
+    hipError_t e = trx::launch_per_sample(tree, capacity, u, n, out_idx, out_priority, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "per_sample launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 }  // extern "C"

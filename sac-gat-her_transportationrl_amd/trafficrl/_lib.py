@@ -21,7 +21,7 @@ REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "
 EXPORTS = (
     "trx_abi_version", "trx_last_error", "trx_graph_create", "trx_graph_destroy", "trx_graph_info",
     "trx_workspace_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe", "trx_gat_forward",
-    "trx_gat_backward",
+    "trx_gat_backward", "trx_per_update", "trx_per_sample",
 )
 
 
@@ -79,8 +79,10 @@ def load():
                                   _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _vp]
     L.trx_gat_backward.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp,
                                    ctypes.c_int32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.trx_per_update.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int32, _vp]
+    L.trx_per_sample.argtypes = [_vp, ctypes.c_int64, _vp, ctypes.c_int32, _vp, _vp, _vp]
     for name in ("trx_graph_create", "trx_graph_destroy", "trx_graph_info", "trx_assign", "trx_reset", "trx_step",
-                 "trx_observe", "trx_gat_forward", "trx_gat_backward"):
+                 "trx_observe", "trx_gat_forward", "trx_gat_backward", "trx_per_update", "trx_per_sample"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != 1:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != 1")

@@ -164,6 +164,17 @@ class VecRepairEnv:
                                _lib.ptr(env_mask), _lib.ptr(self.workspace), self._stream()), "trx_reset")
         return self.observe() if observe else None
 
+    def reset_where(self, env_mask: torch.Tensor, damaged: torch.Tensor, observe: bool = False):
+        """Reset the envs where env_mask (bool/uint8 [B]) is set, with damage
+        rows taken from `damaged` [B,E]; fully on device (no host sync)."""
+        m = env_mask.to(device=self.device, dtype=torch.bool)
+        self.damaged.copy_(torch.where(m[:, None], damaged.to(self.damaged.dtype), self.damaged))
+        L = _lib.load()
+        mu8 = m.to(torch.uint8).contiguous()
+        _lib.check(L.trx_reset(self.graph.handle, ctypes.byref(self.params), self.num_envs, ctypes.byref(self._state),
+                               _lib.ptr(mu8), _lib.ptr(self.workspace), self._stream()), "trx_reset")
+        return self.observe() if observe else None
+
     def step(self, actions: torch.Tensor, observe: bool = True, check: bool = True):
         """Batched RepairEnv.step.  Returns (obs, reward[B] f64, done[B] bool, info)."""
         a = actions.to(device=self.device, dtype=torch.int32).contiguous()

@@ -1,0 +1,184 @@
+"""Device-resident prioritized replay + HER relabelling (src/train.py:27-91,
+125-135, 805-823).
+
+Transitions of fixed-topology graphs are stored as dense device tensors
+(structure of arrays, [capacity, ...]); the PER sum tree runs on the GPU
+(trx_per_update / trx_per_sample, csrc/replay_kernel.hip).  Semantics kept
+from the reference ReplayBuffer:
+  * add(): priority = max_priority, then abs()+eps, max_priority updated,
+    leaf = priority**alpha -- so a batch of k adds gets max_p+eps, max_p+2eps,
+    ... exactly like k sequential reference adds;
+  * sample(): r = u * total, descend `r <= tree[left]`; probs = leaf/total,
+    weights = (size * probs)^-beta / max;
+  * update_priorities(): abs(err)+eps, max_priority, **alpha; for duplicate
+    indices the last one wins (sequential semantics).
+HER (train.py:805-823) reproduces the reference's behaviour including two
+quirks, flagged here: apply_goal writes the goal into edge-feature column -1
+(edge_id_norm; get_state's goal column is 4, repair_env.py:799-808), and the
+relabelled `done` = is_goal_complete(1 - mask', mask') is always 1.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from .. import _lib
+
+
+@dataclass
+class Sample:
+    idx: torch.Tensor          # [bs] int64 slots
+    weights: torch.Tensor      # [bs] float32 importance weights
+    node_x: torch.Tensor       # [bs, N, 4]
+    edge_x: torch.Tensor       # [bs, E, 6]
+    mask: torch.Tensor         # [bs, E]
+    action: torch.Tensor       # [bs] int64 (local link id)
+    reward: torch.Tensor       # [bs] float32 (scaled)
+    next_node_x: torch.Tensor
+    next_edge_x: torch.Tensor
+    next_mask: torch.Tensor
+    done: torch.Tensor         # [bs] float32
+    goal: torch.Tensor         # [bs, E]
+    prev_tstt: torch.Tensor    # [bs] float64
+    next_tstt: torch.Tensor
+    init_tstt: torch.Tensor
+
+
+def _last_occurrence(idx: torch.Tensor) -> torch.Tensor:
+    """Boolean mask keeping the last occurrence of each value (stable)."""
+    n = idx.numel()
+    order = torch.argsort(idx * (n + 1) + torch.arange(n, device=idx.device))
+    s = idx[order]
+    last = torch.ones(n, dtype=torch.bool, device=idx.device)
+    last[:-1] = s[1:] != s[:-1]
+    keep = torch.zeros(n, dtype=torch.bool, device=idx.device)
+    keep[order[last]] = True
+    return keep
+
+
+class DeviceReplay:
+    def __init__(self, capacity: int, num_nodes: int, num_edges: int, node_dim: int = 4, edge_dim: int = 6,
+                 alpha: float = 0.6, beta: float = 0.4, eps: float = 1e-6, device="cuda"):
+        self.capacity = int(capacity)
+        self.alpha, self.beta, self.eps = alpha, beta, eps
+        dev = self.device = torch.device(device)
+        C, N, E = self.capacity, num_nodes, num_edges
+        f32 = dict(device=dev, dtype=torch.float32)
+        self.node_x = torch.zeros(C, N, node_dim, **f32)
+        self.edge_x = torch.zeros(C, E, edge_dim, **f32)
+        self.mask = torch.zeros(C, E, **f32)
+        self.next_node_x = torch.zeros(C, N, node_dim, **f32)
+        self.next_edge_x = torch.zeros(C, E, edge_dim, **f32)
+        self.next_mask = torch.zeros(C, E, **f32)
+        self.goal = torch.zeros(C, E, **f32)
+        self.action = torch.zeros(C, dtype=torch.int64, device=dev)
+        self.reward = torch.zeros(C, **f32)
+        self.done = torch.zeros(C, **f32)
+        self.prev_tstt = torch.zeros(C, dtype=torch.float64, device=dev)
+        self.next_tstt = torch.zeros(C, dtype=torch.float64, device=dev)
+        self.init_tstt = torch.zeros(C, dtype=torch.float64, device=dev)
+        self.tree = torch.zeros(2 * C, dtype=torch.float64, device=dev)
+        self.max_priority = torch.ones((), dtype=torch.float64, device=dev)
+        self.ptr = 0
+        self.size = 0
+
+    def _set(self, idx: torch.Tensor, leaf: torch.Tensor):
+        keep = _last_occurrence(idx)
+        idx = idx[keep].contiguous()
+        leaf = leaf[keep].to(torch.float64).contiguous()
+        L = _lib.load()
+        _lib.check(L.trx_per_update(_lib.ptr(self.tree), self.capacity, _lib.ptr(idx), _lib.ptr(leaf), idx.numel(),
+                                    _lib.stream_ptr(self.device)), "trx_per_update")
+
+    @property
+    def total(self) -> torch.Tensor:
+        return self.tree[1]
+
+    def add_batch(self, node_x, edge_x, mask, action, reward, next_node_x, next_edge_x, next_mask, done, goal,
+                  prev_tstt, next_tstt, init_tstt):
+        B = action.shape[0]
+        idx = (self.ptr + torch.arange(B, device=self.device)) % self.capacity
+        for dst, src in ((self.node_x, node_x), (self.edge_x, edge_x), (self.mask, mask),
+                         (self.next_node_x, next_node_x), (self.next_edge_x, next_edge_x),
+                         (self.next_mask, next_mask), (self.goal, goal)):
+            dst.index_copy_(0, idx, src.to(dst.dtype))
+        self.action.index_copy_(0, idx, action.to(torch.int64))
+        self.reward.index_copy_(0, idx, reward.to(torch.float32))
+        self.done.index_copy_(0, idx, done.to(torch.float32))
+        self.prev_tstt.index_copy_(0, idx, prev_tstt.to(torch.float64))
+        self.next_tstt.index_copy_(0, idx, next_tstt.to(torch.float64))
+        self.init_tstt.index_copy_(0, idx, init_tstt.to(torch.float64))
+        # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
+        pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
+        self.max_priority = pr[-1].clone()
+        self._set(idx, pr ** self.alpha)
+        self.ptr = (self.ptr + B) % self.capacity
+        self.size = min(self.size + B, self.capacity)
+
+    def sample(self, batch_size: int, generator: Optional[torch.Generator] = None) -> Sample:
+        if self.size == 0:
+            raise ValueError("Cannot sample from an empty replay buffer.")
+        u = torch.rand(batch_size, dtype=torch.float64, device=self.device, generator=generator)
+        idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
+        pri = torch.empty(batch_size, dtype=torch.float64, device=self.device)
+        L = _lib.load()
+        _lib.check(L.trx_per_sample(_lib.ptr(self.tree), self.capacity, _lib.ptr(u), batch_size, _lib.ptr(idx),
+                                    _lib.ptr(pri), _lib.stream_ptr(self.device)), "trx_per_sample")
+        probs = pri / self.total
+        w = (self.size * probs) ** (-self.beta)
+        w = w / torch.clamp(w.max(), min=1e-300)
+        return Sample(idx, w.float(), self.node_x[idx], self.edge_x[idx], self.mask[idx], self.action[idx],
+                      self.reward[idx], self.next_node_x[idx], self.next_edge_x[idx], self.next_mask[idx],
+                      self.done[idx], self.goal[idx], self.prev_tstt[idx], self.next_tstt[idx], self.init_tstt[idx])
+
+    def update_priorities(self, idx: torch.Tensor, td_errors: torch.Tensor):
+        pr = td_errors.detach().to(torch.float64).abs() + self.eps
+        self.max_priority = torch.maximum(self.max_priority, pr.max())
+        self._set(idx, pr ** self.alpha)
+
+
+def reward_with_goal(mode, prev, curr, init, complete, alpha=1.0, beta=10.0, gamma=0.1, clip=0.0):
+    """Vectorised RepairEnv.compute_reward_with_goal (repair_env.py:244-291), float64."""
+    bonus = torch.where(complete, torch.full_like(prev, beta), torch.zeros_like(prev))
+    if mode in ("minimize_tstt", "rel_improve"):
+        bb = torch.clamp(init, min=1.0)
+        if mode == "minimize_tstt":
+            r = -alpha * (curr / bb)
+        else:
+            r = alpha * (((prev - curr) / bb) * 100.0) - 1.0 * (curr / bb)
+        r = r + bonus
+    else:
+        if mode == "neg_tstt":
+            delta = -curr
+        elif mode == "log_delta":
+            delta = torch.log10(torch.clamp(prev, min=1.0)) - torch.log10(torch.clamp(curr, min=1.0))
+        else:
+            delta = prev - curr
+        r = alpha * delta + bonus - gamma
+    if clip and clip > 0:
+        r = torch.clamp(r, -clip, clip)
+    return r
+
+
+def her_relabel(s: Sample, her_ratio: float, reward_mode: str, reward_scale: float, alpha: float, beta: float,
+                gamma: float, clip: float, generator: Optional[torch.Generator] = None, goal_column: int = -1):
+    """train.py:805-823 on a sampled batch (in place).  goal_column=-1
+    reproduces apply_goal (train.py:127); 4 would write the real goal column."""
+    if her_ratio <= 0:
+        return s
+    bs = s.action.shape[0]
+    pick = torch.rand(bs, device=s.action.device, generator=generator) < her_ratio
+    goal = 1.0 - s.next_mask
+    complete = ((goal * s.next_mask).sum(dim=1) == 0)
+    r = reward_with_goal(reward_mode, s.prev_tstt, s.next_tstt, s.init_tstt, complete, alpha, beta, gamma, clip)
+    r = (r * reward_scale).float()
+    s.reward = torch.where(pick, r, s.reward)
+    s.done = torch.where(pick, complete.float(), s.done)
+    s.goal = torch.where(pick[:, None], goal, s.goal)
+    s.edge_x = s.edge_x.clone()
+    s.next_edge_x = s.next_edge_x.clone()
+    s.edge_x[pick, :, goal_column] = goal[pick]
+    s.next_edge_x[pick, :, goal_column] = goal[pick]
+    return s

@@ -1,0 +1,341 @@
+"""Vectorised GAT-SAC trainer: the capabilities of src/train.py:216-1193 on
+device-resident envs.
+
+Same YAML keys as the reference configs (configs/sioux_falls.yaml): damage
+(damaged_ratio, fixed_damage, fixed_damage_seed, capacity_damage), assignment
+(assignment_iters, assignment_method), reward (reward_mode, reward_alpha/beta/
+gamma/clip, reward_scale, unassigned_penalty), SAC (hidden_dim, embed_dim,
+gat_layers, lr, actor_lr, critic_lr, alpha_lr, gamma, target_tau, grad_clip,
+alpha_init, alpha_max, target_entropy_ratio, share_critic_encoder), replay
+(buffer_size, batch_size, batch_start, update_every, updates_per_step,
+per_alpha, per_beta, per_eps, her_ratio), loop (episodes, max_steps,
+eval_every, eval_seeds, early_stop_patience, seed, output_dir).  New keys:
+num_envs (envs stepped in lockstep per GPU; the reference's 1 env or
+num_workers CPU processes, train.py:730-913) and amp (bf16 autocast for the
+GAT/SAC GEMMs).
+
+One iteration = every env takes one step: batched actor forward (one
+multinomial per env) -> trx_step + trx_observe -> transitions appended to the
+device replay.  Every `update_every` iterations, `updates_per_step` SAC
+updates on PER samples (+HER).  Multi-GPU (torchrun): envs and replay are
+per-rank shards; the only collective is one bucketed all-reduce of all SAC
+gradients per update (RCCL over xGMI) plus a few episode-metric reductions.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import math
+import os
+import time
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from .data.tntp_parser import load_graph_data, sioux_falls
+from .env.vec_env import VecRepairEnv
+from .rl.replay import DeviceReplay, her_relabel
+from .rl.sac import DiscreteSAC
+
+DEFAULTS: Dict = dict(
+    damaged_ratio=0.3, assignment_iters=30, assignment_method="msa", reward_mode="rel_improve", reward_alpha=1.0,
+    reward_beta=0.0, reward_gamma=0.0, reward_clip=2.0, reward_scale=0.5, capacity_damage=1e-3,
+    unassigned_penalty=1e4, fixed_damage=True, fixed_damage_seed=42, episodes=2000, max_steps=100,
+    buffer_size=1_000_000, batch_start=2000, batch_size=256, update_every=4, updates_per_step=1, per_alpha=0.6,
+    per_beta=0.4, per_eps=1e-6, her_ratio=0.0, hidden_dim=256, embed_dim=256, gat_layers=3, lr=1e-4,
+    actor_lr=None, critic_lr=None, alpha_lr=None, gamma=0.99, target_tau=0.001, grad_clip=1.0,
+    share_critic_encoder=False, alpha_init=0.1, alpha_max=2.5, target_entropy_ratio=0.2, eval_every=20,
+    eval_seeds=[42], early_stop_patience=2000, seed=42, output_dir="outputs", num_envs=256, amp="bf16",
+    log_every=10, save_every=50, net_path=None, trips_path=None,
+)
+
+
+def load_config(path: Optional[str]) -> Dict:
+    cfg = dict(DEFAULTS)
+    if path:
+        import yaml
+        with open(path) as fh:
+            cfg.update(yaml.safe_load(fh) or {})
+    if os.environ.get("SEED_OVERRIDE") is not None:  # train.py:218-222
+        cfg["seed"] = int(os.environ["SEED_OVERRIDE"])
+        cfg["output_dir"] = os.path.join(cfg["output_dir"], f"seed_{cfg['seed']}")
+    return cfg
+
+
+def batched_topology(edge_index: torch.Tensor, num_nodes: int, B: int):
+    """edge_index / batch vector of B copies of one graph (PyG Batch layout)."""
+    E = edge_index.shape[1]
+    dev = edge_index.device
+    off = (torch.arange(B, device=dev) * num_nodes).repeat_interleave(E)
+    ei = torch.stack([edge_index[0].repeat(B) + off, edge_index[1].repeat(B) + off])
+    batch = torch.arange(B, device=dev).repeat_interleave(num_nodes)
+    return ei, batch
+
+
+class GradAllReduce:
+    """One bucketed all-reduce (sum / world) of every gradient per update."""
+
+    def __init__(self, world: int):
+        import torch.distributed as dist
+        self.dist, self.world = dist, world
+
+    def __call__(self, grads):
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        self.dist.all_reduce(flat)
+        flat.div_(self.world)
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n
+
+
+class Trainer:
+    def __init__(self, cfg: Dict, device="cuda", rank: int = 0, world: int = 1, log: bool = True):
+        self.cfg, self.rank, self.world = cfg, rank, world
+        self.device = torch.device(device)
+        torch.manual_seed(int(cfg["seed"]) + rank)
+        np.random.seed(int(cfg["seed"]) + rank)
+        self.gen = torch.Generator(device=self.device).manual_seed(int(cfg["seed"]) * 1000 + rank)
+        self.logger = logging.getLogger("trafficrl.train")
+        if log and rank == 0 and not self.logger.handlers:
+            os.makedirs(os.path.join(cfg["output_dir"], "logs"), exist_ok=True)
+            fh = logging.FileHandler(os.path.join(cfg["output_dir"], "logs", "training.log"))
+            fh.setFormatter(logging.Formatter("%(asctime)s - %(message)s"))
+            self.logger.addHandler(fh)
+            self.logger.addHandler(logging.StreamHandler())
+            self.logger.setLevel(logging.INFO)
+        gd = (load_graph_data(cfg["net_path"], cfg["trips_path"]) if cfg.get("net_path") else sioux_falls())
+        B = int(cfg["num_envs"])
+        self.B = B
+        seeds = [int(cfg["seed"]) * 100003 + rank * B + i for i in range(B)]
+        self.env = VecRepairEnv(
+            gd, B, device=self.device, damaged_ratio=cfg["damaged_ratio"], assignment_iters=cfg["assignment_iters"],
+            assignment_method=cfg["assignment_method"], reward_mode=cfg["reward_mode"],
+            reward_alpha=cfg["reward_alpha"], reward_beta=cfg["reward_beta"], reward_gamma=cfg["reward_gamma"],
+            reward_clip=cfg["reward_clip"], capacity_damage=cfg["capacity_damage"],
+            unassigned_penalty=cfg["unassigned_penalty"], fixed_damage=cfg["fixed_damage"],
+            fixed_damage_seed=cfg["fixed_damage_seed"], seeds=seeds, reset=False)
+        self.N, self.E = self.env.num_nodes, self.env.num_edges
+        amp = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(str(cfg.get("amp")).lower())
+        self.agent = DiscreteSAC(
+            4, 6, cfg["hidden_dim"], cfg["embed_dim"], num_layers=cfg["gat_layers"], lr=cfg["lr"],
+            actor_lr=cfg["actor_lr"], critic_lr=cfg["critic_lr"], alpha_lr=cfg["alpha_lr"],
+            grad_clip=cfg["grad_clip"], gamma=cfg["gamma"], target_tau=cfg["target_tau"],
+            share_critic_encoder=cfg["share_critic_encoder"], alpha_init=cfg["alpha_init"],
+            target_entropy_ratio=cfg["target_entropy_ratio"], device=self.device, amp_dtype=amp)
+        if world > 1:
+            import torch.distributed as dist
+            for m in (self.agent.actor, self.agent.critic1, self.agent.critic2, self.agent.target1,
+                      self.agent.target2):
+                for t in list(m.parameters()) + list(m.buffers()):
+                    dist.broadcast(t.data, src=0)
+            dist.broadcast(self.agent.log_alpha.data, src=0)
+            self.agent.grad_sync = GradAllReduce(world)
+        cap = min(int(cfg["buffer_size"]), max(int(cfg["buffer_size"]) // world, B))
+        self.replay = DeviceReplay(cap, self.N, self.E, alpha=cfg["per_alpha"], beta=cfg["per_beta"],
+                                   eps=cfg["per_eps"], device=self.device)
+        ei = self.env.edge_index
+        self.act_ei, self.act_batch = batched_topology(ei, self.N, B)
+        bs = int(cfg["batch_size"])
+        self.upd_ei, self.upd_batch = batched_topology(ei, self.N, bs)
+        self.fixed_mask = None
+        # per-env episode accumulators (device)
+        self.ep_reward = torch.zeros(B, dtype=torch.float64, device=self.device)
+        self.ep_tstt_sum = torch.zeros(B, dtype=torch.float64, device=self.device)
+        self.ep_auc = torch.zeros(B, dtype=torch.float64, device=self.device)
+        self.ep_prev_tstt = torch.zeros(B, dtype=torch.float64, device=self.device)
+        self.ep_len = torch.zeros(B, dtype=torch.int64, device=self.device)
+        self.episodes_done = 0
+        self.history = []
+        self.last_losses: Dict = {}
+
+    # ------------------------------------------------------------ acting
+    def act(self, obs, deterministic=False):
+        B = self.B
+        return self.agent.select_actions(obs.node_x.reshape(B * self.N, 4), self.act_ei,
+                                         obs.edge_x.reshape(B * self.E, 6), obs.action_mask.reshape(-1),
+                                         self.act_batch, num_graphs=B, deterministic=deterministic,
+                                         generator=self.gen)
+
+    def _reset_envs(self, done_mask: Optional[torch.Tensor]):
+        env = self.env
+        if done_mask is None:
+            env.reset(observe=False)
+            if self.cfg["fixed_damage"]:
+                self.fixed_mask = env.damaged[:1].clone()
+            self.ep_prev_tstt.copy_(env.tstt)
+            return
+        if self.cfg["fixed_damage"] and self.fixed_mask is not None:
+            # every env has the same damage: reset on device, no host round trip
+            env.reset_where(done_mask, self.fixed_mask.expand(self.B, -1))
+        else:
+            ids = torch.nonzero(done_mask).squeeze(1).tolist()
+            if ids:
+                env.reset(env_ids=ids, observe=False)
+        self.ep_prev_tstt = torch.where(done_mask, env.tstt, self.ep_prev_tstt)
+
+    # ------------------------------------------------------------ update
+    def update(self):
+        cfg = self.cfg
+        bs = int(cfg["batch_size"])
+        s = self.replay.sample(bs, generator=self.gen)
+        s = her_relabel(s, cfg["her_ratio"], cfg["reward_mode"], cfg["reward_scale"], cfg["reward_alpha"],
+                        cfg["reward_beta"], cfg["reward_gamma"], cfg["reward_clip"], generator=self.gen)
+        E, N = self.E, self.N
+        action = torch.arange(bs, device=self.device) * E + s.action
+        batch = (s.node_x.reshape(bs * N, -1), self.upd_ei, s.edge_x.reshape(bs * E, -1), s.mask.reshape(-1),
+                 self.upd_batch, action, s.reward, s.next_node_x.reshape(bs * N, -1), s.next_edge_x.reshape(bs * E, -1),
+                 s.next_mask.reshape(-1), self.upd_batch, s.done)
+        out = self.agent.update(batch, weights=s.weights, alpha_max=cfg.get("alpha_max"), sync_metrics=False)
+        self.replay.update_priorities(s.idx, out["td_errors"])
+        self.last_losses = out
+        return out
+
+    # -------------------------------------------------------------- loop
+    def iteration(self, obs, it: int):
+        cfg, env = self.cfg, self.env
+        actions = self.act(obs)
+        prev_obs = (obs.node_x.clone(), obs.edge_x.clone(), obs.action_mask.clone())
+        goal = env.goal.clone()
+        prev_tstt = env.tstt.clone()
+        next_obs, reward, done, info = env.step(actions.to(torch.int32), check=False)
+        scaled = reward * cfg["reward_scale"]
+        self.ep_len += 1
+        trunc = (self.ep_len >= int(cfg["max_steps"])) if cfg["max_steps"] > 0 else torch.zeros_like(done)
+        self.replay.add_batch(prev_obs[0], prev_obs[1], prev_obs[2], actions, scaled, next_obs.node_x,
+                              next_obs.edge_x, next_obs.action_mask, done.float(), goal, prev_tstt, env.tstt,
+                              env.initial_tstt)
+        self.ep_reward += scaled
+        self.ep_tstt_sum += env.tstt
+        self.ep_auc += 0.5 * (self.ep_prev_tstt + env.tstt) * (self.ep_len > 1)
+        self.ep_prev_tstt.copy_(env.tstt)
+        if self.replay.size > int(cfg["batch_start"]) and it % int(cfg["update_every"]) == 0:
+            for _ in range(int(cfg["updates_per_step"])):
+                self.update()
+        finished = done | trunc
+        return next_obs, finished
+
+    def record(self, finished: torch.Tensor):
+        n = int(finished.sum())
+        if n == 0:
+            return
+        f = finished
+        rec = {
+            "episodes": n,
+            "reward": float(self.ep_reward[f].mean()),
+            "tstt_mean": float((self.ep_tstt_sum[f] / self.ep_len[f]).mean()),
+            "tstt_last": float(self.env.tstt[f].mean()),
+            "auc": float(self.ep_auc[f].mean()),
+        }
+        self.episodes_done += n
+        self.history.append(rec)
+        for t in (self.ep_reward, self.ep_tstt_sum, self.ep_auc):
+            t.masked_fill_(f, 0.0)
+        self.ep_len.masked_fill_(f, 0)
+
+    def evaluate(self, seeds=None) -> Dict:
+        """Deterministic-policy episodes (src/train.py:590-664) on a separate env."""
+        cfg = self.cfg
+        seeds = seeds or cfg["eval_seeds"]
+        ev = VecRepairEnv(self.env.graph_data, len(seeds), device=self.device, graph=self.env.graph,
+                          damaged_ratio=cfg["damaged_ratio"], assignment_iters=cfg["assignment_iters"],
+                          assignment_method=cfg["assignment_method"], reward_mode=cfg["reward_mode"],
+                          reward_alpha=cfg["reward_alpha"], reward_beta=cfg["reward_beta"],
+                          reward_gamma=cfg["reward_gamma"], reward_clip=cfg["reward_clip"],
+                          capacity_damage=cfg["capacity_damage"], unassigned_penalty=cfg["unassigned_penalty"],
+                          fixed_damage=cfg["fixed_damage"], fixed_damage_seed=cfg["fixed_damage_seed"],
+                          seeds=list(seeds), reset=False)
+        obs = ev.reset()
+        n = len(seeds)
+        ei, bv = batched_topology(ev.edge_index, self.N, n)
+        curves = []
+        done_all = torch.zeros(n, dtype=torch.bool, device=self.device)
+        for _ in range(int(cfg["max_steps"]) or 10 ** 6):
+            a = self.agent.select_actions(obs.node_x.reshape(-1, 4), ei, obs.edge_x.reshape(-1, 6),
+                                          obs.action_mask.reshape(-1), bv, num_graphs=n, deterministic=True)
+            obs, _, done, _ = ev.step(a.to(torch.int32), check=False)
+            curves.append(torch.where(done_all, torch.full_like(ev.tstt, float("nan")), ev.tstt))
+            done_all |= done
+            if bool(done_all.all()):
+                break
+        c = torch.stack(curves).cpu().numpy()
+        auc = [float(np.trapezoid(c[~np.isnan(c[:, k]), k])) for k in range(n)]
+        return {"tstt_last": float(np.nanmean([c[~np.isnan(c[:, k]), k][-1] for k in range(n)])),
+                "tstt_mean": float(np.nanmean(c)), "auc": float(np.mean(auc))}
+
+    def save(self, tag: str):
+        if self.rank == 0:
+            os.makedirs(self.cfg["output_dir"], exist_ok=True)
+            self.agent.save(os.path.join(self.cfg["output_dir"], f"model_{tag}.pt"))
+
+    def run(self, max_iters: Optional[int] = None):
+        cfg = self.cfg
+        self._reset_envs(None)
+        obs = self.env.observe()
+        best, patience = math.inf, 0
+        t0 = time.perf_counter()
+        it = 0
+        next_eval = int(cfg["eval_every"])
+        while self.episodes_done * self.world < int(cfg["episodes"]):
+            if max_iters is not None and it >= max_iters:
+                break
+            obs, finished = self.iteration(obs, it)
+            it += 1
+            if bool(finished.any()):
+                self.record(finished)
+                self._reset_envs(finished)
+                obs = self.env.observe()
+                rec = self.history[-1]
+                if self.rank == 0:
+                    self.logger.info(f"it {it} episodes {self.episodes_done * self.world} reward {rec['reward']:.3f} "
+                                     f"tstt_mean {rec['tstt_mean']:.2f} auc {rec['auc']:.1f} "
+                                     f"steps/s {it * self.B * self.world / (time.perf_counter() - t0):.0f}")
+                if rec["tstt_mean"] < best - 1e-6:
+                    best, patience = rec["tstt_mean"], 0
+                else:
+                    patience += 1
+                if patience >= int(cfg["early_stop_patience"]):
+                    break
+                if self.episodes_done >= next_eval and cfg["eval_every"] > 0:
+                    next_eval += int(cfg["eval_every"])
+                    ev = self.evaluate()
+                    if self.rank == 0:
+                        self.logger.info(f"eval {ev}")
+                    self.save("last")
+        self.save("last")
+        if self.rank == 0:
+            with open(os.path.join(cfg["output_dir"], "train_metrics.json"), "w") as fh:
+                json.dump(self.history, fh)
+        return self.history
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="vectorised GAT-SAC training (src/train.py equivalent)")
+    ap.add_argument("--config", default=None)
+    ap.add_argument("--num-envs", type=int, default=None)
+    ap.add_argument("--episodes", type=int, default=None)
+    ap.add_argument("--max-iters", type=int, default=None)
+    args = ap.parse_args(argv)
+    cfg = load_config(args.config)
+    if args.num_envs:
+        cfg["num_envs"] = args.num_envs
+    if args.episodes:
+        cfg["episodes"] = args.episodes
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    tr = Trainer(cfg, device=f"cuda:{local}", rank=rank, world=world)
+    tr.run(args.max_iters)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

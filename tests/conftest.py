@@ -6,6 +6,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_DIR = os.path.join(ROOT, "sac-gat-her_transportationrl_amd")
+os.environ["PYTHONPATH"] = os.pathsep.join([PKG_DIR, ROOT, os.environ.get("PYTHONPATH", "")])
 for p in (ROOT, PKG_DIR, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)

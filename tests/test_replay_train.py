@@ -1,0 +1,106 @@
+"""Replay (src/train.py:27-91), HER (805-823) and the vectorised trainer.
+
+GPU: sum-tree sampling == a numpy restatement of ReplayBuffer.sample's
+descent on the same uniforms (float64 tree); add() priority growth
+(max_p + k*eps), last-wins duplicate updates; HER relabel quirks; a short
+training run (acting + env + PER updates) writes a checkpoint with the
+reference's keys.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_descent(tree, capacity, r):
+    idx = 1
+    while idx < capacity:
+        left = 2 * idx
+        if r <= tree[left]:
+            idx = left
+        else:
+            r -= tree[left]
+            idx = left + 1
+    return idx - capacity
+
+
+@pytest.mark.parametrize("cap", [8, 37, 1000])
+def test_per_sampling_matches_reference_descent(cap):
+    from trafficrl.rl.replay import DeviceReplay
+    rb = DeviceReplay(cap, 24, 76, device="cuda")
+    rng = np.random.default_rng(cap)
+    n = min(cap, 3 * cap // 4)
+    idx = torch.arange(n, device="cuda")
+    leaf = torch.as_tensor(rng.random(n) + 0.01, device="cuda", dtype=torch.float64)
+    rb._set(idx, leaf)
+    tree = rb.tree.cpu().numpy()
+    # tree consistency: every internal node = sum of children
+    for k in range(1, cap):
+        a = tree[2 * k] if 2 * k < 2 * cap else 0.0
+        b = tree[2 * k + 1] if 2 * k + 1 < 2 * cap else 0.0
+        assert abs(tree[k] - (a + b)) <= 1e-12 * max(1.0, tree[k])
+    u = torch.rand(4096, dtype=torch.float64, device="cuda", generator=torch.Generator("cuda").manual_seed(0))
+    out = torch.empty(4096, dtype=torch.int64, device="cuda")
+    pri = torch.empty(4096, dtype=torch.float64, device="cuda")
+    from trafficrl import _lib
+    L = _lib.load()
+    _lib.check(L.trx_per_sample(_lib.ptr(rb.tree), cap, _lib.ptr(u), 4096, _lib.ptr(out), _lib.ptr(pri), None), "s")
+    ref = [ref_descent(tree, cap, float(x) * tree[1]) for x in u.cpu().numpy()]
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_add_priorities_and_last_wins():
+    from trafficrl.rl.replay import DeviceReplay
+    rb = DeviceReplay(16, 24, 76, alpha=0.6, eps=1e-6, device="cuda")
+    B = 5
+    z = lambda *s: torch.zeros(*s, device="cuda")  # noqa: E731
+    rb.add_batch(z(B, 24, 4), z(B, 76, 6), z(B, 76), torch.zeros(B, dtype=torch.int64, device="cuda"), z(B),
+                 z(B, 24, 4), z(B, 76, 6), z(B, 76), z(B), z(B, 76), z(B), z(B), z(B))
+    leaves = rb.tree[16:16 + B].cpu().numpy()
+    expect = [(1.0 + (k + 1) * 1e-6) ** 0.6 for k in range(B)]  # sequential reference adds
+    np.testing.assert_allclose(leaves, expect, rtol=1e-14)
+    rb.update_priorities(torch.tensor([2, 3, 2], device="cuda"), torch.tensor([0.5, -2.0, 4.0], device="cuda"))
+    np.testing.assert_allclose(rb.tree[16 + 2].item(), (4.0 + 1e-6) ** 0.6, rtol=1e-12)
+    np.testing.assert_allclose(rb.tree[16 + 3].item(), (2.0 + 1e-6) ** 0.6, rtol=1e-12)
+    assert abs(rb.max_priority.item() - (4.0 + 1e-6)) < 1e-12
+    s = rb.sample(64)
+    assert s.weights.max().item() == pytest.approx(1.0)
+    assert bool((s.idx < B).all())
+
+
+def test_her_relabel_quirks():
+    from trafficrl.rl.replay import DeviceReplay, her_relabel
+    rb = DeviceReplay(8, 24, 76, device="cuda")
+    B = 4
+    nm = (torch.rand(B, 76, device="cuda") < 0.3).float()
+    ex = torch.rand(B, 76, 6, device="cuda")
+    rb.add_batch(torch.zeros(B, 24, 4, device="cuda"), ex, nm, torch.zeros(B, dtype=torch.int64, device="cuda"),
+                 torch.zeros(B, device="cuda"), torch.zeros(B, 24, 4, device="cuda"), ex, nm,
+                 torch.zeros(B, device="cuda"), nm, torch.full((B,), 500.0, device="cuda"),
+                 torch.full((B,), 400.0, device="cuda"), torch.full((B,), 1000.0, device="cuda"))
+    s = rb.sample(16)
+    s = her_relabel(s, 1.0, "rel_improve", 0.5, 1.0, 0.0, 0.0, 2.0)
+    goal = 1.0 - s.next_mask
+    assert torch.equal(s.edge_x[:, :, -1], goal)           # apply_goal writes column -1 (train.py:127)
+    assert torch.equal(s.done, torch.ones_like(s.done))    # (1-m)*m == 0 -> always "complete"
+    r = (100.0 * (500.0 - 400.0) / 1000.0 - 400.0 / 1000.0)
+    torch.testing.assert_close(s.reward, torch.full_like(s.reward, min(r, 2.0) * 0.5))
+
+
+def test_short_training_run(tmp_path):
+    from trafficrl.train import Trainer, load_config
+    cfg = load_config(None)
+    cfg.update(num_envs=64, batch_start=128, batch_size=32, hidden_dim=32, embed_dim=32, episodes=64,
+               eval_every=64, output_dir=str(tmp_path), update_every=1, her_ratio=0.5)
+    tr = Trainer(cfg, device="cuda", log=False)
+    hist = tr.run(max_iters=30)
+    assert tr.episodes_done >= 64 and len(hist) >= 1
+    assert np.isfinite(float(tr.last_losses["critic_loss"]))
+    assert tr.replay.size == 64 * 22 or tr.replay.size > 128
+    sd = torch.load(os.path.join(str(tmp_path), "model_last.pt"), map_location="cpu", weights_only=True)
+    assert set(sd) == {"actor", "critic1", "critic2", "target1", "target2", "log_alpha"}
+    ev = tr.evaluate()
+    assert np.isfinite(ev["tstt_last"])
