@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
 """Benchmark: env steps/s (= full BPR user-equilibrium assignments/s) of N
 vectorised Sioux Falls repair envs per MI355X (BASELINE.json configs[1]:
-4096 envs, MSA 30 iterations).
+4096 envs, MSA 30 iterations, SAC+GAT bf16).
 
-One "step" = RepairEnv.step for every env of the batch (src/env/repair_env.py:
-207-237): repair the chosen link, re-run the 30-iteration assignment, reward,
-done, and the get_state observation (751-819) -- one trx_step + one
-trx_observe launch.  Actions: uniform over each env's damaged links (device
-RNG).  Damage: fixed_damage_seed=42 for all envs (the trainer's config);
-episodes are 22 steps, all envs auto-reset together (the reset assignment is
-inside the timed region but not counted as a step).
+Default workload `train` (configs[1]): one step = the GAT-SAC actor (bf16
+autocast) picks an action for every env from its observation, RepairEnv.step
+runs for all envs (src/env/repair_env.py:207-237: repair, 30-iteration MSA
+assignment, reward, done, get_state 751-819), transitions go to the device
+PER replay, and every 4 steps one SAC update on a 256-graph PER batch
+(src/train.py:954-1024).  Workload `env`: the same env steps with uniform
+random valid actions (no agent).  Damage: fixed_damage_seed=42 for all envs;
+episodes are 22 steps and all envs auto-reset together (the reset assignment
+is inside the timed region but not counted as a step).
 
 Multi-GPU: one process per GPU (torchrun), envs sharded with no data-path
 collective (weak scaling); max elapsed over ranks; value = all ranks' steps /
@@ -121,6 +123,7 @@ def main():
     ap.add_argument("--no-observe", action="store_true", help="skip get_state (assignment-only steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", default="train", choices=["train", "env"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,50 +143,92 @@ def main():
 
     B = args.envs
     gd = sioux_falls()
-    env = VecRepairEnv(gd, B, device=dev, assignment_method=args.method, assignment_iters=args.iters,
-                       reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0, reward_gamma=0.0,
-                       reward_clip=2.0, capacity_damage=1e-3, unassigned_penalty=1e4, reset=False)
-    E, N = env.num_edges, env.num_nodes
-    dmg0 = torch.from_numpy(fixed_damage_mask(E)).to(dev)
-    dmg_all = dmg0[None].expand(B, E).contiguous()
-    ep_len = int(dmg0.sum().item())
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     observe = not args.no_observe
+    ev_pairs = []      # env_kernel launches (HIP events on the launch stream)
+    phase_ev = {}      # per-phase events (train workload)
 
-    ev_pairs = []
+    def timed(fn, bucket):
+        s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_.record()
+        out = fn()
+        e_.record()
+        bucket.append((s_, e_))
+        return out
 
-    def timed_kernel(fn):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        fn()
-        e.record()
-        ev_pairs.append((s, e))
+    if args.workload == "train":
+        from trafficrl.train import Trainer, load_config
+        cfg = load_config(None)
+        cfg.update(num_envs=B, assignment_iters=args.iters, assignment_method=args.method, batch_start=256,
+                   batch_size=256, update_every=4, updates_per_step=1, eval_every=0, episodes=10 ** 9,
+                   output_dir=os.path.join("/tmp", f"trx_bench_{os.getpid()}"), amp="bf16")
+        tr = Trainer(cfg, device=dev, rank=rank, world=world, log=False)
+        env = tr.env
+        raw_step, raw_act, raw_update = env.step, tr.act, tr.update
 
-    state = {"t": 0}
+        def step_w(actions, observe=True, check=True):
+            _, rew, done, info = timed(lambda: raw_step(actions, observe=False, check=check), ev_pairs)
+            return (env.observe() if observe else None), rew, done, info
 
-    def reset():
-        timed_kernel(lambda: env.reset(damaged=dmg_all, observe=False))
-        if observe:
-            env.observe()
-        state["t"] = 0
+        env.step = step_w
+        tr.act = lambda *a, **k: timed(lambda: raw_act(*a, **k), phase_ev.setdefault("act", []))
+        tr.update = lambda *a, **k: timed(lambda: raw_update(*a, **k), phase_ev.setdefault("update", []))
+        tr._reset_envs(None)
+        E, N = env.num_edges, env.num_nodes
+        dmg_all = tr.fixed_mask.expand(B, E).contiguous()
+        ep_len = int(tr.fixed_mask.sum().item())
+        all_true = torch.ones(B, dtype=torch.bool, device=dev)
+        st = {"obs": env.observe(), "it": 0, "t": 0}
 
-    def one_step():
-        scores = torch.rand(B, E, device=dev, generator=gen) * env.damaged
-        actions = scores.argmax(dim=1).to(torch.int32)
-        timed_kernel(lambda: env.step(actions, observe=False, check=False))
-        if observe:
-            env.observe()
-        state["t"] += 1
-        if state["t"] == ep_len:
-            reset()
+        def reset():
+            timed(lambda: env.reset_where(all_true, dmg_all), ev_pairs)
+            st["obs"] = env.observe()
+            st["t"] = 0
+            for acc in (tr.ep_reward, tr.ep_tstt_sum, tr.ep_auc, tr.ep_len):
+                acc.zero_()
+            tr.ep_prev_tstt.copy_(env.tstt)
 
-    reset()
+        def one_step():
+            st["obs"], _ = tr.iteration(st["obs"], st["it"])
+            st["it"] += 1
+            st["t"] += 1
+            if st["t"] == ep_len:
+                reset()
+    else:
+        env = VecRepairEnv(gd, B, device=dev, assignment_method=args.method, assignment_iters=args.iters,
+                           reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0, reward_gamma=0.0,
+                           reward_clip=2.0, capacity_damage=1e-3, unassigned_penalty=1e4, reset=False)
+        E, N = env.num_edges, env.num_nodes
+        dmg0 = torch.from_numpy(fixed_damage_mask(E)).to(dev)
+        dmg_all = dmg0[None].expand(B, E).contiguous()
+        ep_len = int(dmg0.sum().item())
+        st = {"t": 0}
+
+        def reset():
+            timed(lambda: env.reset(damaged=dmg_all, observe=False), ev_pairs)
+            if observe:
+                env.observe()
+            st["t"] = 0
+
+        def one_step():
+            scores = torch.rand(B, E, device=dev, generator=gen) * env.damaged
+            actions = scores.argmax(dim=1).to(torch.int32)
+            timed(lambda: env.step(actions, observe=False, check=False), ev_pairs)
+            if observe:
+                env.observe()
+            st["t"] += 1
+            if st["t"] == ep_len:
+                reset()
+
+        reset()
     for _ in range(args.warmup):
         one_step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     ev_pairs.clear()
+    for v in phase_ev.values():
+        v.clear()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -193,6 +238,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    breakdown = {k: float(np.sum([s_.elapsed_time(e_) for s_, e_ in v])) / args.steps for k, v in phase_ev.items()}
     kern_ms = [s.elapsed_time(e) for s, e in ev_pairs]
     mean_kernel_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
     if dist:
@@ -227,11 +273,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (link flows/costs) + f64 (path labels)",
-            "data": "synthetic: Sioux Falls TNTP, fixed_damage_seed=42, uniform random valid repair actions",
+            "dtype": "f32 (link flows/costs) + f64 (path labels)" + (
+                "; bf16 autocast GAT-SAC" if args.workload == "train" else ""),
+            "data": ("synthetic: Sioux Falls TNTP, fixed_damage_seed=42, random-init GAT-SAC (hidden 256, 4 heads, "
+                     "embed 256)" if args.workload == "train" else
+                     "synthetic: Sioux Falls TNTP, fixed_damage_seed=42, uniform random valid repair actions"),
             "config": {
-                "workload": f"SF {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment per step"
-                            + (", get_state included" if observe else ""),
+                "workload": (f"SF {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment + get_state per"
+                             " step" + (", GAT-SAC bf16 acting every step + 1 PER update (batch 256) every 4 steps"
+                                        if args.workload == "train" else ", uniform random valid actions")),
+                "workload_kind": args.workload,
                 "envs_per_gpu": B, "global_envs": B * world, "network": "SiouxFalls (24 nodes, 76 links, 528 OD)",
                 "method": args.method, "assignment_iters": args.iters, "episode_len": ep_len,
                 "parallelism": f"env-sharded x{world}",
@@ -245,6 +296,7 @@ def main():
                 "bytes_per_assign": bpa, "assigns_per_launch": B,
             },
             "cpu_baseline": cpu,
+            "breakdown_ms_per_step": dict(breakdown, env_kernel=mean_kernel_s * 1e3 * len(kern_ms) / args.steps),
         }
         print(json.dumps(out), flush=True)
     if dist:

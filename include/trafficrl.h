@@ -183,6 +183,15 @@ int trx_per_update(double* tree, int64_t capacity, const int64_t* idx, const dou
 int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
                    double* out_priority, void* stream);
 
+/* ------------------------------------------------------ graph support
+ * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
+ * (passed as void*) into an equivalent fill-kernel node with the same
+ * dependencies.  Works around ROCm 7.2's packet-capture replay of small
+ * memset nodes (torch's reduction semaphores), see csrc/graph_patch.hip.
+ * Used by the trainer's HIP-graph SAC update (train.py:GraphedUpdate); the
+ * reference has no counterpart (its update is eager, src/rl/sac.py:157-263). */
+int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched);
+
 #ifdef __cplusplus
 }
 #endif

@@ -173,7 +173,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
         if (gb < B) {
             if (mode == kModeStep) {
                 int a = action[gb];
-                active = s.damaged[(size_t)gb * E + a] != 0.0f;  // repair_env.py:210
+                // out-of-range ids (the host check is optional: check=False) are
+                // memory-safe no-ops, reported like an already-repaired link
+                active = (unsigned)a < (unsigned)E && s.damaged[(size_t)gb * E + a] != 0.0f;  // repair_env.py:210
                 if (!active) {
                     reward_out[gb] = -1.0;
                     done_out[gb] = 0;

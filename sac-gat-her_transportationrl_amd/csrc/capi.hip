@@ -336,4 +336,13 @@ int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_
     return TRX_OK;
 }
 
+int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
+    if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
+    int n = 0;
+    hipError_t e = trx::patch_graph_memsets(static_cast<hipGraph_t>(hip_graph), &n);
+    if (n_patched) *n_patched = n;
+    if (e != hipSuccess) return fail(TRX_EHIP, "graph_patch_memsets: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 }  // extern "C"

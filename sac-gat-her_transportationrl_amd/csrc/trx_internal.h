@@ -71,6 +71,7 @@ hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, cons
                                const float* gout, float* gxh, float* ga_src, float* ga_dst, float* ga_edge,
                                hipStream_t stream);
 
+hipError_t patch_graph_memsets(hipGraph_t graph, int* n_patched);
 hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* pri, int n,
                              hipStream_t stream);
 hipError_t launch_per_sample(const double* tree, int64_t capacity, const double* u, int n, int64_t* out_idx,

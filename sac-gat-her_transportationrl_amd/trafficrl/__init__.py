@@ -6,6 +6,7 @@ Module layout mirrors the reference's src/ tree:
   trafficrl.env.repair_env     <- src/env/repair_env.py  (RepairEnv facade)
   trafficrl.env.vec_env        (batched VecRepairEnv, the performance path)
   trafficrl.baselines          <- src/baselines/__init__.py
+  trafficrl.models / rl / train <- src/models, src/rl, src/train.py
 """
 from . import _lib  # noqa: F401
 

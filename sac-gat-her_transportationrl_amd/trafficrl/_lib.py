@@ -21,7 +21,7 @@ REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "
 EXPORTS = (
     "trx_abi_version", "trx_last_error", "trx_graph_create", "trx_graph_destroy", "trx_graph_info",
     "trx_workspace_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe", "trx_gat_forward",
-    "trx_gat_backward", "trx_per_update", "trx_per_sample",
+    "trx_gat_backward", "trx_per_update", "trx_per_sample", "trx_graph_patch_memsets",
 )
 
 
@@ -81,8 +81,10 @@ def load():
                                    ctypes.c_int32, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_per_update.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int32, _vp]
     L.trx_per_sample.argtypes = [_vp, ctypes.c_int64, _vp, ctypes.c_int32, _vp, _vp, _vp]
+    L.trx_graph_patch_memsets.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32)]
     for name in ("trx_graph_create", "trx_graph_destroy", "trx_graph_info", "trx_assign", "trx_reset", "trx_step",
-                 "trx_observe", "trx_gat_forward", "trx_gat_backward", "trx_per_update", "trx_per_sample"):
+                 "trx_observe", "trx_gat_forward", "trx_gat_backward", "trx_per_update", "trx_per_sample",
+                 "trx_graph_patch_memsets"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != 1:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != 1")
@@ -107,3 +109,14 @@ def ptr(t) -> ctypes.c_void_p:
 def stream_ptr(device=None) -> ctypes.c_void_p:
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def patch_graph_memsets(graph) -> int:
+    """Rewrite the memset nodes of a torch.cuda.CUDAGraph captured with
+    keep_graph=True (before instantiate) into fill kernels; returns how many
+    were rewritten.  See trx_graph_patch_memsets in include/trafficrl.h."""
+    L = load()
+    n = ctypes.c_int32(0)
+    check(L.trx_graph_patch_memsets(ctypes.c_void_p(graph.raw_cuda_graph()), ctypes.byref(n)),
+          "trx_graph_patch_memsets")
+    return int(n.value)

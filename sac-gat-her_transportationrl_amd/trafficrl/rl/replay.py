@@ -44,18 +44,26 @@ class Sample:
     prev_tstt: torch.Tensor    # [bs] float64
     next_tstt: torch.Tensor
     init_tstt: torch.Tensor
+    pri: Optional[torch.Tensor] = None  # [bs] float64 sampled leaf priorities
 
 
-def _last_occurrence(idx: torch.Tensor) -> torch.Tensor:
-    """Boolean mask keeping the last occurrence of each value (stable)."""
+def _last_wins(idx: torch.Tensor, val: torch.Tensor) -> torch.Tensor:
+    """Give every duplicate of an index the value of its LAST occurrence, so
+    concurrent leaf writes all store the same number (the reference's
+    sequential update order) -- without a data-dependent shape, hence without
+    a host synchronisation (HIP-graph capturable)."""
     n = idx.numel()
-    order = torch.argsort(idx * (n + 1) + torch.arange(n, device=idx.device))
+    pos = torch.arange(n, device=idx.device)
+    order = torch.argsort(idx * (n + 1) + pos)          # stable: by index, then position
     s = idx[order]
-    last = torch.ones(n, dtype=torch.bool, device=idx.device)
-    last[:-1] = s[1:] != s[:-1]
-    keep = torch.zeros(n, dtype=torch.bool, device=idx.device)
-    keep[order[last]] = True
-    return keep
+    is_last = torch.ones(n, dtype=torch.bool, device=idx.device)
+    is_last[:-1] = s[1:] != s[:-1]
+    # run end for each sorted position: smallest q >= p with is_last[q]
+    cand = torch.where(is_last, pos, torch.full_like(pos, n))
+    run_end = torch.flip(torch.cummin(torch.flip(cand, [0]), 0).values, [0])
+    out = torch.empty_like(val)
+    out[order] = val[order[run_end]]
+    return out
 
 
 class DeviceReplay:
@@ -83,11 +91,11 @@ class DeviceReplay:
         self.max_priority = torch.ones((), dtype=torch.float64, device=dev)
         self.ptr = 0
         self.size = 0
+        self.size_t = torch.zeros((), dtype=torch.float64, device=dev)  # device copy for graph-captured sampling
 
     def _set(self, idx: torch.Tensor, leaf: torch.Tensor):
-        keep = _last_occurrence(idx)
-        idx = idx[keep].contiguous()
-        leaf = leaf[keep].to(torch.float64).contiguous()
+        idx = idx.contiguous()
+        leaf = _last_wins(idx, leaf.to(torch.float64)).contiguous()
         L = _lib.load()
         _lib.check(L.trx_per_update(_lib.ptr(self.tree), self.capacity, _lib.ptr(idx), _lib.ptr(leaf), idx.numel(),
                                     _lib.stream_ptr(self.device)), "trx_per_update")
@@ -112,30 +120,36 @@ class DeviceReplay:
         self.init_tstt.index_copy_(0, idx, init_tstt.to(torch.float64))
         # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
         pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
-        self.max_priority = pr[-1].clone()
+        self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
         self._set(idx, pr ** self.alpha)
         self.ptr = (self.ptr + B) % self.capacity
         self.size = min(self.size + B, self.capacity)
+        self.size_t.fill_(float(self.size))
 
-    def sample(self, batch_size: int, generator: Optional[torch.Generator] = None) -> Sample:
+    def sample(self, batch_size: int, generator: Optional[torch.Generator] = None,
+               u: Optional[torch.Tensor] = None) -> Sample:
+        """`u` (float64 [batch_size] in [0,1)) replaces the internal draw; the
+        HIP-graph trainer fills it outside the captured region."""
         if self.size == 0:
             raise ValueError("Cannot sample from an empty replay buffer.")
-        u = torch.rand(batch_size, dtype=torch.float64, device=self.device, generator=generator)
+        if u is None:
+            u = torch.rand(batch_size, dtype=torch.float64, device=self.device, generator=generator)
         idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
         pri = torch.empty(batch_size, dtype=torch.float64, device=self.device)
         L = _lib.load()
         _lib.check(L.trx_per_sample(_lib.ptr(self.tree), self.capacity, _lib.ptr(u), batch_size, _lib.ptr(idx),
                                     _lib.ptr(pri), _lib.stream_ptr(self.device)), "trx_per_sample")
         probs = pri / self.total
-        w = (self.size * probs) ** (-self.beta)
+        w = (self.size_t * probs) ** (-self.beta)
         w = w / torch.clamp(w.max(), min=1e-300)
         return Sample(idx, w.float(), self.node_x[idx], self.edge_x[idx], self.mask[idx], self.action[idx],
                       self.reward[idx], self.next_node_x[idx], self.next_edge_x[idx], self.next_mask[idx],
-                      self.done[idx], self.goal[idx], self.prev_tstt[idx], self.next_tstt[idx], self.init_tstt[idx])
+                      self.done[idx], self.goal[idx], self.prev_tstt[idx], self.next_tstt[idx], self.init_tstt[idx],
+                      pri)
 
     def update_priorities(self, idx: torch.Tensor, td_errors: torch.Tensor):
         pr = td_errors.detach().to(torch.float64).abs() + self.eps
-        self.max_priority = torch.maximum(self.max_priority, pr.max())
+        self.max_priority.copy_(torch.maximum(self.max_priority, pr.max()))
         self._set(idx, pr ** self.alpha)
 
 
@@ -163,13 +177,17 @@ def reward_with_goal(mode, prev, curr, init, complete, alpha=1.0, beta=10.0, gam
 
 
 def her_relabel(s: Sample, her_ratio: float, reward_mode: str, reward_scale: float, alpha: float, beta: float,
-                gamma: float, clip: float, generator: Optional[torch.Generator] = None, goal_column: int = -1):
+                gamma: float, clip: float, generator: Optional[torch.Generator] = None, goal_column: int = -1,
+                u: Optional[torch.Tensor] = None):
     """train.py:805-823 on a sampled batch (in place).  goal_column=-1
-    reproduces apply_goal (train.py:127); 4 would write the real goal column."""
+    reproduces apply_goal (train.py:127); 4 would write the real goal column.
+    `u` (float32 [bs]) replaces the internal draw (graph capture)."""
     if her_ratio <= 0:
         return s
     bs = s.action.shape[0]
-    pick = torch.rand(bs, device=s.action.device, generator=generator) < her_ratio
+    if u is None:
+        u = torch.rand(bs, device=s.action.device, generator=generator)
+    pick = u < her_ratio
     goal = 1.0 - s.next_mask
     complete = ((goal * s.next_mask).sum(dim=1) == 0)
     r = reward_with_goal(reward_mode, s.prev_tstt, s.next_tstt, s.init_tstt, complete, alpha, beta, gamma, clip)
@@ -179,6 +197,7 @@ def her_relabel(s: Sample, her_ratio: float, reward_mode: str, reward_scale: flo
     s.goal = torch.where(pick[:, None], goal, s.goal)
     s.edge_x = s.edge_x.clone()
     s.next_edge_x = s.next_edge_x.clone()
-    s.edge_x[pick, :, goal_column] = goal[pick]
-    s.next_edge_x[pick, :, goal_column] = goal[pick]
+    # masked column write without boolean indexing (no host sync)
+    s.edge_x[:, :, goal_column] = torch.where(pick[:, None], goal, s.edge_x[:, :, goal_column])
+    s.next_edge_x[:, :, goal_column] = torch.where(pick[:, None], goal, s.next_edge_x[:, :, goal_column])
     return s

@@ -27,7 +27,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
-from ..models.gat_encoder import GATEncoder
+from ..models.gat_encoder import GATEncoder, is_regular_batch
 
 
 @dataclass
@@ -37,9 +37,27 @@ class SACOutput:
     probs: torch.Tensor
 
 
-def scatter_sum(src: torch.Tensor, index: torch.Tensor, num: int) -> torch.Tensor:
+def scatter_sum(src: torch.Tensor, index: torch.Tensor, num: int, regular: bool = False) -> torch.Tensor:
+    """torch_scatter.scatter_sum; `regular` (index = arange(num) repeated
+    equally, contiguous) reduces a [num, k] view: no atomics, deterministic."""
+    if regular:
+        return src.view(num, -1, *src.shape[1:]).sum(1)
     out = torch.zeros(num, *src.shape[1:], device=src.device, dtype=src.dtype)
     return out.index_add_(0, index, src)
+
+
+def input_layer_norm(ln: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
+    """nn.LayerNorm over the 4-/6-wide raw node/edge features (sac.py:38-39).
+    torch's generic row kernel spends one workgroup per row there (~0.9 ms per
+    acting call at 4096 graphs); the same math as a handful of vectorised ops
+    costs tens of microseconds.  Wide rows keep the library kernel."""
+    if x.size(-1) >= 32:
+        return ln(x)
+    xf = x.float()
+    mu = xf.mean(-1, keepdim=True)
+    d = xf - mu
+    var = (d * d).mean(-1, keepdim=True)
+    return d * torch.rsqrt(var + ln.eps) * ln.weight + ln.bias
 
 
 def segment_softmax(logits: torch.Tensor, index: torch.Tensor, num: int, per_segment: Optional[int] = None):
@@ -52,6 +70,27 @@ def segment_softmax(logits: torch.Tensor, index: torch.Tensor, num: int, per_seg
     mx = mx.scatter_reduce(0, index, logits, reduce="amax", include_self=True)
     ex = torch.exp(logits - mx[index])
     return ex / (scatter_sum(ex, index, num)[index] + 1e-16)
+
+
+_edge_layout_cache: dict = {}
+
+
+def is_regular_edges(edge_index: torch.Tensor, batch: torch.Tensor, num_graphs: int) -> bool:
+    """True when the edges of graph b are the b-th of num_graphs equal
+    contiguous blocks (PyG Batch of same-size graphs).  Checked once per
+    (edge_index, batch) pair and cached, so steady-state calls never sync."""
+    E = edge_index.shape[1]
+    if num_graphs <= 0 or E % num_graphs:
+        return False
+    key = (edge_index.data_ptr(), edge_index._version, batch.data_ptr(), batch._version, E, num_graphs)
+    r = _edge_layout_cache.get(key)
+    if r is None:
+        eb = batch[edge_index[0]].long()
+        r = bool(torch.equal(eb, torch.arange(num_graphs, device=eb.device).repeat_interleave(E // num_graphs)))
+        if len(_edge_layout_cache) > 64:
+            _edge_layout_cache.clear()
+        _edge_layout_cache[key] = r
+    return r
 
 
 @torch.no_grad()
@@ -107,8 +146,8 @@ class Actor(_EdgeHead):
 
     def forward(self, node_x, edge_index, edge_attr, action_mask, batch, return_attention: bool = False,
                 num_graphs: Optional[int] = None):
-        node_x = self.node_norm(node_x)
-        edge_attr = self.edge_norm(edge_attr)
+        node_x = input_layer_norm(self.node_norm, node_x)
+        edge_attr = input_layer_norm(self.edge_norm, edge_attr)
         B = num_graphs if num_graphs is not None else int(batch.max()) + 1
         node_emb, global_ctx, attn = self.encoder(node_x, edge_index, edge_attr, batch,
                                                   return_attention=return_attention, num_graphs=B)
@@ -116,7 +155,8 @@ class Actor(_EdgeHead):
         edge_batch = batch[src]
         logits = self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, edge_batch).float()
         logits = logits.masked_fill(action_mask <= 0, -1e9)
-        probs = segment_softmax(logits, edge_batch, B, logits.numel() // B if logits.numel() % B == 0 else None)
+        per = logits.numel() // B if is_regular_edges(edge_index, batch, B) else None
+        probs = segment_softmax(logits, edge_batch, B, per)
         return logits, probs, attn
 
 
@@ -130,8 +170,8 @@ class Critic(_EdgeHead):
                                                                       num_layers=num_layers)
 
     def forward(self, node_x, edge_index, edge_attr, batch, num_graphs: Optional[int] = None):
-        node_x = self.node_norm(node_x)
-        edge_attr = self.edge_norm(edge_attr)
+        node_x = input_layer_norm(self.node_norm, node_x)
+        edge_attr = input_layer_norm(self.edge_norm, edge_attr)
         B = num_graphs if num_graphs is not None else int(batch.max()) + 1
         node_emb, global_ctx, _ = self.encoder(node_x, edge_index, edge_attr, batch, num_graphs=B)
         src, dst = edge_index
@@ -143,7 +183,8 @@ class DiscreteSAC:
                  actor_lr: float | None = None, critic_lr: float | None = None, alpha_lr: float | None = None,
                  grad_clip: float | None = None, gamma: float = 0.99, target_tau: float = 0.005,
                  target_entropy: float = None, target_entropy_ratio: float = 0.1, alpha_init: float = 0.1,
-                 share_critic_encoder: bool = True, device=None, amp_dtype: Optional[torch.dtype] = None):
+                 share_critic_encoder: bool = True, device=None, amp_dtype: Optional[torch.dtype] = None,
+                 capturable: bool = False):
         self.actor = Actor(node_in, edge_in, hidden, embed, num_layers=num_layers)
         self.share_critic_encoder = share_critic_encoder
         if share_critic_encoder:
@@ -167,17 +208,21 @@ class DiscreteSAC:
         actor_lr = lr if actor_lr is None else actor_lr
         critic_lr = lr if critic_lr is None else critic_lr
         alpha_lr = lr if alpha_lr is None else alpha_lr
-        self.actor_opt = torch.optim.Adam(self.actor.parameters(), lr=actor_lr)
+        # capturable: Adam keeps its step count on the device so update() can be
+        # replayed from a HIP graph (train.py); same arithmetic otherwise
+        self.capturable = capturable
+        adam = dict(capturable=True, foreach=True) if capturable else {}
+        self.actor_opt = torch.optim.Adam(self.actor.parameters(), lr=actor_lr, **adam)
         if share_critic_encoder:
             critic_params = (list(self.critic_encoder.parameters()) + list(self.critic1.edge_mlp.parameters())
                              + list(self.critic2.edge_mlp.parameters()))
         else:
             critic_params = list(self.critic1.parameters()) + list(self.critic2.parameters())
         self.critic_params = critic_params
-        self.critic_opt = torch.optim.Adam(critic_params, lr=critic_lr)
+        self.critic_opt = torch.optim.Adam(critic_params, lr=critic_lr, **adam)
         dev = device if device is not None else "cpu"
         self.log_alpha = torch.tensor(float(np.log(max(alpha_init, 1e-8))), requires_grad=True, device=dev)
-        self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=alpha_lr)
+        self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=alpha_lr, **adam)
         self.gamma = gamma
         self.target_tau = target_tau
         self.target_entropy = target_entropy
@@ -194,7 +239,9 @@ class DiscreteSAC:
     def _amp(self):
         if self.amp_dtype is None:
             return torch.autocast("cuda", enabled=False)
-        return torch.autocast("cuda", dtype=self.amp_dtype)
+        # no weight-cast cache: a graph-captured update must re-cast the weights
+        # the optimizer changed in place on every replay
+        return torch.autocast("cuda", dtype=self.amp_dtype, cache_enabled=not self.capturable)
 
     # ------------------------------------------------------------ acting
     def select_action(self, node_x, edge_index, edge_attr, action_mask, deterministic: bool = False) -> SACOutput:
@@ -224,6 +271,22 @@ class DiscreteSAC:
         """sac.py:157-263.  sync_metrics=True returns python floats and a
         td_errors list like the reference; False keeps them as device tensors
         (no host synchronisation, for the vectorised trainer)."""
+        out = self.compute_gradients(batch, weights)
+        if self.grad_sync is not None:
+            self.grad_sync(self.gradients())
+        self.apply_gradients(alpha_max)
+        if sync_metrics:
+            out = {k: (v.cpu().numpy().tolist() if k == "td_errors" else float(v)) for k, v in out.items()}
+        return out
+
+    def gradients(self):
+        return [p.grad for p in self._all_params() if p.grad is not None]
+
+    def compute_gradients(self, batch, weights=None):
+        """Losses and the three backward passes of sac.py:157-243.  None of
+        critic, actor and alpha backward depends on another's optimizer step,
+        so all gradients exist before any step: one synchronisation point for
+        data parallelism.  No host synchronisation (HIP-graph capturable)."""
         if isinstance(batch, list) and len(batch) == 1:
             batch = batch[0]
         (node_x, edge_index, edge_attr, action_mask, batch_vec, action, reward, next_node_x, next_edge_attr,
@@ -236,13 +299,15 @@ class DiscreteSAC:
             if weights_tensor.dim() == 0:
                 weights_tensor = weights_tensor.unsqueeze(0).expand_as(reward)
         edge_batch = batch_vec[edge_index[0]]
+        reg = is_regular_edges(edge_index, batch_vec, B)
         with self._amp():
             with torch.no_grad():
                 _, next_probs, _ = self.actor(next_node_x, edge_index, next_edge_attr, next_action_mask,
                                               next_batch_vec, num_graphs=B)
                 q_next = torch.min(self.target1(next_node_x, edge_index, next_edge_attr, next_batch_vec, B),
                                    self.target2(next_node_x, edge_index, next_edge_attr, next_batch_vec, B))
-                v_next = scatter_sum(next_probs * (q_next - self.alpha * torch.log(next_probs + 1e-8)), edge_batch, B)
+                v_next = scatter_sum(next_probs * (q_next - self.alpha * torch.log(next_probs + 1e-8)), edge_batch, B,
+                                     reg)
                 target = reward + (1.0 - done) * self.gamma * v_next
             q1_all = self.critic1(node_x, edge_index, edge_attr, batch_vec, B)
             q2_all = self.critic2(node_x, edge_index, edge_attr, batch_vec, B)
@@ -257,29 +322,40 @@ class DiscreteSAC:
         # alpha detached: the reference zeroes log_alpha.grad (alpha_opt.zero_grad,
         # sac.py:236) after actor_loss.backward, so this term never reaches it
         actor_terms = probs * (self.alpha.detach() * torch.log(probs + 1e-8) - q_all)
-        actor_loss = scatter_sum(actor_terms, edge_batch, B).mean()
+        actor_loss = scatter_sum(actor_terms, edge_batch, B, reg).mean()
         if self.target_entropy is None:
-            valid = scatter_sum((action_mask > 0).float(), edge_batch, B)
+            valid = scatter_sum((action_mask > 0).float(), edge_batch, B, reg)
             target_entropy = (self.target_entropy_ratio * torch.log(valid + 1e-8)).mean()
         else:
             target_entropy = self.target_entropy
         log_probs = torch.log(probs + 1e-8).detach()
-        alpha_term = scatter_sum(probs.detach() * (log_probs + target_entropy), edge_batch, B)
+        alpha_term = scatter_sum(probs.detach() * (log_probs + target_entropy), edge_batch, B, reg)
         alpha_loss = -(self.log_alpha * alpha_term).mean()
-        entropy = scatter_sum(-(probs.detach() * log_probs), edge_batch, B).mean()
+        entropy = scatter_sum(-(probs.detach() * log_probs), edge_batch, B, reg).mean()
         q_taken = torch.min(q1, q2).detach()
-        logp_mean = scatter_sum(probs.detach() * log_probs, edge_batch, B).mean().detach()
+        logp_mean = scatter_sum(probs.detach() * log_probs, edge_batch, B, reg).mean().detach()
 
-        # three independent backward passes, then (multi-GPU) ONE bucketed all-reduce
         self.critic_opt.zero_grad(set_to_none=False)
         self.actor_opt.zero_grad(set_to_none=False)
         self.alpha_opt.zero_grad(set_to_none=False)
         critic_loss.backward()
         actor_loss.backward()
         alpha_loss.backward()
-        if self.grad_sync is not None:
-            grads = [p.grad for p in self._all_params() if p.grad is not None]
-            self.grad_sync(grads)
+        return {
+            "critic_loss": critic_loss.detach(),
+            "actor_loss": actor_loss.detach(),
+            "alpha": self.alpha.detach(),
+            "alpha_loss": alpha_loss.detach(),
+            "policy_entropy": entropy,
+            "q_taken": q_taken.mean(),
+            "q_mean": q_all.mean(),
+            "logp_mean": logp_mean,
+            "td_errors": td_error,
+        }
+
+    def apply_gradients(self, alpha_max: float = None):
+        """Clipping, the three optimizer steps, the log_alpha clamps and the
+        Polyak target update (sac.py:224-263), in the reference's order."""
         clip = self.grad_clip is not None and self.grad_clip > 0
         if clip:
             clip_grad_norm_listwise_(list(self.critic1.parameters()) + list(self.critic2.parameters()), self.grad_clip)
@@ -301,20 +377,6 @@ class DiscreteSAC:
         else:
             self._soft_update(self.critic1, self.target1)
             self._soft_update(self.critic2, self.target2)
-        out = {
-            "critic_loss": critic_loss.detach(),
-            "actor_loss": actor_loss.detach(),
-            "alpha": self.alpha.detach(),
-            "alpha_loss": alpha_loss.detach(),
-            "policy_entropy": entropy,
-            "q_taken": q_taken.mean(),
-            "q_mean": q_all.mean(),
-            "logp_mean": logp_mean,
-            "td_errors": td_error,
-        }
-        if sync_metrics:
-            out = {k: (v.cpu().numpy().tolist() if k == "td_errors" else float(v)) for k, v in out.items()}
-        return out
 
     def _all_params(self):
         seen, out = set(), []
@@ -338,9 +400,14 @@ class DiscreteSAC:
         self.target2.load_state_dict(state["target2"])
         self.log_alpha = state["log_alpha"].to(map_location).requires_grad_()
         lr = self.alpha_opt.param_groups[0]["lr"]
-        self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=lr)
+        adam = dict(capturable=True, foreach=True) if self.capturable else {}
+        self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=lr, **adam)
 
     @torch.no_grad()
     def _soft_update(self, src, tgt):
-        for p, tp in zip(src.parameters(), tgt.parameters()):
-            tp.data.copy_(tp.data * (1.0 - self.target_tau) + p.data * self.target_tau)
+        """tp <- tp*(1-tau) + p*tau (sac.py:288-291), as two multi-tensor ops."""
+        ps = [p.data for p in src.parameters()]
+        tps = [tp.data for tp in tgt.parameters()]
+        scaled = torch._foreach_mul(ps, self.target_tau)
+        torch._foreach_mul_(tps, 1.0 - self.target_tau)
+        torch._foreach_add_(tps, scaled)

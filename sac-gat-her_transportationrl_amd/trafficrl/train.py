@@ -37,6 +37,7 @@ import torch
 from .data.tntp_parser import load_graph_data, sioux_falls
 from .env.vec_env import VecRepairEnv
 from .rl.replay import DeviceReplay, her_relabel
+from . import _lib
 from .rl.sac import DiscreteSAC
 
 DEFAULTS: Dict = dict(
@@ -48,7 +49,7 @@ DEFAULTS: Dict = dict(
     actor_lr=None, critic_lr=None, alpha_lr=None, gamma=0.99, target_tau=0.001, grad_clip=1.0,
     share_critic_encoder=False, alpha_init=0.1, alpha_max=2.5, target_entropy_ratio=0.2, eval_every=20,
     eval_seeds=[42], early_stop_patience=2000, seed=42, output_dir="outputs", num_envs=256, amp="bf16",
-    log_every=10, save_every=50, net_path=None, trips_path=None,
+    log_every=10, save_every=50, net_path=None, trips_path=None, graph_update=True,
 )
 
 
@@ -92,6 +93,99 @@ class GradAllReduce:
             off += n
 
 
+def capture_graph(fn, pool=None):
+    """torch.cuda.graph capture of fn() with the memset nodes rewritten into
+    fill kernels before instantiation (trx_graph_patch_memsets: ROCm 7.2's
+    packet-capture replay skips small memset nodes, which torch's multi-block
+    reductions use to clear their semaphores)."""
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g, pool=pool):
+        out = fn()
+    _lib.patch_graph_memsets(g)
+    g.instantiate()
+    return g, out
+
+
+def graph_memset_replays_ok(device) -> bool:
+    """Self-test of capture_graph: a captured 4-byte hipMemsetAsync followed
+    by an add must start from the cleared value on every replay."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+    except OSError:
+        return False
+    hip.hipMemsetAsync.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+    z = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def body():
+        hip.hipMemsetAsync(ctypes.c_void_p(z.data_ptr()), 0, 4, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        z.add_(1)
+
+    g, _ = capture_graph(body)
+    vals = []
+    for _ in range(3):
+        g.replay()
+        vals.append(int(z.item()))
+    return vals == [1, 1, 1]
+
+
+class GraphedUpdate:
+    """Trainer.update replayed from HIP graphs (torch.cuda.CUDAGraph).
+
+    One SAC update at batch 256 is ~1500 small kernels; launched from Python
+    it is host-bound (~25 ms).  After `warmup` eager updates (on a side
+    stream: optimizer state, CSR/layout caches, allocator) the whole update --
+    PER sample, HER relabel, six forwards, three backwards, clipping, the Adam
+    steps, the Polyak update and the priority write-back -- is captured once
+    and replayed.  The random draws stay outside the graph: they are written
+    into static buffers before each replay, from the trainer's generator.
+    With data parallelism the update is captured as two graphs around the
+    gradient all-reduce, which runs eagerly (one RCCL call per update)."""
+
+    def __init__(self, trainer: "Trainer", warmup: int = 3):
+        self.tr, self.warmup, self.calls = trainer, warmup, 0
+        self.g_grads = self.g_apply = None
+        self.out = None
+        self.side = torch.cuda.Stream(trainer.device)
+
+    def __call__(self):
+        tr = self.tr
+        u, her_u = tr._draw_update_randoms()
+        if self.g_grads is None and self.calls < self.warmup:
+            self.side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.side):
+                out = tr._update_once(u, her_u)
+            torch.cuda.current_stream().wait_stream(self.side)
+            self.calls += 1
+            return out
+        if self.g_grads is None:
+            self._capture(u, her_u)
+        self._replay()
+        return self.out
+
+    def _replay(self):
+        self.g_grads.replay()
+        if self.tr.agent.grad_sync is not None:
+            self.tr.agent.grad_sync(self.tr.agent.gradients())
+        if self.g_apply is not None:
+            self.g_apply.replay()
+
+    def _capture(self, u, her_u):
+        tr = self.tr
+        torch.cuda.synchronize(tr.device)
+        split = tr.agent.grad_sync is not None
+        def grads_part():
+            s, out = tr._update_grads(u, her_u)
+            if not split:
+                tr._update_apply(s, out)
+            return s, out
+
+        g1, (s, out) = capture_graph(grads_part)
+        if split:
+            self.g_apply, _ = capture_graph(lambda: tr._update_apply(s, out), pool=g1.pool())
+        self.g_grads, self.out = g1, out
+
+
 class Trainer:
     def __init__(self, cfg: Dict, device="cuda", rank: int = 0, world: int = 1, log: bool = True):
         self.cfg, self.rank, self.world = cfg, rank, world
@@ -120,12 +214,17 @@ class Trainer:
             fixed_damage_seed=cfg["fixed_damage_seed"], seeds=seeds, reset=False)
         self.N, self.E = self.env.num_nodes, self.env.num_edges
         amp = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(str(cfg.get("amp")).lower())
+        self.use_graphs = bool(cfg.get("graph_update", True)) and self.device.type == "cuda"
+        if self.use_graphs and not graph_memset_replays_ok(self.device):
+            self.logger.warning("HIP graph memset replay self-test failed; SAC updates run eagerly")
+            self.use_graphs = False
         self.agent = DiscreteSAC(
             4, 6, cfg["hidden_dim"], cfg["embed_dim"], num_layers=cfg["gat_layers"], lr=cfg["lr"],
             actor_lr=cfg["actor_lr"], critic_lr=cfg["critic_lr"], alpha_lr=cfg["alpha_lr"],
             grad_clip=cfg["grad_clip"], gamma=cfg["gamma"], target_tau=cfg["target_tau"],
             share_critic_encoder=cfg["share_critic_encoder"], alpha_init=cfg["alpha_init"],
-            target_entropy_ratio=cfg["target_entropy_ratio"], device=self.device, amp_dtype=amp)
+            target_entropy_ratio=cfg["target_entropy_ratio"], device=self.device, amp_dtype=amp,
+            capturable=self.use_graphs)
         if world > 1:
             import torch.distributed as dist
             for m in (self.agent.actor, self.agent.critic1, self.agent.critic2, self.agent.target1,
@@ -151,6 +250,9 @@ class Trainer:
         self.episodes_done = 0
         self.history = []
         self.last_losses: Dict = {}
+        self._u = torch.empty(bs, dtype=torch.float64, device=self.device)      # PER draws
+        self._her_u = torch.empty(bs, dtype=torch.float32, device=self.device)  # HER draws
+        self._graphed = GraphedUpdate(self) if self.use_graphs else None
 
     # ------------------------------------------------------------ acting
     def act(self, obs, deterministic=False):
@@ -179,20 +281,44 @@ class Trainer:
 
     # ------------------------------------------------------------ update
     def update(self):
+        """One SAC update on a PER batch (src/train.py:954-1024 update block)."""
+        if self._graphed is not None:
+            out = self._graphed()
+        else:
+            out = self._update_once(*self._draw_update_randoms())
+        self.last_losses = out
+        return out
+
+    def _draw_update_randoms(self):
+        self._u.uniform_(generator=self.gen)
+        if self.cfg["her_ratio"] > 0:
+            self._her_u.uniform_(generator=self.gen)
+        return self._u, self._her_u
+
+    def _update_once(self, u, her_u):
+        s, out = self._update_grads(u, her_u)
+        if self.agent.grad_sync is not None:
+            self.agent.grad_sync(self.agent.gradients())
+        self._update_apply(s, out)
+        return out
+
+    def _update_grads(self, u, her_u):
         cfg = self.cfg
         bs = int(cfg["batch_size"])
-        s = self.replay.sample(bs, generator=self.gen)
+        s = self.replay.sample(bs, u=u)
         s = her_relabel(s, cfg["her_ratio"], cfg["reward_mode"], cfg["reward_scale"], cfg["reward_alpha"],
-                        cfg["reward_beta"], cfg["reward_gamma"], cfg["reward_clip"], generator=self.gen)
+                        cfg["reward_beta"], cfg["reward_gamma"], cfg["reward_clip"], u=her_u)
         E, N = self.E, self.N
         action = torch.arange(bs, device=self.device) * E + s.action
         batch = (s.node_x.reshape(bs * N, -1), self.upd_ei, s.edge_x.reshape(bs * E, -1), s.mask.reshape(-1),
                  self.upd_batch, action, s.reward, s.next_node_x.reshape(bs * N, -1), s.next_edge_x.reshape(bs * E, -1),
                  s.next_mask.reshape(-1), self.upd_batch, s.done)
-        out = self.agent.update(batch, weights=s.weights, alpha_max=cfg.get("alpha_max"), sync_metrics=False)
+        out = self.agent.compute_gradients(batch, weights=s.weights)
+        return s, out
+
+    def _update_apply(self, s, out):
+        self.agent.apply_gradients(self.cfg.get("alpha_max"))
         self.replay.update_priorities(s.idx, out["td_errors"])
-        self.last_losses = out
-        return out
 
     # -------------------------------------------------------------- loop
     def iteration(self, obs, it: int):

@@ -104,3 +104,82 @@ def test_short_training_run(tmp_path):
     assert set(sd) == {"actor", "critic1", "critic2", "target1", "target2", "log_alpha"}
     ev = tr.evaluate()
     assert np.isfinite(ev["tstt_last"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("her", [0.0, 0.5])
+def test_graphed_update_matches_eager(tmp_path, her):
+    """The HIP-graph replayed update (train.GraphedUpdate) does the same
+    arithmetic as the eager one: same RNG draws, same PER indices, parameters
+    equal up to kernel-order rounding after several updates."""
+    from trafficrl.train import Trainer, load_config
+    trs = []
+    for graphed in (False, True):
+        cfg = load_config(None)
+        cfg.update(num_envs=32, batch_start=64, batch_size=16, hidden_dim=32, embed_dim=32, eval_every=0,
+                   output_dir=str(tmp_path), update_every=1, her_ratio=her, graph_update=graphed)
+        tr = Trainer(cfg, device="cuda", log=False)
+        trs.append(tr)
+    ag = trs[0].agent   # same (device-side step count) Adam arithmetic in both
+    ag.capturable = True
+    ad = dict(lr=1e-4, capturable=True, foreach=True)
+    ag.actor_opt = torch.optim.Adam(ag.actor.parameters(), **ad)
+    ag.critic_opt = torch.optim.Adam(ag.critic_params, **ad)
+    ag.alpha_opt = torch.optim.Adam([ag.log_alpha], **ad)
+    # identical weights, identical replay contents
+    for m_e, m_g in zip((trs[0].agent.actor, trs[0].agent.critic1, trs[0].agent.critic2, trs[0].agent.target1,
+                         trs[0].agent.target2),
+                        (trs[1].agent.actor, trs[1].agent.critic1, trs[1].agent.critic2, trs[1].agent.target1,
+                         trs[1].agent.target2)):
+        m_g.load_state_dict(m_e.state_dict())
+    obs = []
+    for tr in trs:
+        tr._reset_envs(None)
+        obs.append(tr.env.observe())
+    for it in range(3):
+        a = trs[0].act(obs[0])
+        trs[1].act(obs[1])   # keep both generators in step
+        for k, tr in enumerate(trs):
+            o = obs[k]
+            prev = (o.node_x.clone(), o.edge_x.clone(), o.action_mask.clone())
+            goal, prev_t = tr.env.goal.clone(), tr.env.tstt.clone()
+            nxt, rew, done, _ = tr.env.step(a.to(torch.int32), check=False)
+            tr.replay.add_batch(prev[0], prev[1], prev[2], a, rew * 0.5, nxt.node_x, nxt.edge_x, nxt.action_mask,
+                                done.float(), goal, prev_t, tr.env.tstt, tr.env.initial_tstt)
+            obs[k] = nxt
+    for step in range(6):   # 3 eager warm-up + capture + 2 replays on the graphed trainer
+        outs = [tr.update() for tr in trs]
+        torch.cuda.synchronize()
+        torch.testing.assert_close(outs[1]["td_errors"], outs[0]["td_errors"], rtol=2e-3, atol=2e-4)
+    assert trs[1]._graphed.g_grads is not None
+    for (k, p_e), p_g in zip(trs[0].agent.actor.state_dict().items(), trs[1].agent.actor.state_dict().values()):
+        torch.testing.assert_close(p_g, p_e, rtol=1e-3, atol=1e-4, msg=k)
+    torch.testing.assert_close(trs[1].replay.tree, trs[0].replay.tree, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(trs[1].agent.log_alpha, trs[0].agent.log_alpha)
+
+
+@pytest.mark.gpu
+def test_graph_memset_replay_selftest():
+    """capture_graph rewrites captured memset nodes into fill kernels, so a
+    small hipMemsetAsync replays correctly (ROCm 7.2 packet-capture defect)
+    and the trainer keeps HIP-graph updates enabled."""
+    from trafficrl.train import graph_memset_replays_ok
+    assert graph_memset_replays_ok(torch.device("cuda", 0))
+
+
+@pytest.mark.gpu
+def test_graphed_column_reduction_replays():
+    """Multi-block column sums (Linear bias gradients; torch clears their
+    semaphores with a small memset) equal eager on every replay."""
+    from trafficrl.train import capture_graph
+    x = torch.randn(6144, 1024, device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        x.sum(0)
+    torch.cuda.current_stream().wait_stream(side)
+    g, y = capture_graph(lambda: x.sum(0))
+    for _ in range(4):
+        x.normal_()
+        g.replay()
+        torch.testing.assert_close(y, x.double().sum(0).float(), rtol=1e-4, atol=1e-3)

@@ -1,0 +1,49 @@
+"""Per-phase op profile of the GAT-SAC trainer (acting at B envs, one SAC
+update at batch 256) with torch.profiler; prints the top device-time ops of
+each phase and the wall time per call.  Usage: python tools/agent_profile.py [B]
+"""
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
+
+
+def main():
+    from torch.profiler import ProfilerActivity, profile
+
+    from trafficrl.train import Trainer, load_config
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    cfg = load_config(None)
+    cfg.update(num_envs=B, batch_start=256, eval_every=0, output_dir="/tmp/trx_prof", buffer_size=65536)
+    tr = Trainer(cfg, device="cuda:0", log=False)
+    tr._reset_envs(None)
+    obs = tr.env.observe()
+    for it in range(8):
+        obs, _ = tr.iteration(obs, it)
+    torch.cuda.synchronize()
+
+    def timeit(fn, n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n * 1e3
+
+    print(f"act    wall {timeit(lambda: tr.act(obs), 10):8.3f} ms/call")
+    print(f"update wall {timeit(tr.update, 10):8.3f} ms/call")
+    for name, fn in (("act", lambda: tr.act(obs)), ("update", tr.update)):
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize()
+        print(f"===== {name} (5 calls)")
+        print(prof.key_averages().table(sort_by="self_device_time_total", row_limit=40, max_name_column_width=70))
+
+
+if __name__ == "__main__":
+    main()

@@ -22,13 +22,15 @@ for s in "$@"; do
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py ;;
         benchq) step bench 400 python bench.py --steps 44 --warmup 22 --cpu-seconds 5 ;;
+        benchenv) step bench_env 400 python bench.py --workload env --steps 66 --warmup 22 --no-cpu ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 44 --warmup 22 --no-cpu ;;
-        pmc) step pmc1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --steps 22 --warmup 0 --no-cpu
-             step pmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --steps 22 --warmup 0 --no-cpu
-             step pmc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc3 -o run --output-format csv -- python3 bench.py --steps 22 --warmup 0 --no-cpu
-             step pmc4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc4 -o run --output-format csv -- python3 bench.py --steps 22 --warmup 0 --no-cpu ;;
+        profenv) step profenv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profenv -o run --output-format csv -- python3 bench.py --workload env --steps 44 --warmup 22 --no-cpu ;;
+        pmc) step pmc1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu
+             step pmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu
+             step pmc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc3 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu
+             step pmc4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc4 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu ;;
         stamps) step stamps 300 python tools/phase_stamps.py 4096 ;;
-        epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --steps 44 --warmup 22 --no-cpu; done ;;
+        epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --workload env --steps 44 --warmup 22 --no-cpu; done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
