@@ -169,6 +169,73 @@ int trx_gat_backward(int32_t num_nodes, int32_t heads, int32_t channels, const i
                      const float* alpha, const float* grad_out, float* grad_xh, float* grad_a_src, float* grad_a_dst,
                      float* grad_a_edge, void* stream);
 
+/* ------------------------------------------------ fused GAT inference
+ * Acting (and the no-grad target/next-state passes of the SAC update) run
+ * the whole GATEncoder layer (src/models/gat_encoder.py:36-52) as ONE kernel
+ * per layer, one workgroup per graph: the graph's xh rows are staged in LDS
+ * once, then attention logits (PyG GATConv: <xh,att_src>, <xh,att_dst>,
+ * a_edge, leaky_relu, softmax over in-edges +1e-16), neighbour aggregation,
+ * + bias, LayerNorm, residual (layer 0: input_proj(x) computed in-kernel;
+ * later layers: the previous layer's output), ReLU / ELU and, on the last
+ * layer, global mean|max pooling.  The dense `lin` projection of layers >= 1
+ * stays a bf16 MFMA GEMM on the torch side.  Batches must be regular: graph
+ * b owns nodes [b*n, (b+1)*n) and its CSR-by-destination range, n <= 32,
+ * <= 256 edges (self loops included) per graph.  Numerics follow the
+ * bf16-autocast torch path (bf16 roundings at the same points).             */
+typedef struct trx_gat_layer_args {
+    int32_t num_graphs, nodes_per_graph, heads, channels, concat;
+    int32_t max_graph_edges;    /* CSR positions per graph (self loops included), <= 256;
+                                   a graph with more gets NaN outputs */
+    int32_t in_dim;             /* 4: layer 0, xh = bf16(x0 @ w0^T) in-kernel; 0: xh given */
+    const void* xh;             /* bf16 [N, heads*channels]                   (in_dim == 0) */
+    const float* x0;            /* [N, in_dim] layer input                    (in_dim > 0)  */
+    const float* w0;            /* [heads*channels, in_dim] lin.weight, bf16-representable  */
+    const int32_t* rowptr;      /* [N+1] CSR by destination (self loops included)           */
+    const int32_t* col;         /* [Et]  source node of each CSR position                   */
+    const float* a_edge;        /* [Et, a_edge_stride] edge logits in CSR order             */
+    int32_t a_edge_stride, a_edge_offset;
+    const float* att_src;       /* [heads*channels] */
+    const float* att_dst;       /* [heads*channels] */
+    const float* bias;          /* [out] (out = concat ? heads*channels : channels)         */
+    float negative_slope;
+    const float* ln_weight;     /* [out] */
+    const float* ln_bias;       /* [out] */
+    float ln_eps;
+    int32_t residual;           /* 0 none, 1 res [N,out] fp32, 2 bf16(x0 @ wp^T + bp)       */
+    const float* res;
+    const float* wp;            /* [out, in_dim] bf16-representable */
+    const float* bp;            /* [out] bf16-representable */
+    int32_t activation;         /* 0 relu, 1 elu */
+    float* out_f32;             /* [N, out] or NULL */
+    void* out_bf16;             /* [N, out] bf16 or NULL */
+    float* pool;                /* [num_graphs, 2*out] mean | max, or NULL */
+} trx_gat_layer_args;
+int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
+
+/* Edge scorer of Actor/Critic (src/rl/sac.py:42-46, 69-78) for regular
+ * batches, one workgroup per graph:
+ *   z = bf16(bf16(p[src,:H] + p[dst,H:]) + bf16(bf16(ea) @ we^T)) + c[graph]
+ *   logit = bf16(bf16(relu(z)) . w2 + b2)
+ * p [N, 2H] bf16 = node_emb @ [W_src; W_dst]^T, c [B, H] fp32 = bf16(ctx @ W_ctx^T) + b1.
+ * softmax != 0: logits masked (mask <= 0 -> -1e9) and soft-maxed per graph
+ * (Actor probs); else raw logits (Critic Q).  hidden <= 512, edge_dim <= 8. */
+typedef struct trx_edge_head_args {
+    int32_t num_graphs, edges_per_graph, hidden, edge_dim;
+    const int32_t* src;         /* [B*E] global node ids */
+    const int32_t* dst;
+    const void* p;              /* bf16 [N, 2*hidden] */
+    const float* c;             /* [B, hidden] */
+    const float* ea;            /* [B*E, edge_dim] normalised edge features */
+    const float* we;            /* [hidden, edge_dim] bf16-representable */
+    const float* w2;            /* [hidden] bf16-representable */
+    const float* b2;            /* [1] bf16-representable (device: no host read) */
+    const float* mask;          /* [B*E] (softmax only) */
+    int32_t softmax;
+    float* out;                 /* [B*E] probs (softmax) or logits */
+    float* logits;              /* [B*E] masked logits when softmax, or NULL */
+} trx_edge_head_args;
+int trx_edge_head_infer(const trx_edge_head_args* a, void* stream);
+
 /* ------------------------------------------------- prioritized replay
  * Sum tree of src/train.py:27-91 (ReplayBuffer) on the device: tree[1] is the
  * root, leaf i is tree[capacity + i], children of k are 2k, 2k+1; float64.

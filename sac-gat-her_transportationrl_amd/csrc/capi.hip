@@ -336,6 +336,51 @@ int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_
     return TRX_OK;
 }
 
+int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_layer_infer: NULL args");
+    const int HC = a->heads * a->channels;
+    if (a->num_graphs < 0) return fail(TRX_EINVAL, "gat_layer_infer: num_graphs < 0");
+    if (a->nodes_per_graph < 1 || a->nodes_per_graph > 32)
+        return fail(TRX_EUNSUP, "gat_layer_infer: nodes_per_graph must be 1..32 (got %d)", a->nodes_per_graph);
+    if (a->heads < 1 || a->heads > 8 || a->channels % 4 != 0 || (HC != 256 && HC != 512 && HC != 1024))
+        return fail(TRX_EUNSUP, "gat_layer_infer: heads*channels must be 256, 512 or 1024 (got %d x %d)", a->heads,
+                    a->channels);
+    if (!a->concat && a->heads != 1) return fail(TRX_EUNSUP, "gat_layer_infer: concat=False needs heads == 1");
+    if (a->max_graph_edges < 1 || a->max_graph_edges > 256)
+        return fail(TRX_EUNSUP, "gat_layer_infer: max_graph_edges must be 1..256");
+    if (a->in_dim != 0 && a->in_dim != 4) return fail(TRX_EUNSUP, "gat_layer_infer: in_dim must be 0 or 4");
+    if (a->channels > 256) return fail(TRX_EUNSUP, "gat_layer_infer: channels must be <= 256");
+    if (a->in_dim == 0 ? !a->xh : (!a->x0 || !a->w0)) return fail(TRX_EINVAL, "gat_layer_infer: NULL layer input");
+    if (!a->rowptr || !a->col || !a->a_edge || !a->att_src || !a->att_dst || !a->bias || !a->ln_weight ||
+        !a->ln_bias)
+        return fail(TRX_EINVAL, "gat_layer_infer: NULL parameter buffer");
+    if (a->a_edge_stride < a->a_edge_offset + a->heads || a->a_edge_offset < 0)
+        return fail(TRX_EINVAL, "gat_layer_infer: a_edge stride/offset");
+    if (a->residual == 1 ? !a->res : a->residual == 2 ? (!a->wp || !a->bp || a->in_dim == 0) : a->residual != 0)
+        return fail(TRX_EINVAL, "gat_layer_infer: bad residual spec");
+    if (a->activation != 0 && a->activation != 1) return fail(TRX_EINVAL, "gat_layer_infer: activation 0|1");
+    if (!a->out_f32 && !a->out_bf16 && !a->pool) return fail(TRX_EINVAL, "gat_layer_infer: no output");
+    if (trx::gat_layer_infer_smem(*a) > 160 * 1024) return fail(TRX_EUNSUP, "gat_layer_infer: LDS > 160 KB");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_gat_layer_infer(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_layer_infer launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "edge_head_infer: NULL args");
+    if (a->num_graphs < 0 || a->edges_per_graph < 1 || a->edges_per_graph > 4096)
+        return fail(TRX_EUNSUP, "edge_head_infer: edges_per_graph must be 1..4096");
+    if (a->hidden < 1 || a->hidden > 512 || a->edge_dim < 1 || a->edge_dim > 8)
+        return fail(TRX_EUNSUP, "edge_head_infer: hidden 1..512, edge_dim 1..8");
+    if (!a->src || !a->dst || !a->p || !a->c || !a->ea || !a->we || !a->w2 || !a->b2 || !a->out || (a->softmax && !a->mask))
+        return fail(TRX_EINVAL, "edge_head_infer: NULL buffer");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_edge_head_infer(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "edge_head_infer launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
     if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
     int n = 0;

@@ -21,7 +21,8 @@ REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "
 EXPORTS = (
     "trx_abi_version", "trx_last_error", "trx_graph_create", "trx_graph_destroy", "trx_graph_info",
     "trx_workspace_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe", "trx_gat_forward",
-    "trx_gat_backward", "trx_per_update", "trx_per_sample", "trx_graph_patch_memsets",
+    "trx_gat_backward", "trx_per_update", "trx_per_sample", "trx_graph_patch_memsets", "trx_gat_layer_infer",
+    "trx_edge_head_infer",
 )
 
 
@@ -44,6 +45,32 @@ class TrxState(ctypes.Structure):
 
 _vp = ctypes.c_void_p
 _lib = None
+
+_i32, _f32 = ctypes.c_int32, ctypes.c_float
+
+
+class TrxGatLayerArgs(ctypes.Structure):
+    """trx_gat_layer_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("nodes_per_graph", _i32), ("heads", _i32), ("channels", _i32), ("concat", _i32),
+        ("max_graph_edges", _i32), ("in_dim", _i32),
+        ("xh", _vp), ("x0", _vp), ("w0", _vp), ("rowptr", _vp), ("col", _vp),
+        ("a_edge", _vp), ("a_edge_stride", _i32), ("a_edge_offset", _i32),
+        ("att_src", _vp), ("att_dst", _vp), ("bias", _vp), ("negative_slope", _f32),
+        ("ln_weight", _vp), ("ln_bias", _vp), ("ln_eps", _f32),
+        ("residual", _i32), ("res", _vp), ("wp", _vp), ("bp", _vp),
+        ("activation", _i32),
+        ("out_f32", _vp), ("out_bf16", _vp), ("pool", _vp),
+    ]
+
+
+class TrxEdgeHeadArgs(ctypes.Structure):
+    """trx_edge_head_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("edges_per_graph", _i32), ("hidden", _i32), ("edge_dim", _i32),
+        ("src", _vp), ("dst", _vp), ("p", _vp), ("c", _vp), ("ea", _vp), ("we", _vp), ("w2", _vp),
+        ("b2", _vp), ("mask", _vp), ("softmax", _i32), ("out", _vp), ("logits", _vp),
+    ]
 
 
 class TrafficRLError(RuntimeError):
@@ -82,9 +109,11 @@ def load():
     L.trx_per_update.argtypes = [_vp, ctypes.c_int64, _vp, _vp, ctypes.c_int32, _vp]
     L.trx_per_sample.argtypes = [_vp, ctypes.c_int64, _vp, ctypes.c_int32, _vp, _vp, _vp]
     L.trx_graph_patch_memsets.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32)]
+    L.trx_gat_layer_infer.argtypes = [ctypes.POINTER(TrxGatLayerArgs), _vp]
+    L.trx_edge_head_infer.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp]
     for name in ("trx_graph_create", "trx_graph_destroy", "trx_graph_info", "trx_assign", "trx_reset", "trx_step",
                  "trx_observe", "trx_gat_forward", "trx_gat_backward", "trx_per_update", "trx_per_sample",
-                 "trx_graph_patch_memsets"):
+                 "trx_graph_patch_memsets", "trx_gat_layer_infer", "trx_edge_head_infer"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != 1:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != 1")

@@ -1,0 +1,201 @@
+"""Fused bf16 inference path of the GAT-SAC networks (csrc/gat_infer.hip).
+
+Used by Actor.forward / Critic.forward (rl/sac.py) when no gradient is
+needed, bf16 autocast is active and the batch is a regular batch of
+same-size graphs (the trainer's acting pass over 4096 envs, and the
+next-state actor / target critic passes inside the SAC update).  Anything
+else takes the general autograd path, which computes the same function.
+
+Per encoder layer: one bf16 MFMA GEMM for `lin` (layers >= 1; layer 0's
+4-wide input is projected inside the kernel) + one trx_gat_layer_infer
+launch; then one GEMM for the per-node edge-MLP projections and one
+trx_edge_head_infer launch for the edge scores / masked softmax.  The
+intermediate tensors are bf16 [N, H*C] (plus one fp32 residual), instead
+of ~10 fp32 [N, H*C] tensors per layer.
+
+Numerics: the same bf16 rounding points as torch autocast on the general
+path (lin outputs, a_edge, the edge-MLP GEMM inputs/outputs); the kernel's
+fp32 reductions (attention dot products, LayerNorm moments, pooling) run in
+a different order, so the two paths agree to ~1e-2 relative on logits --
+tests/test_gat_infer.py states the tolerances.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .. import _lib
+from .gat_encoder import GATEncoder, GraphCSR, _LoopMean, build_csr, is_regular_batch
+
+
+@dataclass
+class Topology:
+    B: int
+    n: int                  # nodes per graph
+    e: int                  # input edges per graph
+    g: GraphCSR
+    max_graph_edges: int    # CSR positions per graph (self loops included)
+    src32: torch.Tensor
+    dst32: torch.Tensor
+
+
+_topo_cache: Dict[Tuple, Optional[Topology]] = {}
+
+
+def topology(edge_index: torch.Tensor, batch: torch.Tensor, B: int) -> Optional[Topology]:
+    """Regular-batch description of (edge_index, batch), or None when the
+    fused kernels cannot take it.  Host checks run once per tensor pair."""
+    key = (edge_index.data_ptr(), edge_index._version, batch.data_ptr(), batch._version, edge_index.shape[1],
+           batch.numel(), B)
+    if key in _topo_cache:
+        return _topo_cache[key]
+    topo = None
+    N, E = batch.numel(), edge_index.shape[1]
+    if B > 0 and N % B == 0 and E % B == 0 and is_regular_batch(batch, B):
+        n, e = N // B, E // B
+        src, dst = edge_index[0].long(), edge_index[1].long()
+        eb = torch.arange(B, device=batch.device).repeat_interleave(e)
+        same = bool(torch.equal(src // n, eb)) and bool(torch.equal(dst // n, eb))
+        if same and n <= 32:
+            g = build_csr(edge_index, N)
+            per = g.rowptr.view(-1)[:: n].diff() if N else g.rowptr
+            mx = int(per.max()) if per.numel() else 0
+            if 0 < mx <= 256:
+                topo = Topology(B, n, e, g, mx, src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous())
+    if len(_topo_cache) > 64:
+        _topo_cache.clear()
+    _topo_cache[key] = topo
+    return topo
+
+
+def autocast_bf16() -> bool:
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+def encoder_supported(enc: GATEncoder) -> bool:
+    layers = list(enc.layers)
+    if len(layers) < 2 or layers[0].in_channels != 4 or layers[0].lin_edge is None or layers[0].edge_dim > 8:
+        return False
+    for i, l in enumerate(layers):
+        last = i == len(layers) - 1
+        hc = l.heads * l.out_channels
+        if hc not in (256, 512, 1024) or l.lin_edge is None or l.bias is None:
+            return False
+        if last and (l.concat or l.heads != 1 or hc > 512):
+            return False
+        if not last and not l.concat:
+            return False
+    return True
+
+
+def _bf16r(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().to(torch.bfloat16).float().contiguous()
+
+
+def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology):
+    """GATEncoder.forward (gat_encoder.py) for a regular batch, no grad, bf16
+    autocast semantics.  Returns (node_emb bf16 [N, out], global ctx fp32
+    [B, 2*out])."""
+    L = _lib.load()
+    g = topo.g
+    dev = x.device
+    N = x.shape[0]
+    layers = list(enc.layers)
+    x = x.float().contiguous()
+    ea = edge_attr if g.kept_idx is None else edge_attr.index_select(0, g.kept_idx)
+    ea = ea.float()
+    full = torch.cat([ea, _LoopMean.apply(ea, g)], 0)
+    Ms = [(l.lin_edge.weight.view(l.heads, l.out_channels, -1).float() * l.att_edge.view(l.heads, l.out_channels, 1)
+           .float()).sum(1) for l in layers]
+    offs = [0]
+    for M in Ms:
+        offs.append(offs[-1] + M.shape[0])
+    a_all = (full @ torch.cat(Ms, 0).t())            # bf16 under autocast, like GATConv's a_edge
+    a_all = a_all[g.perm].float().contiguous()        # CSR order
+    stride = a_all.shape[1]
+    stream = _lib.stream_ptr(dev)
+    prev_f32, prev_bf16 = None, None
+    emb = ctx = None
+    for i, l in enumerate(layers):
+        last = i == len(layers) - 1
+        HC = l.heads * l.out_channels
+        args = _lib.TrxGatLayerArgs()
+        args.num_graphs, args.nodes_per_graph, args.heads, args.channels = topo.B, topo.n, l.heads, l.out_channels
+        args.concat, args.max_graph_edges = int(l.concat), topo.max_graph_edges
+        keep = []
+        if i == 0:
+            w0 = _bf16r(l.lin.weight)
+            wp, bp = _bf16r(enc.input_proj.weight), _bf16r(enc.input_proj.bias)
+            keep += [w0, wp, bp]
+            args.in_dim, args.x0, args.w0 = x.shape[1], x.data_ptr(), w0.data_ptr()
+            args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
+        else:
+            xh = torch.mm(prev_bf16, l.lin.weight.detach().to(torch.bfloat16).t())
+            keep.append(xh)
+            args.in_dim, args.xh = 0, xh.data_ptr()
+            if last:
+                args.residual = 0
+            else:
+                args.residual, args.res = 1, prev_f32.data_ptr()
+        att_s = l.att_src.detach().float().reshape(-1).contiguous()
+        att_d = l.att_dst.detach().float().reshape(-1).contiguous()
+        bias = l.bias.detach().float().contiguous()
+        norm = enc.norms[i]
+        lw, lb = norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous()
+        keep += [att_s, att_d, bias, lw, lb]
+        args.rowptr, args.col = g.rowptr.data_ptr(), g.col.data_ptr()
+        args.a_edge, args.a_edge_stride, args.a_edge_offset = a_all.data_ptr(), stride, offs[i]
+        args.att_src, args.att_dst, args.bias = att_s.data_ptr(), att_d.data_ptr(), bias.data_ptr()
+        args.negative_slope = float(l.negative_slope)
+        args.ln_weight, args.ln_bias, args.ln_eps = lw.data_ptr(), lb.data_ptr(), float(norm.eps)
+        args.activation = 1 if last else 0
+        out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+        args.out_bf16 = out_bf16.data_ptr()
+        out_f32 = None
+        if last:
+            ctx = torch.empty(topo.B, 2 * HC, device=dev, dtype=torch.float32)
+            args.pool = ctx.data_ptr()
+        elif i + 1 < len(layers) - 1:   # the next layer is a middle layer: it needs our fp32 output as residual
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32)
+            args.out_f32 = out_f32.data_ptr()
+        _lib.check(L.trx_gat_layer_infer(args, stream), "trx_gat_layer_infer")
+        prev_f32, prev_bf16 = out_f32, out_bf16
+        emb = out_bf16
+        del keep
+    return emb, ctx
+
+
+def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: torch.Tensor, topo: Topology,
+                    mask: Optional[torch.Tensor] = None):
+    """_EdgeHead.edge_scores (+ the Actor's mask and per-graph softmax when
+    `mask` is given).  Returns logits (Critic) or (masked logits, probs)."""
+    L = _lib.load()
+    dev = emb_bf16.device
+    W1, b1 = head.edge_mlp[0].weight, head.edge_mlp[0].bias
+    d, k = head.embed, head.edge_in
+    hid = W1.shape[0]
+    w_nodes = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0).detach().to(torch.bfloat16)
+    p = torch.mm(emb_bf16, w_nodes.t()).contiguous()                      # bf16 [N, 2*hid]
+    c = (ctx @ W1[:, 2 * d + k:].t() + b1).float().contiguous()           # autocast: bf16 GEMM + fp32 bias
+    we = _bf16r(W1[:, 2 * d:2 * d + k])
+    w2 = _bf16r(head.edge_mlp[2].weight.reshape(-1))
+    b2 = _bf16r(head.edge_mlp[2].bias.reshape(-1))                     # stays on the device (graph capture)
+    ea = edge_attr.float().contiguous()
+    BE = topo.B * topo.e
+    out = torch.empty(BE, device=dev, dtype=torch.float32)
+    logits = torch.empty(BE, device=dev, dtype=torch.float32) if mask is not None else None
+    m = mask.float().contiguous() if mask is not None else None
+    args = _lib.TrxEdgeHeadArgs()
+    args.num_graphs, args.edges_per_graph, args.hidden, args.edge_dim = topo.B, topo.e, hid, k
+    args.src, args.dst, args.p, args.c = topo.src32.data_ptr(), topo.dst32.data_ptr(), p.data_ptr(), c.data_ptr()
+    args.ea, args.we, args.w2, args.b2 = ea.data_ptr(), we.data_ptr(), w2.data_ptr(), b2.data_ptr()
+    args.mask = 0 if m is None else m.data_ptr()
+    args.softmax = 1 if mask is not None else 0
+    args.out = out.data_ptr()
+    args.logits = 0 if logits is None else logits.data_ptr()
+    _lib.check(L.trx_edge_head_infer(args, _lib.stream_ptr(dev)), "trx_edge_head_infer")
+    if mask is None:
+        return out
+    return logits, out

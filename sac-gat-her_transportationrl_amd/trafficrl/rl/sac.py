@@ -27,6 +27,7 @@ import torch
 from torch import nn
 import torch.nn.functional as F
 
+from ..models import fused
 from ..models.gat_encoder import GATEncoder, is_regular_batch
 
 
@@ -117,6 +118,18 @@ def clip_grad_norm_listwise_(params, max_norm: float):
     return total
 
 
+FUSED_INFERENCE = True   # module switch (tests compare both paths)
+
+
+def _fused_topology(encoder, node_x, edge_index, batch, B):
+    """Topology for the fused inference kernels, or None -> general path.
+    Taken only without autograd, under bf16 autocast, on the GPU."""
+    if (not FUSED_INFERENCE or torch.is_grad_enabled() or not node_x.is_cuda or not fused.autocast_bf16()
+            or not fused.encoder_supported(encoder)):
+        return None
+    return fused.topology(edge_index, batch, B)
+
+
 class _EdgeHead(nn.Module):
     """Owner of edge_mlp (state_dict keys edge_mlp.0.*, edge_mlp.2.*)."""
 
@@ -149,6 +162,11 @@ class Actor(_EdgeHead):
         node_x = input_layer_norm(self.node_norm, node_x)
         edge_attr = input_layer_norm(self.edge_norm, edge_attr)
         B = num_graphs if num_graphs is not None else int(batch.max()) + 1
+        topo = _fused_topology(self.encoder, node_x, edge_index, batch, B) if not return_attention else None
+        if topo is not None:
+            emb, ctx = fused.encoder_infer(self.encoder, node_x, edge_attr, topo)
+            logits, probs = fused.edge_head_infer(self, emb, ctx, edge_attr, topo, mask=action_mask)
+            return logits, probs, None
         node_emb, global_ctx, attn = self.encoder(node_x, edge_index, edge_attr, batch,
                                                   return_attention=return_attention, num_graphs=B)
         src, dst = edge_index
@@ -173,6 +191,10 @@ class Critic(_EdgeHead):
         node_x = input_layer_norm(self.node_norm, node_x)
         edge_attr = input_layer_norm(self.edge_norm, edge_attr)
         B = num_graphs if num_graphs is not None else int(batch.max()) + 1
+        topo = _fused_topology(self.encoder, node_x, edge_index, batch, B)
+        if topo is not None:
+            emb, ctx = fused.encoder_infer(self.encoder, node_x, edge_attr, topo)
+            return fused.edge_head_infer(self, emb, ctx, edge_attr, topo)
         node_emb, global_ctx, _ = self.encoder(node_x, edge_index, edge_attr, batch, num_graphs=B)
         src, dst = edge_index
         return self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, batch[src]).float()

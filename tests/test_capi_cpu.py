@@ -99,3 +99,41 @@ def test_damage_sampler_matches_reference_seeds():
     fixed = DamageSampler(G, 0, fixed_damage=True, fixed_damage_seed=42).sample(0.3)
     r = np.load(golden("sf_reset_seed42_crpow.npz"))
     np.testing.assert_array_equal(fixed, r["msa30_damaged"])
+
+
+def test_fused_args_layout_matches_header(tmp_path):
+    """Every field offset of trx_gat_layer_args / trx_edge_head_args as the C
+    compiler lays them out equals the ctypes mirror in trafficrl/_lib.py."""
+    from trafficrl import _lib
+    lines = []
+    for cname, cls in (("trx_gat_layer_args", _lib.TrxGatLayerArgs), ("trx_edge_head_args", _lib.TrxEdgeHeadArgs)):
+        lines.append(f'printf("%zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("%zu\\n", offsetof({cname}, {f}));')
+    src = tmp_path / "probe2.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"trafficrl.h\"\nint main(){" + "".join(lines)
+                   + "return 0;}\n")
+    exe = tmp_path / "probe2"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    vals = list(map(int, subprocess.check_output([str(exe)]).split()))
+    want = []
+    for cls in (_lib.TrxGatLayerArgs, _lib.TrxEdgeHeadArgs):
+        want.append(ctypes.sizeof(cls))
+        want += [getattr(cls, f).offset for f, _ in cls._fields_]
+    assert vals == want
+
+
+def test_fused_infer_validation_without_gpu():
+    """Argument checks run before any HIP call: unsupported shapes are refused
+    with TRX_EUNSUP / TRX_EINVAL and a message."""
+    from trafficrl import _lib
+    L = _lib.load()
+    a = _lib.TrxGatLayerArgs()
+    a.num_graphs, a.nodes_per_graph, a.heads, a.channels, a.concat, a.max_graph_edges = 4, 64, 4, 256, 1, 100
+    assert L.trx_gat_layer_infer(a, None) == -3
+    assert b"nodes_per_graph" in L.trx_last_error()
+    a.nodes_per_graph = 24
+    assert L.trx_gat_layer_infer(a, None) == -1       # NULL layer input
+    h = _lib.TrxEdgeHeadArgs()
+    h.num_graphs, h.edges_per_graph, h.hidden, h.edge_dim = 4, 76, 256, 32
+    assert L.trx_edge_head_infer(h, None) == -3

@@ -1,0 +1,118 @@
+"""Fused GAT-SAC inference (csrc/gat_infer.hip, models/fused.py) against the
+general autograd path of the same modules, both under bf16 autocast.
+
+The fused kernels round to bf16 at the same points as autocast but reduce in
+a different order (attention dot products, LayerNorm moments, pooling), so
+the comparison is to bf16 precision: node embeddings within 3e-2 absolute
+(LayerNorm-scaled values of magnitude ~1), logits within 2% of their range,
+probabilities within 1e-2 absolute, and each graph's fused greedy action
+within 1e-2 probability of the general path's best.  The batch is real
+environment observations (Sioux Falls, 64 envs with random damage) so
+feature scales are the trainer's.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _obs_batch(B=64, seed=0):
+    from trafficrl.data import sioux_falls
+    from trafficrl.env import VecRepairEnv
+    from trafficrl.train import batched_topology
+    env = VecRepairEnv(sioux_falls(), B, device="cuda", seeds=list(range(seed, seed + B)), reset=False)
+    obs = env.reset()
+    N, E = env.num_nodes, env.num_edges
+    ei, bv = batched_topology(env.edge_index, N, B)
+    return (obs.node_x.reshape(B * N, 4).clone(), ei, obs.edge_x.reshape(B * E, 6).clone(),
+            obs.action_mask.reshape(-1).clone(), bv, B, E)
+
+
+def _both(fn):
+    from trafficrl.rl import sac
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        sac.FUSED_INFERENCE = False
+        ref = fn()
+        sac.FUSED_INFERENCE = True
+        got = fn()
+    torch.cuda.synchronize()
+    return ref, got
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_actor_fused_matches_general(seed):
+    from trafficrl.rl.sac import Actor
+    torch.manual_seed(seed)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=seed)
+    (lr, pr, _), (lf, pf, _) = _both(lambda: actor(node_x, ei, ea, mask, bv, num_graphs=B))
+    valid = mask > 0
+    span = (lr[valid].max() - lr[valid].min()).item()
+    assert torch.isfinite(pf).all()
+    assert (lf[valid] - lr[valid]).abs().max().item() <= 0.02 * span + 1e-3
+    assert torch.equal(lf[~valid], lr[~valid])                      # masked to -1e9 on both
+    assert (pf - pr).abs().max().item() < 1e-2
+    torch.testing.assert_close(pf.view(B, E).sum(1), torch.ones(B, device="cuda"), atol=1e-5, rtol=0)
+    # greedy actions agree up to near-ties: the fused argmax is (one of) the
+    # general path's best links within the probability tolerance
+    af = pf.view(B, E).argmax(1)
+    prv = pr.view(B, E)
+    gap = prv.max(1).values - prv.gather(1, af[:, None]).squeeze(1)
+    assert gap.max().item() < 1e-2
+    print(f"max|dlogit| {(lf[valid] - lr[valid]).abs().max().item():.3e} (span {span:.3f}), "
+          f"max|dprob| {(pf - pr).abs().max().item():.3e}, argmax agree "
+          f"{(af == prv.argmax(1)).float().mean().item():.3f}")
+
+
+def test_critic_fused_matches_general():
+    from trafficrl.rl.sac import Critic
+    torch.manual_seed(3)
+    critic = Critic(4, 6, 256, 256, 3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=5)
+    qr, qf = _both(lambda: critic(node_x, ei, ea, bv, B))
+    span = (qr.max() - qr.min()).item()
+    assert (qf - qr).abs().max().item() <= 0.02 * span + 1e-3
+
+
+def test_encoder_fused_matches_general():
+    from trafficrl.models import fused
+    from trafficrl.models.gat_encoder import GATEncoder
+    torch.manual_seed(7)
+    enc = GATEncoder(4, 256, 256, edge_dim=6, heads=4, num_layers=3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=9)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        emb_r, ctx_r, _ = enc(node_x, ei, ea, bv, num_graphs=B)
+        topo = fused.topology(ei, bv, B)
+        assert topo is not None and topo.n == 24 and topo.e == 76 and topo.max_graph_edges == 100
+        emb_f, ctx_f = fused.encoder_infer(enc, node_x, ea, topo)
+    de = (emb_f.float() - emb_r.float()).abs().max().item()
+    dc = (ctx_f - ctx_r.float()).abs().max().item()
+    print(f"max|d emb| {de:.3e}, max|d ctx| {dc:.3e}")
+    assert de < 3e-2 and dc < 3e-2
+
+
+def test_irregular_batch_takes_general_path():
+    """Graphs of different sizes: no fused topology, same call still works."""
+    from trafficrl.models import fused
+    from trafficrl.rl.sac import Actor
+    torch.manual_seed(2)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    sizes = [5, 9, 7]
+    x, eis, bvs, off = [], [], [], 0
+    for b, n in enumerate(sizes):
+        src = torch.arange(n)
+        dst = (src + 1) % n
+        eis.append(torch.stack([torch.cat([src, dst]), torch.cat([dst, src])]) + off)
+        bvs.append(torch.full((n,), b))
+        off += n
+    ei = torch.cat(eis, 1).cuda()
+    bv = torch.cat(bvs).cuda()
+    node_x = torch.randn(off, 4, device="cuda")
+    ea = torch.randn(ei.shape[1], 6, device="cuda")
+    mask = torch.ones(ei.shape[1], device="cuda")
+    assert fused.topology(ei, bv, len(sizes)) is None
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        _, probs, _ = actor(node_x, ei, ea, mask, bv, num_graphs=len(sizes))
+    assert torch.isfinite(probs).all()
+    sums = torch.zeros(len(sizes), device="cuda").index_add_(0, bv[ei[0]], probs)
+    torch.testing.assert_close(sums, torch.ones(len(sizes), device="cuda"), atol=1e-5, rtol=0)

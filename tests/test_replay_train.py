@@ -107,16 +107,18 @@ def test_short_training_run(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("her", [0.0, 0.5])
-def test_graphed_update_matches_eager(tmp_path, her):
+@pytest.mark.parametrize("her,hidden,embed", [(0.0, 32, 32), (0.5, 32, 32), (0.0, 64, 256)])
+def test_graphed_update_matches_eager(tmp_path, her, hidden, embed):
     """The HIP-graph replayed update (train.GraphedUpdate) does the same
     arithmetic as the eager one: same RNG draws, same PER indices, parameters
-    equal up to kernel-order rounding after several updates."""
+    equal up to kernel-order rounding after several updates.  hidden 64 x 4
+    heads / embed 256 puts the no-grad passes on the fused inference kernels
+    inside the captured graph."""
     from trafficrl.train import Trainer, load_config
     trs = []
     for graphed in (False, True):
         cfg = load_config(None)
-        cfg.update(num_envs=32, batch_start=64, batch_size=16, hidden_dim=32, embed_dim=32, eval_every=0,
+        cfg.update(num_envs=32, batch_start=64, batch_size=16, hidden_dim=hidden, embed_dim=embed, eval_every=0,
                    output_dir=str(tmp_path), update_every=1, her_ratio=her, graph_update=graphed)
         tr = Trainer(cfg, device="cuda", log=False)
         trs.append(tr)
