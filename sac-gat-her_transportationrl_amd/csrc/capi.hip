@@ -349,7 +349,8 @@ int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream) {
     if (a->max_graph_edges < 1 || a->max_graph_edges > 256)
         return fail(TRX_EUNSUP, "gat_layer_infer: max_graph_edges must be 1..256");
     if (a->in_dim != 0 && a->in_dim != 4) return fail(TRX_EUNSUP, "gat_layer_infer: in_dim must be 0 or 4");
-    if (a->channels > 256) return fail(TRX_EUNSUP, "gat_layer_infer: channels must be <= 256");
+    if (a->channels > 256 || (a->channels < 64 ? 64 % a->channels : a->channels % 64) != 0 || a->channels % 8 != 0)
+        return fail(TRX_EUNSUP, "gat_layer_infer: channels must be 8..256, dividing or divisible by 64");
     if (a->in_dim == 0 ? !a->xh : (!a->x0 || !a->w0)) return fail(TRX_EINVAL, "gat_layer_infer: NULL layer input");
     if (!a->rowptr || !a->col || !a->a_edge || !a->att_src || !a->att_dst || !a->bias || !a->ln_weight ||
         !a->ln_bias)

@@ -33,16 +33,34 @@ constexpr int kWave = 64;
 constexpr int kInferThreads = 256;
 constexpr int kInferWaves = kInferThreads / kWave;
 
-__device__ __forceinline__ float wave_max_f(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-    return v;
-}
+// Wave-wide reductions on DPP + readlane (no LDS round trips): quad butterflies
+// (xor 1, xor 2), half-row and row mirrors give every lane its 16-lane row
+// total; the four row totals are combined from lanes 0/16/32/48.
+#define TRX_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false))
 __device__ __forceinline__ float wave_sum_f(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+    v = v + TRX_DPP(v, 0xB1);   // quad_perm [1,0,3,2]
+    v = v + TRX_DPP(v, 0x4E);   // quad_perm [2,3,0,1]
+    v = v + TRX_DPP(v, 0x141);  // row_half_mirror
+    v = v + TRX_DPP(v, 0x140);  // row_mirror
+    return (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+           (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
 }
+#define TRX_DPPM(v, ctrl) \
+    __int_as_float(__builtin_amdgcn_update_dpp((int)0xff800000, __float_as_int(v), ctrl, 0xf, 0xf, false))
+__device__ __forceinline__ float wave_max_f(float v) {
+    v = fmaxf(v, TRX_DPPM(v, 0xB1));
+    v = fmaxf(v, TRX_DPPM(v, 0x4E));
+    v = fmaxf(v, TRX_DPPM(v, 0x141));
+    v = fmaxf(v, TRX_DPPM(v, 0x140));
+    return fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))),
+                 fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
+                       __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
+}
+#undef TRX_DPP
+#undef TRX_DPPM
 __device__ __forceinline__ float leaky_f(float x, float slope) { return x > 0.0f ? x : x * slope; }
 
 // fp32 -> bf16 bits, round to nearest even (torch's conversion)
@@ -79,23 +97,21 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
         return;
     }
 
+    const int SL = C < 64 ? C : 64, S = C / SL;          // attention dot-product segments
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // [n][HC] bf16
     float* as_ = reinterpret_cast<float*>(xs + n * HC);  // [n*H]
     float* ad_ = as_ + n * H;                            // [n*H]
-    float* al = ad_ + n * H;                             // [ne*H] attention weights
-    float* ae = al + a.max_graph_edges * H;              // [ne*H] edge logits of this layer
-    int* cl = reinterpret_cast<int*>(ae + a.max_graph_edges * H);  // [ne] source, graph-local
+    const int alsz = a.max_graph_edges * H > 2 * n * H * S ? a.max_graph_edges * H : 2 * n * H * S;
+    float* al = ad_ + n * H;        // [me*H] edge logits, then attention weights (in place)
+    float* part = al;               // [2*n*H*S] partial dot products (step 2 only, aliases al)
+    int* cl = reinterpret_cast<int*>(al + alsz);         // [me] source, graph-local
     int* rp = cl + a.max_graph_edges;                    // [n+1] graph-local row pointers
-    float* x0l = reinterpret_cast<float*>(rp + 33);      // [n*IN]
-    float* yt = x0l + 32 * (IN > 0 ? IN : 1);            // [n][HC] (pool only)
+    float* x0l = reinterpret_cast<float*>(rp + n + 1);   // [n*IN]
+    float* yt = x0l + n * IN;                            // [n][HC] (pool only)
 
     // 0. graph-local CSR slice, edge logits, layer-0 inputs
     for (int v = tid; v <= n; v += kInferThreads) rp[v] = a.rowptr[node0 + v] - ebeg;
     for (int v = tid; v < ne; v += kInferThreads) cl[v] = a.col[ebeg + v] - node0;
-    for (int v = tid; v < ne * H; v += kInferThreads) {
-        const int e = v / H, h = v - e * H;
-        ae[v] = a.a_edge[(size_t)(ebeg + e) * a.a_edge_stride + a.a_edge_offset + h];
-    }
     if (IN > 0)
         for (int v = tid; v < n * IN; v += kInferThreads) x0l[v] = bf16r(a.x0[(size_t)node0 * IN + v]);
     if (IN == 0) {
@@ -124,37 +140,48 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
         __syncthreads();
     }
 
-    // 2. attention dot products: unit u = (h, i), h-major so a wave keeps att in registers
+    // 2. attention dot products <xh[i,h,:], att[h,:]>: every thread takes
+    //    (node, head, 64-wide segment) units, partials are combined in order
     {
-        int hcur = -1;
-        float ats[4], atd[4];  // C <= 256: c = lane + 64m
-        for (int u = wave; u < n * H; u += kInferWaves) {
-            const int h = u / n, i = u - h * n;
-            if (h != hcur) {
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const int c = lane + kWave * m;
-                    ats[m] = c < C ? a.att_src[h * C + c] : 0.0f;
-                    atd[m] = c < C ? a.att_dst[h * C + c] : 0.0f;
-                }
-                hcur = h;
-            }
+        for (int u = tid; u < n * H * S; u += kInferThreads) {
+            const int sg = u % S, ih = u / S, i = ih / H, h = ih - (ih / H) * H;
+            const uint16_t* xr = xs + i * HC + h * C + sg * SL;
+            const float4* s_att = reinterpret_cast<const float4*>(a.att_src + h * C + sg * SL);
+            const float4* d_att = reinterpret_cast<const float4*>(a.att_dst + h * C + sg * SL);
             float s1 = 0.0f, s2 = 0.0f;
+            for (int c = 0; c < SL; c += 8) {
+                const uint4 q = *reinterpret_cast<const uint4*>(xr + c);
+                const float4 sa0 = s_att[c / 4], sa1 = s_att[c / 4 + 1];
+                const float4 da0 = d_att[c / 4], da1 = d_att[c / 4 + 1];
+                const float v[8] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                                    __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u),
+                                    __uint_as_float(q.z << 16), __uint_as_float(q.z & 0xffff0000u),
+                                    __uint_as_float(q.w << 16), __uint_as_float(q.w & 0xffff0000u)};
+                const float sa[8] = {sa0.x, sa0.y, sa0.z, sa0.w, sa1.x, sa1.y, sa1.z, sa1.w};
+                const float da[8] = {da0.x, da0.y, da0.z, da0.w, da1.x, da1.y, da1.z, da1.w};
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int c = lane + kWave * m;
-                if (c < C) {
-                    const float v = bf2f(xs[i * HC + h * C + c]);
-                    s1 += v * ats[m];
-                    s2 += v * atd[m];
+                for (int r = 0; r < 8; ++r) {
+                    s1 += v[r] * sa[r];
+                    s2 += v[r] * da[r];
                 }
             }
-            s1 = wave_sum_f(s1);
-            s2 = wave_sum_f(s2);
-            if (lane == 0) {
-                as_[i * H + h] = s1;
-                ad_[i * H + h] = s2;
+            part[2 * u] = s1;
+            part[2 * u + 1] = s2;
+        }
+        __syncthreads();
+        for (int t = tid; t < n * H; t += kInferThreads) {
+            float s1 = 0.0f, s2 = 0.0f;
+            for (int sg = 0; sg < S; ++sg) {
+                s1 += part[2 * (t * S + sg)];
+                s2 += part[2 * (t * S + sg) + 1];
             }
+            as_[t] = s1;  // t = i*H + h
+            ad_[t] = s2;
+        }
+        __syncthreads();
+        for (int v = tid; v < ne * H; v += kInferThreads) {  // edge logits of this layer into al
+            const int e = v / H, h = v - e * H;
+            al[v] = a.a_edge[(size_t)(ebeg + e) * a.a_edge_stride + a.a_edge_offset + h];
         }
     }
     __syncthreads();
@@ -165,13 +192,13 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
         const int p0 = rp[i], p1 = rp[i + 1];
         const float ad = ad_[t];
         float m = -__builtin_huge_valf();
-        for (int p = p0; p < p1; ++p) m = fmaxf(m, leaky_f(as_[cl[p] * H + h] + ad + ae[p * H + h], a.negative_slope));
+        for (int p = p0; p < p1; ++p) m = fmaxf(m, leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope));
         float ssum = 0.0f;
         for (int p = p0; p < p1; ++p)
-            ssum += __expf(leaky_f(as_[cl[p] * H + h] + ad + ae[p * H + h], a.negative_slope) - m);
+            ssum += __expf(leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope) - m);
         const float denom = ssum + 1e-16f;
-        for (int p = p0; p < p1; ++p)
-            al[p * H + h] = __expf(leaky_f(as_[cl[p] * H + h] + ad + ae[p * H + h], a.negative_slope) - m) / denom;
+        for (int p = p0; p < p1; ++p)  // in place: logit -> attention weight
+            al[p * H + h] = __expf(leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope) - m) / denom;
     }
     __syncthreads();
 
@@ -195,6 +222,11 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
         }
     for (int i = wave; i < n; i += kInferWaves) {
         const int node = node0 + i;
+        float4 res4[KC];  // issue the residual loads before the aggregation (latency overlap)
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+            res4[k] = a.residual == 1 ? *reinterpret_cast<const float4*>(a.res + (size_t)node * HC + 4 * (lane + kWave * k))
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 acc[KC];
 #pragma unroll
         for (int k = 0; k < KC; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -235,9 +267,7 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
             const int f0 = 4 * (lane + kWave * k);
-            float4 res4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (a.residual == 1) res4 = *reinterpret_cast<const float4*>(a.res + (size_t)node * HC + f0);
-            const float resv[4] = {res4.x, res4.y, res4.z, res4.w};
+            const float resv[4] = {res4[k].x, res4[k].y, res4[k].z, res4[k].w};
             float y4[4];
             uint16_t ob[4];
 #pragma unroll
@@ -307,31 +337,45 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         for (int j = 0; j < ED; ++j) we_r[m][j] = (ok && j < D) ? a.we[k * D + j] : 0.0f;
     }
     const float b2 = a.b2[0];
-    for (int e = wave; e < E; e += kInferWaves) {
-        const int eg = g * E + e;
-        const int s = a.src[eg], d = a.dst[eg];
-        float ear[ED];
+    constexpr int EU = 2;  // links per wave iteration: independent loads in flight together
+    for (int e0 = wave * EU; e0 < E; e0 += kInferWaves * EU) {
+        float ear[EU][ED];
+        const uint16_t* ps[EU];
+        const uint16_t* pd[EU];
 #pragma unroll
-        for (int j = 0; j < ED; ++j) ear[j] = j < D ? bf16r(a.ea[(size_t)eg * D + j]) : 0.0f;
-        const uint16_t* ps = p + (size_t)s * 2 * Hd;
-        const uint16_t* pd = p + (size_t)d * 2 * Hd + Hd;
-        float part = 0.0f;
+        for (int u = 0; u < EU; ++u) {
+            const int e = e0 + u < E ? e0 + u : E - 1;
+            const int eg = g * E + e;
+#pragma unroll
+            for (int j = 0; j < ED; ++j) ear[u][j] = j < D ? bf16r(a.ea[(size_t)eg * D + j]) : 0.0f;
+            ps[u] = p + (size_t)a.src[eg] * 2 * Hd;
+            pd[u] = p + (size_t)a.dst[eg] * 2 * Hd + Hd;
+        }
+        float part[EU];
+#pragma unroll
+        for (int u = 0; u < EU; ++u) part[u] = 0.0f;
 #pragma unroll
         for (int m = 0; m < MK; ++m) {
             const int k = lane + kWave * m;
             if (k < Hd) {
-                float ew = 0.0f;
 #pragma unroll
-                for (int j = 0; j < ED; ++j)
-                    if (j < D) ew += ear[j] * we_r[m][j];
-                const float z1 = bf16r(bf2f(ps[k]) + bf2f(pd[k]));
-                const float z2 = bf16r(z1 + bf16r(ew));
-                const float z3 = z2 + c_r[m];
-                part += bf16r(fmaxf(z3, 0.0f)) * w2_r[m];
+                for (int u = 0; u < EU; ++u) {
+                    float ew = 0.0f;
+#pragma unroll
+                    for (int j = 0; j < ED; ++j)
+                        if (j < D) ew += ear[u][j] * we_r[m][j];
+                    const float z1 = bf16r(bf2f(ps[u][k]) + bf2f(pd[u][k]));
+                    const float z2 = bf16r(z1 + bf16r(ew));
+                    const float z3 = z2 + c_r[m];
+                    part[u] += bf16r(fmaxf(z3, 0.0f)) * w2_r[m];
+                }
             }
         }
-        const float t = wave_sum_f(part);
-        if (lane == 0) lg[e] = bf16r(t + b2);
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+            const float t = wave_sum_f(part[u]);
+            if (lane == 0 && e0 + u < E) lg[e0 + u] = bf16r(t + b2);
+        }
     }
     __syncthreads();
     if (!a.softmax) {
@@ -365,8 +409,10 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
 
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a) {
     const int HC = a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
-    size_t b = (size_t)n * HC * 2 + 2 * (size_t)n * H * 4 + 2 * (size_t)me * H * 4 + (size_t)me * 4 + 33 * 4 +
-               32 * 4 * (a.in_dim > 0 ? a.in_dim : 1);
+    const int SL = a.channels < 64 ? a.channels : 64, S = a.channels / SL;
+    const size_t alsz = (size_t)me * H > 2 * (size_t)n * H * S ? (size_t)me * H : 2 * (size_t)n * H * S;
+    size_t b = (size_t)n * HC * 2 + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 + (size_t)(n + 1) * 4 +
+               (size_t)n * a.in_dim * 4;
     if (a.pool) b += (size_t)n * HC * 4;
     return b;
 }

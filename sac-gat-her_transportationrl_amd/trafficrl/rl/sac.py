@@ -104,17 +104,26 @@ def clip_grad_norm_listwise_(params, max_norm: float):
     twice; torch's fused CUDA path instead scales the same tensor from two
     workgroups at once (a read-modify-write race: g*c or g*c^2).  This helper
     always applies the sequential semantics."""
-    grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
-        return torch.zeros(())
-    total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g, 2.0) for g in grads]), 2.0)
-    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
-    mult = {}
+    uniq, count = [], {}
     for p in params:
         if p.grad is not None:
-            mult[id(p)] = (p, mult.get(id(p), (p, 0))[1] + 1)
-    for p, n in mult.values():
-        p.grad.mul_(coef if n == 1 else coef ** n)
+            if id(p) not in count:
+                uniq.append(p)
+                count[id(p)] = 0
+            count[id(p)] += 1
+    if not uniq:
+        return torch.zeros(())
+    # one multi-tensor norm launch instead of a kernel per tensor
+    norms = torch.stack(torch._foreach_norm([p.grad for p in uniq], 2.0))
+    if all(count[id(p)] == 1 for p in uniq):
+        total = torch.linalg.vector_norm(norms, 2.0)
+    else:
+        mult = torch.tensor([float(count[id(p)]) for p in uniq], device=norms.device)
+        total = torch.sqrt((norms * norms * mult).sum())
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    for n in sorted(set(count.values())):
+        group = [p.grad for p in uniq if count[id(p)] == n]
+        torch._foreach_mul_(group, coef if n == 1 else coef ** n)
     return total
 
 
@@ -233,7 +242,7 @@ class DiscreteSAC:
         # capturable: Adam keeps its step count on the device so update() can be
         # replayed from a HIP graph (train.py); same arithmetic otherwise
         self.capturable = capturable
-        adam = dict(capturable=True, foreach=True) if capturable else {}
+        adam = dict(capturable=True, fused=True) if capturable else {}
         self.actor_opt = torch.optim.Adam(self.actor.parameters(), lr=actor_lr, **adam)
         if share_critic_encoder:
             critic_params = (list(self.critic_encoder.parameters()) + list(self.critic1.edge_mlp.parameters())
@@ -261,9 +270,9 @@ class DiscreteSAC:
     def _amp(self):
         if self.amp_dtype is None:
             return torch.autocast("cuda", enabled=False)
-        # no weight-cast cache: a graph-captured update must re-cast the weights
-        # the optimizer changed in place on every replay
-        return torch.autocast("cuda", dtype=self.amp_dtype, cache_enabled=not self.capturable)
+        # the autocast context opens and closes inside every (captured) forward
+        # pass, so its weight-cast cache never outlives one graph replay
+        return torch.autocast("cuda", dtype=self.amp_dtype)
 
     # ------------------------------------------------------------ acting
     def select_action(self, node_x, edge_index, edge_attr, action_mask, deterministic: bool = False) -> SACOutput:
@@ -422,7 +431,7 @@ class DiscreteSAC:
         self.target2.load_state_dict(state["target2"])
         self.log_alpha = state["log_alpha"].to(map_location).requires_grad_()
         lr = self.alpha_opt.param_groups[0]["lr"]
-        adam = dict(capturable=True, foreach=True) if self.capturable else {}
+        adam = dict(capturable=True, fused=True) if self.capturable else {}
         self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=lr, **adam)
 
     @torch.no_grad()

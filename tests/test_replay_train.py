@@ -124,7 +124,7 @@ def test_graphed_update_matches_eager(tmp_path, her, hidden, embed):
         trs.append(tr)
     ag = trs[0].agent   # same (device-side step count) Adam arithmetic in both
     ag.capturable = True
-    ad = dict(lr=1e-4, capturable=True, foreach=True)
+    ad = dict(lr=1e-4, capturable=True, fused=True)
     ag.actor_opt = torch.optim.Adam(ag.actor.parameters(), **ad)
     ag.critic_opt = torch.optim.Adam(ag.critic_params, **ad)
     ag.alpha_opt = torch.optim.Adam([ag.log_alpha], **ad)

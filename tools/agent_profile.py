@@ -1,6 +1,6 @@
 """Per-phase op profile of the GAT-SAC trainer (acting at B envs, one SAC
 update at batch 256) with torch.profiler; prints the top device-time ops of
-each phase and the wall time per call.  Usage: python tools/agent_profile.py [B]
+each phase and the wall time per call.  Usage: python tools/agent_profile.py [B] [act|update]
 """
 import os
 import sys
@@ -34,6 +34,13 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e3
 
+    only = sys.argv[2] if len(sys.argv) > 2 else None
+    if only == "update":   # for rocprofv3: only SAC updates (graph replays after 3 eager warm-ups)
+        print(f"update wall {timeit(tr.update, 30):8.3f} ms/call")
+        return
+    if only == "act":
+        print(f"act    wall {timeit(lambda: tr.act(obs), 30):8.3f} ms/call")
+        return
     print(f"act    wall {timeit(lambda: tr.act(obs), 10):8.3f} ms/call")
     print(f"update wall {timeit(tr.update, 10):8.3f} ms/call")
     for name, fn in (("act", lambda: tr.act(obs)), ("update", tr.update)):
