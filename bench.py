@@ -47,38 +47,49 @@ def bytes_per_assign(N, E, Z, P, K):
     return (K + 1) * 20 * E + K * (Z * (8 * E + 12 * N) + 4 * P + 4 * E + 12 * E) + 8 * E
 
 
-def fixed_damage_mask(E, seed=42, ratio=0.3):
-    from trafficrl.data import sioux_falls
+NETWORKS = {
+    # name: (GraphData loader, golden graph arrays for the CPU baseline, label)
+    "sf": ("sioux_falls", "sf_graph.npz", "SiouxFalls (24 nodes, 76 links, 528 OD)"),
+    "anaheim": ("anaheim_synthetic", "ana_graph.npz",
+                "AnaheimSynth (seeded synthetic Anaheim-size: 416 nodes, 914 links, 38 zones, 1076 OD)"),
+}
+
+
+def load_network(name):
+    import trafficrl.data as D
+    return getattr(D, NETWORKS[name][0])()
+
+
+def fixed_damage_mask(gd, seed=42, ratio=0.3):
     from trafficrl.graph import DamageSampler
 
-    g = sioux_falls()
-
     class _G:
-        num_edges = len(g.edges)
-        num_nodes = g.num_nodes
-        src = np.array([e.u - 1 for e in g.edges], np.int32)
-        dst = np.array([e.v - 1 for e in g.edges], np.int32)
+        num_edges = len(gd.edges)
+        num_nodes = gd.num_nodes
+        src = np.array([e.u - 1 for e in gd.edges], np.int32)
+        dst = np.array([e.v - 1 for e in gd.edges], np.int32)
 
     return DamageSampler(_G, 0, fixed_damage=True, fixed_damage_seed=seed).sample(ratio)
 
 
-def cpu_baseline(method, iters, seconds=12.0):
+def cpu_baseline(network, method, iters, seconds=12.0):
     """Time the oracle's C restatement (same algorithm: scipy-order Dijkstra,
     predecessor path walk, fp32 MSA/FW) on the host cores, warm-started
     steps of the fixed-damage env (one assignment each)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # test/baseline infrastructure only
 
-    og = O.OracleGraph.from_npz(os.path.join(ROOT, "tests", "golden", "sf_graph.npz"))
-    gr = np.load(os.path.join(ROOT, "tests", "golden", "sf_graph.npz"))
+    npz = os.path.join(ROOT, "tests", "golden", NETWORKS[network][1])
+    og = O.OracleGraph.from_npz(npz)
+    gr = np.load(npz)
     E = og.E
-    dmg = fixed_damage_mask(E)
+    dmg = fixed_damage_mask(load_network(network))
     cap = np.where(dmg > 0, np.float32(1e-3), gr["cap0"]).astype(np.float32)
     f0, _, _, _ = og.assign(cap, dmg, np.zeros(E, np.float32), method=method, iters=iters)
     threads = max(1, min(16, os.cpu_count() or 1, O.max_threads()))
     # repair one random damaged link per row, warm start from the reset flow
     rng = np.random.default_rng(7)
-    B = 64 * threads
+    B = (64 if network == "sf" else 4) * threads
     cand = np.where(dmg > 0)[0]
     C = np.repeat(cap[None], B, 0)
     D = np.repeat(dmg[None], B, 0)
@@ -93,7 +104,7 @@ def cpu_baseline(method, iters, seconds=12.0):
         done += B
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "env steps/s", "cores": threads, "kind": "port",
-            "sample": f"{done} warm-started {method.upper()}-{iters} steps (SF, fixed damage seed 42, one repaired "
+            "sample": f"{done} warm-started {method.upper()}-{iters} steps ({network}, fixed damage seed 42, one repaired "
                       f"link each) in {dt:.1f}s on {threads} host threads; oracle/trx_oracle.c"}
 
 
@@ -117,14 +128,24 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=66)
     ap.add_argument("--warmup", type=int, default=22)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--method", default="msa", choices=["msa", "fw", "cfw"])
+    ap.add_argument("--network", default="sf", choices=sorted(NETWORKS),
+                    help="sf = Sioux Falls (configs #1-#4); anaheim = config #5's 416-node network (env workload, "
+                         "1024 envs, FW by default)")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096 sf / 1024 anaheim)")
+    ap.add_argument("--method", default=None, choices=["msa", "fw", "cfw"], help="default msa (sf) / fw (anaheim)")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--no-observe", action="store_true", help="skip get_state (assignment-only steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", default="train", choices=["train", "env"])
+    ap.add_argument("--workload", default=None, choices=["train", "env"], help="default train (sf) / env (anaheim)")
     args = ap.parse_args()
+    big = args.network != "sf"
+    if args.envs is None:
+        args.envs = 1024 if big else 4096
+    if args.method is None:
+        args.method = "fw" if big else "msa"
+    if args.workload is None:
+        args.workload = "env" if big else "train"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -138,11 +159,10 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
 
-    from trafficrl.data import sioux_falls
     from trafficrl.env import VecRepairEnv
 
     B = args.envs
-    gd = sioux_falls()
+    gd = load_network(args.network)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     observe = not args.no_observe
     ev_pairs = []      # env_kernel launches (HIP events on the launch stream)
@@ -199,7 +219,7 @@ def main():
                            reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0, reward_gamma=0.0,
                            reward_clip=2.0, capacity_damage=1e-3, unassigned_penalty=1e4, reset=False)
         E, N = env.num_edges, env.num_nodes
-        dmg0 = torch.from_numpy(fixed_damage_mask(E)).to(dev)
+        dmg0 = torch.from_numpy(fixed_damage_mask(gd)).to(dev)
         dmg_all = dmg0[None].expand(B, E).contiguous()
         ep_len = int(dmg0.sum().item())
         st = {"t": 0}
@@ -256,12 +276,12 @@ def main():
     bpa = bytes_per_assign(N, E, Z, P, args.iters)
     achieved = bpa * B / mean_kernel_s
     traffic, traffic_src = measured_traffic()
-    if (args.envs, args.iters, args.method) != (4096, 30, "msa"):
+    if (args.network, args.envs, args.iters, args.method, args.workload) != ("sf", 4096, 30, "msa", "train"):
         traffic, traffic_src = None, None  # the committed PMC pass is for the default workload
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args.method, args.iters, args.cpu_seconds)
+            cpu = cpu_baseline(args.network, args.method, args.iters, args.cpu_seconds)
         out = {
             "metric": METRIC,
             "value": value,
@@ -275,15 +295,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f32 (link flows/costs) + f64 (path labels)" + (
                 "; bf16 autocast GAT-SAC" if args.workload == "train" else ""),
-            "data": ("synthetic: Sioux Falls TNTP, fixed_damage_seed=42, random-init GAT-SAC (hidden 256, 4 heads, "
-                     "embed 256)" if args.workload == "train" else
-                     "synthetic: Sioux Falls TNTP, fixed_damage_seed=42, uniform random valid repair actions"),
+            "data": (f"synthetic: {'Sioux Falls TNTP' if not big else 'seeded AnaheimSynth TNTP'}, "
+                     "fixed_damage_seed=42, " + ("random-init GAT-SAC (hidden 256, 4 heads, embed 256)"
+                                                 if args.workload == "train" else "uniform random valid repair actions")),
             "config": {
-                "workload": (f"SF {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment + get_state per"
+                "workload": (f"{'SF' if not big else 'AnaheimSynth'} {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment + get_state per"
                              " step" + (", GAT-SAC bf16 acting every step + 1 PER update (batch 256) every 4 steps"
                                         if args.workload == "train" else ", uniform random valid actions")),
                 "workload_kind": args.workload,
-                "envs_per_gpu": B, "global_envs": B * world, "network": "SiouxFalls (24 nodes, 76 links, 528 OD)",
+                "envs_per_gpu": B, "global_envs": B * world, "network": NETWORKS[args.network][2],
                 "method": args.method, "assignment_iters": args.iters, "episode_len": ep_len,
                 "parallelism": f"env-sharded x{world}",
             },
@@ -292,7 +312,7 @@ def main():
                 "frac": achieved / HBM_PEAK, "traffic": traffic,
                 "traffic_note": (f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {traffic_src} "
                                  "(raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic else None,
-                "kernel": "trx::env_kernel<24>", "kernel_mean_ms": mean_kernel_s * 1e3,
+                "kernel": "trx::env_kernel_big" if big else "trx::env_kernel_q<24>", "kernel_mean_ms": mean_kernel_s * 1e3,
                 "bytes_per_assign": bpa, "assigns_per_launch": B,
             },
             "cpu_baseline": cpu,

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 #include "trx_internal.h"
@@ -72,26 +73,22 @@ int check_state(const trx_state* s, bool need_initial) {
     return TRX_OK;
 }
 
-int check_small(const trx_graph* g) {
-    if (!g) return fail(TRX_EINVAL, "graph is NULL");
-    if (g->dg.N > trx::kSmallMaxNodes)
-        return fail(TRX_EUNSUP, "graph has %d nodes; the register-resident kernel supports <= %d", g->dg.N,
-                    trx::kSmallMaxNodes);
-    return TRX_OK;
-}
-
 int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mode, const int32_t* action,
         double* reward, uint8_t* done, uint8_t* valid, const uint8_t* env_mask, void* ws, void* stream) {
     int rc;
-    if ((rc = check_small(g)) || (rc = check_params(p)) || (rc = check_state(s, mode != trx::kModeAssign))) return rc;
+    if (!g) return fail(TRX_EINVAL, "graph is NULL");
+    if ((rc = check_params(p)) || (rc = check_state(s, mode != trx::kModeAssign))) return rc;
     if (B < 0) return fail(TRX_EINVAL, "num_envs < 0");
     if (B == 0) return TRX_OK;
     if (!ws) return fail(TRX_EINVAL, "workspace is NULL (size it with trx_workspace_bytes)");
     hipError_t e = hipSetDevice(g->device);
     if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
-    (void)ws;
-    e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
-                                    static_cast<hipStream_t>(stream));
+    if (g->dg.N <= trx::kSmallMaxNodes)
+        e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
+                                        static_cast<hipStream_t>(stream));
+    else
+        e = trx::launch_env_kernel_big(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws,
+                                       static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
@@ -112,33 +109,37 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     if (N <= 0 || E < 0 || P < 0) return fail(TRX_EINVAL, "bad sizes N=%d E=%d P=%d", N, E, P);
     if (E > 0 && (!src || !dst || !t0 || !cap0)) return fail(TRX_EINVAL, "NULL edge array");
     if (P > 0 && (!od_o || !od_d || !od_v)) return fail(TRX_EINVAL, "NULL OD array");
-    if (N > trx::kSmallMaxNodes)
-        return fail(TRX_EUNSUP, "graph has %d nodes; this build supports <= %d (register-resident kernel)", N,
-                    trx::kSmallMaxNodes);
-    const int NP = N <= 8 ? 8 : N <= 16 ? 16 : N <= 24 ? 24 : 32;
+    if (N > trx::kBigMaxNodes)
+        return fail(TRX_EUNSUP, "graph has %d nodes; this build supports <= %d", N, trx::kBigMaxNodes);
+    if (E > 32767) return fail(TRX_EUNSUP, "graph has %d links; this build supports <= 32767", E);
+    const bool small = N <= trx::kSmallMaxNodes;
+    const int NP = !small ? 0 : N <= 8 ? 8 : N <= 16 ? 16 : N <= 24 ? 24 : 32;
 
-    std::vector<int16_t> eid_of((size_t)NP * NP, -1);
     for (int e = 0; e < E; ++e) {
         if (src[e] < 0 || src[e] >= N || dst[e] < 0 || dst[e] >= N)
             return fail(TRX_EINVAL, "edge %d endpoint out of range", e);
         if (!(t0[e] > 0.0f) || !std::isfinite(t0[e]))
             return fail(TRX_EUNSUP, "edge %d has non-positive free-flow time %g", e, (double)t0[e]);
-        int16_t& slot = eid_of[(size_t)src[e] * NP + dst[e]];
-        if (slot >= 0) return fail(TRX_EUNSUP, "parallel links %d->%d (scipy csr_matrix would sum them)", src[e], dst[e]);
-        slot = (int16_t)e;
     }
-    // scipy CSR: rows by source, columns ascending
-    std::vector<int32_t> indptr(N + 1, 0), indices, csr_eid;
-    for (int u = 0; u < N; ++u) {
-        for (int v = 0; v < N; ++v) {
-            int e = eid_of[(size_t)u * NP + v];
-            if (e >= 0) {
-                indices.push_back(v);
-                csr_eid.push_back(e);
-            }
-        }
-        indptr[u + 1] = (int32_t)indices.size();
+    // scipy CSR: rows by source, columns ascending (csr_matrix((w,(row,col))))
+    std::vector<int32_t> order(E);
+    for (int e = 0; e < E; ++e) order[e] = e;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+        return src[a] != src[b] ? src[a] < src[b] : dst[a] < dst[b];
+    });
+    std::vector<int32_t> indptr(N + 1, 0), indices(E), csr_eid(E);
+    for (int k = 0; k < E; ++k) {
+        const int e = order[k];
+        if (k > 0 && src[order[k - 1]] == src[e] && dst[order[k - 1]] == dst[e])
+            return fail(TRX_EUNSUP, "parallel links %d->%d (scipy csr_matrix would sum them)", src[e], dst[e]);
+        indices[k] = dst[e];
+        csr_eid[k] = e;
+        indptr[src[e] + 1]++;
     }
+    for (int u = 0; u < N; ++u) indptr[u + 1] += indptr[u];
+    std::vector<int16_t> eid_of(small ? (size_t)NP * NP : 1, -1);
+    if (small)
+        for (int e = 0; e < E; ++e) eid_of[(size_t)src[e] * NP + dst[e]] = (int16_t)e;
     // origins = nodes with at least one OD entry (repair_env.py:490-493)
     std::vector<int> has(N, 0);
     double total = 0.0;
@@ -161,8 +162,20 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
         }
     const int Z = (int)origins.size();
     if (Z == 0) return fail(TRX_EUNSUP, "no OD demand");
-    std::vector<float> dem((size_t)Z * N, 0.0f);
-    for (int k = 0; k < P; ++k) dem[(size_t)zone_of[od_o[k]] * N + od_d[k]] = (float)od_v[k];
+    std::vector<float> dem(small ? (size_t)Z * N : 1, 0.0f);
+    if (small)
+        for (int k = 0; k < P; ++k) dem[(size_t)zone_of[od_o[k]] * N + od_d[k]] = (float)od_v[k];
+    // OD entries grouped per origin zone, dict order kept (repair_env.py:491)
+    std::vector<int32_t> od_ptr(Z + 1, 0), od_dst(P > 0 ? P : 1), od_pos(Z, 0);
+    std::vector<float> od_dem(P > 0 ? P : 1);
+    for (int k = 0; k < P; ++k) od_ptr[zone_of[od_o[k]] + 1]++;
+    for (int z = 0; z < Z; ++z) od_ptr[z + 1] += od_ptr[z];
+    for (int k = 0; k < P; ++k) {
+        int z = zone_of[od_o[k]];
+        int at = od_ptr[z] + od_pos[z]++;
+        od_dst[at] = od_d[k];
+        od_dem[at] = (float)od_v[k];
+    }
     // networkx node insertion order (repair_env.py:106-109)
     std::vector<int32_t> nx_order;
     std::vector<int> seen(N, 0);
@@ -174,21 +187,105 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
             }
     for (int n = 0; n < N; ++n)
         if (!seen[n]) nx_order.push_back(n);
-    // adjacency views for the observation kernel
-    std::vector<int32_t> out_ptr(N + 1, 0), out_dst, out_eid, in_ptr(N + 1, 0), in_src, in_eid;
+    // adjacency views (file order within a node) for the observation kernels
+    std::vector<int32_t> out_ptr(N + 1, 0), out_dst(E > 0 ? E : 1), out_eid(E > 0 ? E : 1), in_ptr(N + 1, 0),
+        in_src(E > 0 ? E : 1), in_eid(E > 0 ? E : 1);
+    for (int e = 0; e < E; ++e) {
+        out_ptr[src[e] + 1]++;
+        in_ptr[dst[e] + 1]++;
+    }
     for (int u = 0; u < N; ++u) {
-        for (int e = 0; e < E; ++e)
-            if (src[e] == u) {
-                out_dst.push_back(dst[e]);
-                out_eid.push_back(e);
+        out_ptr[u + 1] += out_ptr[u];
+        in_ptr[u + 1] += in_ptr[u];
+    }
+    {
+        std::vector<int32_t> op(out_ptr.begin(), out_ptr.end() - 1), ip(in_ptr.begin(), in_ptr.end() - 1);
+        for (int e = 0; e < E; ++e) {
+            int a = op[src[e]]++;
+            out_dst[a] = dst[e];
+            out_eid[a] = e;
+            int b = ip[dst[e]]++;
+            in_src[b] = src[e];
+            in_eid[b] = e;
+        }
+    }
+    if (!small)
+        for (int u = 0; u < N; ++u)
+            if (out_ptr[u + 1] - out_ptr[u] > 64)
+                return fail(TRX_EUNSUP, "node %d has %d out-links; the large-graph kernels take <= 64", u,
+                            out_ptr[u + 1] - out_ptr[u]);
+    // large-graph kernel: packed in-link lists.  Nodes in DFS preorder of the
+    // undirected graph (neighbours ascending) are dealt to the 64 lanes in
+    // contiguous chunks balanced by entry count, so consecutive nodes of a
+    // lane are mostly adjacent and one Gauss-Seidel sweep carries a label
+    // along the whole chunk (assign_big.hip).
+    int KMAX = 0;
+    std::vector<uint32_t> blist(1, 0);
+    std::vector<int16_t> blink(1, -1);
+    if (!small) {
+        std::vector<std::vector<int>> und(N);
+        for (int e = 0; e < E; ++e) {
+            und[src[e]].push_back(dst[e]);
+            und[dst[e]].push_back(src[e]);
+        }
+        for (auto& a : und) {
+            std::sort(a.begin(), a.end());
+            a.erase(std::unique(a.begin(), a.end()), a.end());
+        }
+        std::vector<int32_t> perm;
+        std::vector<char> vis(N, 0);
+        for (int r = 0; r < N; ++r) {
+            if (vis[r]) continue;
+            std::vector<int> stack{r};
+            while (!stack.empty()) {
+                int v = stack.back();
+                stack.pop_back();
+                if (vis[v]) continue;
+                vis[v] = 1;
+                perm.push_back(v);
+                for (auto it = und[v].rbegin(); it != und[v].rend(); ++it)
+                    if (!vis[*it]) stack.push_back(*it);
             }
-        out_ptr[u + 1] = (int32_t)out_dst.size();
-        for (int e = 0; e < E; ++e)
-            if (dst[e] == u) {
-                in_src.push_back(src[e]);
-                in_eid.push_back(e);
+        }
+        auto cost = [&](int v) { return std::max(1, in_ptr[v + 1] - in_ptr[v]); };
+        int tot = 0;
+        for (int v = 0; v < N; ++v) tot += cost(v);
+        std::vector<int> lane_start;
+        for (int T = (tot + trx::kBigLanes - 1) / trx::kBigLanes;; ++T) {
+            lane_start.assign(1, 0);
+            int acc = 0;
+            for (int i = 0; i < N; ++i) {
+                if (acc > 0 && acc + cost(perm[i]) > T) {
+                    lane_start.push_back(i);
+                    acc = 0;
+                }
+                acc += cost(perm[i]);
             }
-        in_ptr[u + 1] = (int32_t)in_src.size();
+            if ((int)lane_start.size() <= trx::kBigLanes) {
+                KMAX = T;
+                break;
+            }
+        }
+        while ((int)lane_start.size() < trx::kBigLanes) lane_start.push_back(N);
+        lane_start.push_back(N);
+        blist.assign((size_t)KMAX * trx::kBigLanes, 0u);
+        blink.assign((size_t)KMAX * trx::kBigLanes, -1);
+        for (int l = 0; l < trx::kBigLanes; ++l) {
+            int k = 0;
+            for (int i = lane_start[l]; i < lane_start[l + 1]; ++i) {
+                const int v = perm[i];
+                const int n = in_ptr[v + 1] - in_ptr[v];
+                for (int q = 0; q < std::max(1, n); ++q) {
+                    const int u = n ? in_src[in_ptr[v] + q] : v;
+                    uint32_t word = (uint32_t)u | ((uint32_t)v << 16);
+                    if (q == 0) word |= 1u << 30;
+                    if (q == std::max(1, n) - 1) word |= 1u << 31;
+                    blist[(size_t)k * trx::kBigLanes + l] = word;
+                    blink[(size_t)k * trx::kBigLanes + l] = (int16_t)(n ? in_eid[in_ptr[v] + q] : -1);
+                    ++k;
+                }
+            }
+        }
     }
 
     trx_graph* g = new trx_graph();
@@ -202,6 +299,7 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     d.E = E;
     d.Z = Z;
     d.NP = NP;
+    d.KMAX = KMAX;
     d.total_demand = total;
     float mt = 0.f, mc = 0.f;
     for (int e = 0; e < E; ++e) {
@@ -220,9 +318,17 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
         (rc = upload(g, origins, &d.origins)) || (rc = upload(g, nx_order, &d.nx_order)) ||
         (rc = upload(g, out_ptr, &d.out_ptr)) || (rc = upload(g, out_dst, &d.out_dst)) ||
         (rc = upload(g, out_eid, &d.out_eid)) || (rc = upload(g, in_ptr, &d.in_ptr)) ||
-        (rc = upload(g, in_src, &d.in_src)) || (rc = upload(g, in_eid, &d.in_eid))) {
+        (rc = upload(g, in_src, &d.in_src)) || (rc = upload(g, in_eid, &d.in_eid)) ||
+        (rc = upload(g, blist, &d.blist)) || (rc = upload(g, blink, &d.blink)) ||
+        (rc = upload(g, od_ptr, &d.od_ptr)) || (rc = upload(g, od_dst, &d.od_dst)) ||
+        (rc = upload(g, od_dem, &d.od_dem))) {
         trx_graph_destroy(g);
         return rc;
+    }
+    if (!small && trx::big_waves(d) <= 0) {
+        int rc2 = fail(TRX_EUNSUP, "graph (N=%d, E=%d) does not fit the large-graph kernel's LDS budget", N, E);
+        trx_graph_destroy(g);
+        return rc2;
     }
     *out = g;
     return TRX_OK;
@@ -247,7 +353,9 @@ int trx_graph_info(const trx_graph* g, int32_t* num_nodes, int32_t* num_edges, i
 
 int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs) {
     if (!g || num_envs < 0) return fail(TRX_EINVAL, "bad arguments");
-    return 256;  // all per-env work lives in LDS; kept in the ABI for larger-graph kernels
+    if (g->dg.N <= trx::kSmallMaxNodes) return 256;  // all per-env work lives in LDS
+    // large graphs: one exact-heap scratch slot per wave (rarely touched)
+    return (int64_t)std::max<size_t>(256, trx::big_workspace_bytes(g->dg, num_envs));
 }
 
 int trx_assign(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, const uint8_t* env_mask, void* ws,
@@ -270,12 +378,16 @@ int trx_observe(const trx_graph* g, int32_t B, const trx_state* s, float* node_x
                 void* ws, void* stream) {
     (void)ws;
     int rc;
-    if ((rc = check_small(g)) || (rc = check_state(s, false))) return rc;
+    if (!g) return fail(TRX_EINVAL, "graph is NULL");
+    if ((rc = check_state(s, false))) return rc;
     if (!node_x || !edge_x) return fail(TRX_EINVAL, "observation buffers are NULL");
     if (B <= 0) return B == 0 ? TRX_OK : fail(TRX_EINVAL, "num_envs < 0");
     hipError_t e = hipSetDevice(g->device);
     if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
-    e = trx::launch_observe_kernel(g->dg, B, *s, node_x, edge_x, mask, static_cast<hipStream_t>(stream));
+    if (g->dg.N <= trx::kSmallMaxNodes)
+        e = trx::launch_observe_kernel(g->dg, B, *s, node_x, edge_x, mask, static_cast<hipStream_t>(stream));
+    else
+        e = trx::launch_observe_big(g->dg, B, *s, node_x, edge_x, mask, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "observe launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }

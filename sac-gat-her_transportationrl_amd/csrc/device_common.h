@@ -72,53 +72,65 @@ __device__ __forceinline__ float pairwise_sum(const float* a, int n) { return pa
 
 // ------------------------------------------- exact scipy heap (rare path)
 // Restates scipy 1.15.3 _shortest_path.pyx FibonacciHeap on index links.
+// HT is a heap-storage type exposing val/parent/left/right/child/rank/state/
+// roots arrays (FibLane: per-lane LDS, int8 links, N <= 32; FibBig: per-wave
+// global scratch, int16 links, N <= 16383) and its link type idx_t.
+template <typename HT>
 struct Heap {
-    FibLane* h;
+    HT* h;
     int min;
 };
 
-__device__ void fh_add_sibling(FibLane* h, int node, int ns) {
+template <typename HT>
+__device__ void fh_add_sibling(HT* h, int node, int ns) {
+    using I = typename HT::idx_t;
     int r = h->right[node];
-    if (r >= 0) h->left[r] = (int8_t)ns;
-    h->right[ns] = (int8_t)r;
-    h->left[ns] = (int8_t)node;
-    h->right[node] = (int8_t)ns;
+    if (r >= 0) h->left[r] = (I)ns;
+    h->right[ns] = (I)r;
+    h->left[ns] = (I)node;
+    h->right[node] = (I)ns;
     int par = h->parent[node];
-    h->parent[ns] = (int8_t)par;
+    h->parent[ns] = (I)par;
     if (par >= 0) h->rank[par] += 1;
 }
-__device__ void fh_add_child(FibLane* h, int node, int c) {
-    h->parent[c] = (int8_t)node;
+template <typename HT>
+__device__ void fh_add_child(HT* h, int node, int c) {
+    using I = typename HT::idx_t;
+    h->parent[c] = (I)node;
     int ch = h->child[node];
     if (ch >= 0) {
         fh_add_sibling(h, ch, c);
     } else {
-        h->child[node] = (int8_t)c;
+        h->child[node] = (I)c;
         h->right[c] = -1;
         h->left[c] = -1;
         h->rank[node] = 1;
     }
 }
-__device__ void fh_remove(FibLane* h, int node) {
+template <typename HT>
+__device__ void fh_remove(HT* h, int node) {
+    using I = typename HT::idx_t;
     int par = h->parent[node];
     if (par >= 0) {
         h->rank[par] -= 1;
         if (h->child[par] == node) h->child[par] = h->right[node];
     }
     int l = h->left[node], r = h->right[node];
-    if (l >= 0) h->right[l] = (int8_t)r;
-    if (r >= 0) h->left[r] = (int8_t)l;
+    if (l >= 0) h->right[l] = (I)r;
+    if (r >= 0) h->left[r] = (I)l;
     h->left[node] = -1;
     h->right[node] = -1;
     h->parent[node] = -1;
 }
-__device__ void fh_insert(Heap& H, int node) {
-    FibLane* h = H.h;
+template <typename HT>
+__device__ void fh_insert(Heap<HT>& H, int node) {
+    using I = typename HT::idx_t;
+    HT* h = H.h;
     if (H.min >= 0) {
         if (h->val[node] < h->val[H.min]) {
             h->left[node] = -1;
-            h->right[node] = (int8_t)H.min;
-            h->left[H.min] = (int8_t)node;
+            h->right[node] = (I)H.min;
+            h->left[H.min] = (I)node;
             H.min = node;
         } else {
             fh_add_sibling(h, H.min, node);
@@ -127,8 +139,10 @@ __device__ void fh_insert(Heap& H, int node) {
         H.min = node;
     }
 }
-__device__ void fh_decrease(Heap& H, int node, double nv) {
-    FibLane* h = H.h;
+template <typename HT>
+__device__ void fh_decrease(Heap<HT>& H, int node, double nv) {
+    using I = typename HT::idx_t;
+    HT* h = H.h;
     h->val[node] = nv;
     int par = h->parent[node];
     if (par >= 0 && h->val[par] >= nv) {
@@ -136,18 +150,20 @@ __device__ void fh_decrease(Heap& H, int node, double nv) {
         fh_insert(H, node);
     } else if (h->val[H.min] > nv) {
         fh_remove(h, node);
-        h->right[node] = (int8_t)H.min;
-        h->left[H.min] = (int8_t)node;
+        h->right[node] = (I)H.min;
+        h->left[H.min] = (I)node;
         H.min = node;
     }
 }
-__device__ void fh_link(Heap& H, int node) {
-    FibLane* h = H.h;
+template <typename HT>
+__device__ void fh_link(Heap<HT>& H, int node) {
+    using I = typename HT::idx_t;
+    HT* h = H.h;
     for (;;) {
         int rk = h->rank[node];
         int ln = h->roots[rk];
         if (ln < 0) {
-            h->roots[rk] = (int8_t)node;
+            h->roots[rk] = (I)node;
             return;
         }
         h->roots[rk] = -1;
@@ -161,8 +177,10 @@ __device__ void fh_link(Heap& H, int node) {
         }
     }
 }
-__device__ int fh_remove_min(Heap& H) {
-    FibLane* h = H.h;
+template <typename HT>
+__device__ int fh_remove_min(Heap<HT>& H) {
+    using I = typename HT::idx_t;
+    HT* h = H.h;
     int temp = h->child[H.min];
     while (temp >= 0) {
         int tr = h->right[temp];
@@ -186,17 +204,17 @@ __device__ int fh_remove_min(Heap& H) {
     while (h->left[temp] >= 0) temp = h->left[temp];
     if (H.min != temp) {
         fh_remove(h, H.min);
-        h->right[H.min] = (int8_t)temp;
-        h->left[temp] = (int8_t)H.min;
+        h->right[H.min] = (I)temp;
+        h->left[temp] = (I)H.min;
     }
     return out;
 }
 
 // Exact scipy-order SSSP for one lane; writes scan order and predecessors
 // (node-major [v][L] LDS layout) and returns the number of scanned nodes.
-template <typename CostFn>
+template <typename HT, typename CostFn>
 __device__ int exact_sssp(const int N, const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-                          CostFn cost, int origin, FibLane* h, uint8_t* ord, uint8_t* pred, int L, int lane) {
+                          CostFn cost, int origin, HT* h, uint8_t* ord, uint8_t* pred, int L, int lane) {
     for (int k = 0; k < N; ++k) {
         h->val[k] = 0.0;
         h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
@@ -204,7 +222,7 @@ __device__ int exact_sssp(const int N, const int32_t* __restrict__ indptr, const
         h->state[k] = 0;
         pred[k * L + lane] = kNoPred;
     }
-    Heap H{h, -1};
+    Heap<HT> H{h, -1};
     fh_insert(H, origin);
     int k = 0;
     while (H.min >= 0) {
@@ -231,6 +249,46 @@ __device__ int exact_sssp(const int N, const int32_t* __restrict__ indptr, const
         }
     }
     return k;
+}
+
+// Same replay, recording each node's predecessor LINK id (csr_eid of the
+// relaxing CSR entry; -1 = unreached / origin) instead of the node: the
+// large-graph kernel walks paths by link.  cost(j) is the weight of CSR
+// entry j.
+template <typename HT, typename CostFn>
+__device__ void exact_sssp_links(const int N, const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                                 const int32_t* __restrict__ csr_eid, CostFn cost, int origin, HT* h,
+                                 int16_t* pred_link) {
+    for (int k = 0; k < N; ++k) {
+        h->val[k] = 0.0;
+        h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
+        h->rank[k] = 0;
+        h->state[k] = 0;
+        pred_link[k] = -1;
+    }
+    Heap<HT> H{h, -1};
+    fh_insert(H, origin);
+    while (H.min >= 0) {
+        int v = fh_remove_min(H);
+        h->state[v] = 2;
+        double vv = h->val[v];
+        for (int j = indptr[v]; j < indptr[v + 1]; ++j) {
+            int jc = indices[j];
+            int st = h->state[jc];
+            if (st != 2) {
+                double nv = vv + (double)cost(j);
+                if (st == 0) {
+                    h->state[jc] = 1;
+                    h->val[jc] = nv;
+                    fh_insert(H, jc);
+                    pred_link[jc] = (int16_t)csr_eid[j];
+                } else if (h->val[jc] > nv) {
+                    fh_decrease(H, jc, nv);
+                    pred_link[jc] = (int16_t)csr_eid[j];
+                }
+            }
+        }
+    }
 }
 
 // compute_reward_with_goal (repair_env.py:244-291)

@@ -10,6 +10,7 @@
 // per-lane BFS state lives node-major in LDS ([node][lane], conflict-free).
 #include <hip/hip_runtime.h>
 
+#include "obs_common.h"
 #include "trx_internal.h"
 
 namespace trx {
@@ -17,32 +18,6 @@ namespace trx {
 namespace {
 
 constexpr int kObsThreads = 64;
-
-__device__ float pairwise_small(const float* a, int n, int stride) {
-    // numpy pairwise_sum for n <= 128 (float32), strided reads
-    if (n < 8) {
-        float r = 0.0f;
-        for (int i = 0; i < n; ++i) r = __fadd_rn(r, a[i * stride]);
-        return r;
-    }
-    float r[8];
-    for (int j = 0; j < 8; ++j) r[j] = a[j * stride];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8)
-        for (int j = 0; j < 8; ++j) r[j] = __fadd_rn(r[j], a[(i + j) * stride]);
-    float res = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
-                          __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
-    for (; i < n; ++i) res = __fadd_rn(res, a[i * stride]);
-    return res;
-}
-
-__device__ float pairwise_any(const float* a, int n) {
-    if (n <= 128) return pairwise_small(a, n, 1);
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    // depth is tiny for small graphs; recursion depth <= log2(E/128)
-    return __fadd_rn(pairwise_any(a, n2), pairwise_any(a + n2, n - n2));
-}
 
 }  // namespace
 
@@ -163,60 +138,12 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     __syncthreads();
 
     if (tid < EPW && env0 + tid < B) {
-        const int el = tid, gb = env0 + tid;
-        const size_t eb = (size_t)gb * E;
-        float bmax = 0.0f;
-        for (int v = 0; v < N; ++v) bmax = fmaxf(bmax, bwv[el * N + v]);
-        // remaining goal ratio, avg undamaged flow (np.mean), log10 tstt
-        float* prod = reinterpret_cast<float*>(delta) + el * (E + 8);  // scratch
-        for (int e = 0; e < E; ++e) prod[e] = __fmul_rn(s.goal[eb + e], s.damaged[eb + e]);
-        float rem = pairwise_any(prod, E);
-        for (int e = 0; e < E; ++e) prod[e] = s.goal[eb + e];
-        float gtot = pairwise_any(prod, E);
-        double remaining_ratio = (double)rem / ((double)gtot > 1.0 ? (double)gtot : 1.0);
-        int nund = 0;
-        for (int e = 0; e < E; ++e)
-            if (s.damaged[eb + e] == 0.0f) prod[nund++] = s.flow[eb + e];
-        double avg_flow = 0.0;
-        if (nund > 0) {
-            float sm = pairwise_any(prod, nund);
-            avg_flow = (double)(float)((double)sm / (double)nund);
-        }
-        double denom = g.total_demand / (double)(E > 1 ? E : 1);
-        double avg_norm = avg_flow / (denom > 1.0 ? denom : 1.0);
-        double ts = s.tstt[gb];
-        double log_tstt = log10(ts > 1.0 ? ts : 1.0);
-        for (int v = 0; v < N; ++v) {
-            float b = bwv[el * N + v];
-            if (bmax > 0.0f) b = __fdiv_rn(b, bmax);
-            float* nx = node_x + ((size_t)gb * N + v) * 4;
-            nx[0] = b;
-            nx[1] = (float)remaining_ratio;
-            nx[2] = (float)avg_norm;
-            nx[3] = (float)log_tstt;
-        }
+        // feature scratch reuses delta (>= E + 8 floats per env, checked at launch)
+        obs_env_features(g, s, env0 + tid, bwv + tid * N, reinterpret_cast<float*>(delta) + tid * (E + 8), node_x);
     }
-    // ---------------- edge features
-    const double lt0 = log10((double)g.max_t0 + 1.0), lcap = log10((double)g.max_cap + 1.0);
-    const float idn = (float)(E - 1 > 1 ? E - 1 : 1);
     for (int i = tid; i < EPW * E; i += L) {
         int el = i / E, e = i - el * E, gb = env0 + el;
-        if (gb >= B) continue;
-        size_t gi = (size_t)gb * E + e;
-        float cap = s.capacity[gi], fl = s.flow[gi], dm = s.damaged[gi];
-        float c6 = cap > 1e-6f ? cap : 1e-6f;
-        float raw = __fdiv_rn(fl, c6);
-        float vc = dm > 0.0f ? 0.0f : raw;
-        vc = log1pf(vc);
-        vc = vc < 0.0f ? 0.0f : (vc > 10.0f ? 10.0f : vc);
-        float* ex = edge_x + gi * 6;
-        ex[0] = (float)((double)log10f(__fadd_rn(g.t0[e], 1.0f)) / lt0);
-        ex[1] = (float)((double)log10f(__fadd_rn(cap, 1.0f)) / lcap);
-        ex[2] = vc;
-        ex[3] = dm;
-        ex[4] = s.goal[gi];
-        ex[5] = __fdiv_rn((float)e, idn);
-        if (mask) mask[gi] = dm;
+        if (gb < B) obs_edge_features(g, s, gb, e, edge_x, mask);
     }
 }
 

@@ -11,6 +11,11 @@ namespace trx {
 // Largest node count handled by the register-resident small-graph kernel
 // (dist labels live in VGPRs, one lane per (env, origin) SSSP).
 constexpr int kSmallMaxNodes = 32;
+// Largest node count of the LDS-resident large-graph kernel (14-bit node ids
+// in the packed in-link entries; the LDS budget is checked per graph).
+constexpr int kBigMaxNodes = 16383;
+// Lanes that cooperate on one shortest-path tree in the large-graph kernel.
+constexpr int kBigLanes = 64;
 
 // Device-resident, immutable graph description (built by trx_graph_create).
 struct DevGraph {
@@ -32,16 +37,35 @@ struct DevGraph {
     const int32_t* in_ptr;      // [N+1]  predecessors (any order: distinct tails)
     const int32_t* in_src;      // [E]
     const int32_t* in_eid;      // [E]
+    // large-graph kernel (N > kSmallMaxNodes): in-links grouped per node, nodes
+    // dealt to lanes in contiguous chunks of a DFS order (see capi.hip)
+    int KMAX;                   // packed entries per lane
+    const uint32_t* blist;      // [KMAX][kBigLanes] u | v<<16 | first<<30 | last<<31
+    const int16_t* blink;       // [KMAX][kBigLanes] link id of the entry, -1 = padding / no in-link
+    const int32_t* od_ptr;      // [Z+1]  OD entries of origin zone zi (dict order)
+    const int32_t* od_dst;      // [P]
+    const float* od_dem;        // [P]
     double total_demand;        // float(np.sum(list(od_demand.values())))
     float max_t0, max_cap;      // RepairEnv.max_t0 / max_capacity
 };
 
 // Per-lane Fibonacci-heap state for the exact (scipy-order) SSSP fallback.
 struct FibLane {
+    using idx_t = int8_t;
     double val[kSmallMaxNodes];
     int8_t parent[kSmallMaxNodes], left[kSmallMaxNodes], right[kSmallMaxNodes], child[kSmallMaxNodes];
     uint8_t rank[kSmallMaxNodes], state[kSmallMaxNodes];
     int8_t roots[32];
+};
+
+// Per-wave Fibonacci-heap scratch of the large-graph kernel, carved from the
+// caller's workspace (global memory): int16 links, N <= kBigMaxNodes.
+struct FibBig {
+    using idx_t = int16_t;
+    double* val;
+    int16_t *parent, *left, *right, *child;
+    uint8_t *rank, *state;
+    int16_t* roots;  // [32]
 };
 
 enum RunMode { kModeAssign = 0, kModeReset = 1, kModeStep = 2 };
@@ -59,6 +83,15 @@ hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const 
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream);
 
+size_t big_smem_bytes(const DevGraph& g, int waves);
+int big_waves(const DevGraph& g);  // waves per workgroup that fit the LDS budget (0 = none)
+size_t big_workspace_bytes(const DevGraph& g, int num_envs);
+hipError_t launch_env_kernel_big(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
+                                 const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                                 const uint8_t* env_mask, void* workspace, hipStream_t stream);
+
+hipError_t launch_observe_big(const DevGraph& g, int num_envs, const trx_state& s, float* node_x, float* edge_x,
+                              float* mask, hipStream_t stream);
 hipError_t launch_observe_kernel(const DevGraph& g, int num_envs, const trx_state& s, float* node_x, float* edge_x,
                                  float* mask, hipStream_t stream);
 

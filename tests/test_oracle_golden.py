@@ -148,3 +148,51 @@ def test_summary_greedy_sequences_match_survey():
     assert s["crpow"]["greedy_msa30_actions"] == [55, 72, 68, 22, 45, 10, 36, 74, 18, 44, 12, 8, 43, 49, 53, 20, 69,
                                                   2, 71, 67, 32, 35]
     assert s["native"]["greedy_fw30_actions"] == s["crpow"]["greedy_fw30_actions"]
+
+
+# ---------------------------------------------------- large graph (config #5)
+def _ana_oracle():
+    return O.OracleGraph.from_npz(golden("ana_graph.npz"))
+
+
+@pytest.mark.parametrize("key,method", [("msa30", "msa"), ("fw30", "fw")])
+def test_oracle_anaheim_synth_reset_bitexact(key, method):
+    """Oracle == reference on the 416-node synthetic network (fixed damage 42)."""
+    og = _ana_oracle()
+    r = np.load(golden("ana_resets_crpow.npz"))
+    d = r[key + "_damaged"]
+    cap = np.where(d > 0, np.float32(1e-3), og.cap0).astype(np.float32)
+    f, t, ts, un = og.assign(cap, d, np.zeros(og.E, np.float32), method=method, iters=30)
+    np.testing.assert_array_equal(f, r[key + "_flow"])
+    np.testing.assert_array_equal(t, r[key + "_t"])
+    assert ts == float(r[key + "_tstt"]) and un == float(r[key + "_unassigned"])
+
+
+def test_oracle_anaheim_synth_steps_bitexact():
+    og = _ana_oracle()
+    z = np.load(golden("ana_steps_crpow.npz"))
+    for i in range(len(z["seeds"])):
+        d = z["damaged"][i].copy()
+        cap = np.where(d > 0, np.float32(1e-3), og.cap0).astype(np.float32)
+        f, _, ts, _ = og.assign(cap, d, np.zeros(og.E, np.float32), iters=30)
+        np.testing.assert_array_equal(f, z["flow"][i])
+        assert ts == z["tstt"][i]
+        for j in range(3):
+            a = int(z["actions"][i, j])
+            if d[a] == 0:  # already repaired: no assignment (repair_env.py:210-212)
+                assert z["step_reward"][i, j] == -1.0
+                continue
+            d[a] = 0.0
+            cap[a] = og.cap0[a]
+            f, _, ts, _ = og.assign(cap, d, f, iters=30)
+            np.testing.assert_array_equal(f, z["step_flow"][i, j])
+            assert ts == z["step_tstt"][i, j]
+
+
+def test_oracle_anaheim_synth_scipy_preds():
+    """Oracle's scipy-heap Dijkstra == scipy's predecessors (38 origins, 6 patterns)."""
+    og = _ana_oracle()
+    z = np.load(golden("ana_scipy_pred.npz"))
+    for k in range(len(z["seeds"])):
+        _, p = og.all_pairs(z["t"][k])
+        np.testing.assert_array_equal(p[z["origins"]], z["pred"][k])
