@@ -219,7 +219,9 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     // contiguous chunks balanced by entry count, so consecutive nodes of a
     // lane are mostly adjacent and one Gauss-Seidel sweep carries a label
     // along the whole chunk (assign_big.hip).
-    int KMAX = 0;
+    int KMAX = 0, big_g = 64;
+    std::vector<int32_t> b_origin(1, 0), b_od_dst(1, 0), b_indptr(1, 0), b_indices(1, 0), b_csr_eid(1, 0);
+    std::vector<int16_t> b_lsrc(1, 0);
     std::vector<uint32_t> blist(1, 0);
     std::vector<int16_t> blink(1, -1);
     if (!small) {
@@ -247,11 +249,40 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
                     if (!vis[*it]) stack.push_back(*it);
             }
         }
+        // the large-graph kernels number nodes by DFS position: a lane's chunk
+        // is then a run of consecutive label slots, so the 64 lanes' LDS label
+        // reads spread over the banks instead of colliding at random
+        std::vector<int32_t> inv(N);
+        for (int i = 0; i < N; ++i) inv[perm[i]] = i;
+        b_origin.resize(Z);
+        for (int z = 0; z < Z; ++z) b_origin[z] = inv[origins[z]];
+        b_od_dst.resize(P > 0 ? P : 1);
+        for (int q = 0; q < P; ++q) b_od_dst[q] = inv[od_dst[q]];
+        b_lsrc.resize(E > 0 ? E : 1);
+        for (int e = 0; e < E; ++e) b_lsrc[e] = (int16_t)inv[src[e]];
+        b_indptr.assign(N + 1, 0);
+        b_indices.clear();
+        b_csr_eid.clear();
+        for (int r = 0; r < N; ++r) {  // rows by DFS position, entries in scipy order
+            const int o = perm[r];
+            for (int j = indptr[o]; j < indptr[o + 1]; ++j) {
+                b_indices.push_back(inv[indices[j]]);
+                b_csr_eid.push_back(csr_eid[j]);
+            }
+            b_indptr[r + 1] = (int32_t)b_indices.size();
+        }
+        // chunk the DFS order over the G lanes of a tree, balanced by entry
+        // count (every node owns >= 1 entry: a dummy if it has no in-link)
+        static const int lanes_env = [] {
+            const char* e = getenv("TRX_BIG_LANES");  // tuning knob (A/B runs): 32 or 64
+            return e ? atoi(e) : 0;
+        }();
+        big_g = lanes_env == 64 ? 64 : lanes_env == 16 ? 16 : 32;
         auto cost = [&](int v) { return std::max(1, in_ptr[v + 1] - in_ptr[v]); };
         int tot = 0;
         for (int v = 0; v < N; ++v) tot += cost(v);
         std::vector<int> lane_start;
-        for (int T = (tot + trx::kBigLanes - 1) / trx::kBigLanes;; ++T) {
+        for (int T = (tot + big_g - 1) / big_g;; ++T) {
             lane_start.assign(1, 0);
             int acc = 0;
             for (int i = 0; i < N; ++i) {
@@ -261,30 +292,32 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
                 }
                 acc += cost(perm[i]);
             }
-            if ((int)lane_start.size() <= trx::kBigLanes) {
+            if ((int)lane_start.size() <= big_g) {
                 KMAX = T;
                 break;
             }
         }
-        while ((int)lane_start.size() < trx::kBigLanes) lane_start.push_back(N);
+        while ((int)lane_start.size() < big_g) lane_start.push_back(N);
         lane_start.push_back(N);
-        blist.assign((size_t)KMAX * trx::kBigLanes, 0u);
-        blink.assign((size_t)KMAX * trx::kBigLanes, -1);
-        for (int l = 0; l < trx::kBigLanes; ++l) {
+        blist.assign((size_t)KMAX * big_g, 0u);
+        blink.assign((size_t)KMAX * big_g, -1);
+        for (int l = 0; l < big_g; ++l) {
             int k = 0;
             for (int i = lane_start[l]; i < lane_start[l + 1]; ++i) {
                 const int v = perm[i];
                 const int n = in_ptr[v + 1] - in_ptr[v];
                 for (int q = 0; q < std::max(1, n); ++q) {
                     const int u = n ? in_src[in_ptr[v] + q] : v;
-                    uint32_t word = (uint32_t)u | ((uint32_t)v << 16);
+                    uint32_t word = (uint32_t)inv[u] | ((uint32_t)inv[v] << 16);
                     if (q == 0) word |= 1u << 30;
                     if (q == std::max(1, n) - 1) word |= 1u << 31;
-                    blist[(size_t)k * trx::kBigLanes + l] = word;
-                    blink[(size_t)k * trx::kBigLanes + l] = (int16_t)(n ? in_eid[in_ptr[v] + q] : -1);
+                    blist[(size_t)k * big_g + l] = word;
+                    blink[(size_t)k * big_g + l] = (int16_t)(n ? in_eid[in_ptr[v] + q] : -1);
                     ++k;
                 }
             }
+            // padding entries: node N (the dummy label slot, always +inf)
+            for (; k < KMAX; ++k) blist[(size_t)k * big_g + l] = (uint32_t)N | ((uint32_t)N << 16) | (3u << 30);
         }
     }
 
@@ -300,6 +333,7 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     d.Z = Z;
     d.NP = NP;
     d.KMAX = KMAX;
+    d.big_g = big_g;
     d.total_demand = total;
     float mt = 0.f, mc = 0.f;
     for (int e = 0; e < E; ++e) {
@@ -321,7 +355,10 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
         (rc = upload(g, in_src, &d.in_src)) || (rc = upload(g, in_eid, &d.in_eid)) ||
         (rc = upload(g, blist, &d.blist)) || (rc = upload(g, blink, &d.blink)) ||
         (rc = upload(g, od_ptr, &d.od_ptr)) || (rc = upload(g, od_dst, &d.od_dst)) ||
-        (rc = upload(g, od_dem, &d.od_dem))) {
+        (rc = upload(g, od_dem, &d.od_dem)) || (rc = upload(g, b_origin, &d.b_origin)) ||
+        (rc = upload(g, b_od_dst, &d.b_od_dst)) || (rc = upload(g, b_lsrc, &d.b_lsrc)) ||
+        (rc = upload(g, b_indptr, &d.b_indptr)) || (rc = upload(g, b_indices, &d.b_indices)) ||
+        (rc = upload(g, b_csr_eid, &d.b_csr_eid))) {
         trx_graph_destroy(g);
         return rc;
     }

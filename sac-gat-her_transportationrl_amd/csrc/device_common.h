@@ -70,6 +70,56 @@ __device__ __forceinline__ float pairwise_rec(const float* a, int n) {
 }
 __device__ __forceinline__ float pairwise_sum(const float* a, int n) { return pairwise_rec<4>(a, n); }
 
+// Same recursion for any n, evaluated iteratively (explicit post-order stack)
+// so that large-graph kernels do not inline 2^depth copies of the block sum.
+__device__ __noinline__ float pairwise_sum_any(const float* a, int n) {
+    if (n <= 128) return pairwise_block(a, n);
+    int off[32], cnt[32];
+    float lft[32];
+    uint8_t st[32];
+    int sp = 0;
+    off[0] = 0;
+    cnt[0] = n;
+    st[0] = 0;
+    float ret = 0.0f;
+    bool have = false;
+    for (;;) {
+        if (!have) {
+            const int c = cnt[sp];
+            if (c <= 128) {
+                ret = pairwise_block(a + off[sp], c);
+                have = true;
+                --sp;
+            } else {  // descend into the left half
+                int n2 = c / 2;
+                n2 -= n2 % 8;
+                st[sp] = 1;
+                off[sp + 1] = off[sp];
+                cnt[sp + 1] = n2;
+                st[sp + 1] = 0;
+                ++sp;
+            }
+        } else {
+            if (sp < 0) return ret;
+            if (st[sp] == 1) {  // left done: keep it, descend into the right half
+                const int c = cnt[sp];
+                int n2 = c / 2;
+                n2 -= n2 % 8;
+                lft[sp] = ret;
+                st[sp] = 2;
+                off[sp + 1] = off[sp] + n2;
+                cnt[sp + 1] = c - n2;
+                st[sp + 1] = 0;
+                ++sp;
+                have = false;
+            } else {  // both halves done
+                ret = __fadd_rn(lft[sp], ret);
+                --sp;
+            }
+        }
+    }
+}
+
 // ------------------------------------------- exact scipy heap (rare path)
 // Restates scipy 1.15.3 _shortest_path.pyx FibonacciHeap on index links.
 // HT is a heap-storage type exposing val/parent/left/right/child/rank/state/
@@ -251,20 +301,20 @@ __device__ int exact_sssp(const int N, const int32_t* __restrict__ indptr, const
     return k;
 }
 
-// Same replay, recording each node's predecessor LINK id (csr_eid of the
-// relaxing CSR entry; -1 = unreached / origin) instead of the node: the
-// large-graph kernel walks paths by link.  cost(j) is the weight of CSR
-// entry j.
+// Same replay, recording each node's predecessor as a packed
+// (link id | tail node << 16) word (-1 = unreached / origin) instead of the
+// node: the large-graph kernel walks paths by link.  cost(j) is the weight of
+// CSR entry j.
 template <typename HT, typename CostFn>
 __device__ void exact_sssp_links(const int N, const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
                                  const int32_t* __restrict__ csr_eid, CostFn cost, int origin, HT* h,
-                                 int16_t* pred_link) {
+                                 int32_t* pred_packed) {
     for (int k = 0; k < N; ++k) {
         h->val[k] = 0.0;
         h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
         h->rank[k] = 0;
         h->state[k] = 0;
-        pred_link[k] = -1;
+        pred_packed[k] = -1;
     }
     Heap<HT> H{h, -1};
     fh_insert(H, origin);
@@ -281,10 +331,10 @@ __device__ void exact_sssp_links(const int N, const int32_t* __restrict__ indptr
                     h->state[jc] = 1;
                     h->val[jc] = nv;
                     fh_insert(H, jc);
-                    pred_link[jc] = (int16_t)csr_eid[j];
+                    pred_packed[jc] = csr_eid[j] | (v << 16);
                 } else if (h->val[jc] > nv) {
                     fh_decrease(H, jc, nv);
-                    pred_link[jc] = (int16_t)csr_eid[j];
+                    pred_packed[jc] = csr_eid[j] | (v << 16);
                 }
             }
         }

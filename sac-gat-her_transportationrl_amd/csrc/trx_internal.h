@@ -13,9 +13,7 @@ namespace trx {
 constexpr int kSmallMaxNodes = 32;
 // Largest node count of the LDS-resident large-graph kernel (14-bit node ids
 // in the packed in-link entries; the LDS budget is checked per graph).
-constexpr int kBigMaxNodes = 16383;
-// Lanes that cooperate on one shortest-path tree in the large-graph kernel.
-constexpr int kBigLanes = 64;
+constexpr int kBigMaxNodes = 16382;  // node id 16382 < 2^14 - 1; N itself is the dummy node
 
 // Device-resident, immutable graph description (built by trx_graph_create).
 struct DevGraph {
@@ -40,8 +38,16 @@ struct DevGraph {
     // large-graph kernel (N > kSmallMaxNodes): in-links grouped per node, nodes
     // dealt to lanes in contiguous chunks of a DFS order (see capi.hip)
     int KMAX;                   // packed entries per lane
-    const uint32_t* blist;      // [KMAX][kBigLanes] u | v<<16 | first<<30 | last<<31
-    const int16_t* blink;       // [KMAX][kBigLanes] link id of the entry, -1 = padding / no in-link
+    int big_g;                  // lanes per shortest-path tree (32 or 64)
+    const uint32_t* blist;      // [KMAX][big_g] u | v<<16 | first<<30 | last<<31 (DFS positions)
+    const int16_t* blink;       // [KMAX][big_g] link id of the entry, -1 = padding / no in-link
+    // node ids of the large-graph kernels are DFS positions (capi.hip):
+    const int32_t* b_origin;    // [Z]    origin of zone zi
+    const int32_t* b_od_dst;    // [P]    OD destination
+    const int16_t* b_lsrc;      // [E]    tail of each link
+    const int32_t* b_indptr;    // [N+1]  scipy CSR, rows by DFS position, entries in scipy order
+    const int32_t* b_indices;   // [E]
+    const int32_t* b_csr_eid;   // [E]
     const int32_t* od_ptr;      // [Z+1]  OD entries of origin zone zi (dict order)
     const int32_t* od_dst;      // [P]
     const float* od_dem;        // [P]
