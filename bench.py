@@ -108,17 +108,16 @@ def cpu_baseline(network, method, iters, seconds=12.0):
                       f"link each) in {dt:.1f}s on {threads} host threads; oracle/trx_oracle.c"}
 
 
-def measured_traffic():
-    """HBM bytes per env_kernel launch from the latest committed rocprofv3 PMC
-    summary (profiles/*_pmc.json, written by tools/pmc_summary.py from
-    separate FETCH_SIZE / WRITE_SIZE passes of this bench's workload)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-    if not files:
-        return None, None
+def measured_traffic(network):
+    """HBM bytes per env-kernel launch from the committed rocprofv3 PMC summary
+    of this workload (profiles/r01_v3_pmc.json for Sioux Falls,
+    profiles/r01_ana_pmc.json for the Anaheim-size network; separate
+    FETCH_SIZE / WRITE_SIZE passes, see tools/pmc_summary.py)."""
+    name = {"sf": "r01_v3_pmc.json", "anaheim": "r01_ana_pmc.json"}[network]
+    path = os.path.join(ROOT, "profiles", name)
     try:
-        d = json.load(open(files[-1]))
-        return d.get("hbm_bytes_per_launch_raw"), os.path.relpath(files[-1], ROOT)
+        d = json.load(open(path))
+        return d.get("hbm_bytes_per_launch_raw"), os.path.relpath(path, ROOT)
     except (OSError, ValueError):
         return None, None
 
@@ -275,9 +274,9 @@ def main():
     P = len(env.graph.od_o)
     bpa = bytes_per_assign(N, E, Z, P, args.iters)
     achieved = bpa * B / mean_kernel_s
-    traffic, traffic_src = measured_traffic()
-    if (args.network, args.envs, args.iters, args.method, args.workload) != ("sf", 4096, 30, "msa", "train"):
-        traffic, traffic_src = None, None  # the committed PMC pass is for the default workload
+    traffic, traffic_src = measured_traffic(args.network)
+    if (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")):
+        traffic, traffic_src = None, None  # the committed PMC passes are for the default workloads
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
