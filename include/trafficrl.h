@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 1
+#define TRX_ABI_VERSION 2
 
 /* error codes */
 #define TRX_OK 0
@@ -42,6 +42,7 @@ extern "C" {
 #define TRX_METHOD_MSA 0
 #define TRX_METHOD_FW 1
 #define TRX_METHOD_CFW 2
+#define TRX_METHOD_GP 3   /* path-based: _compute_flow_assignment_gp, repair_env.py:351-419 */
 
 /* reward modes: RepairEnv.compute_reward_with_goal repair_env.py:244-291 */
 #define TRX_REWARD_DELTA 0
@@ -64,6 +65,9 @@ typedef struct trx_params {
     int32_t reward_mode;        /* TRX_REWARD_*                      reward_mode         */
     int32_t _pad1;
     double reward_alpha, reward_beta, reward_gamma, reward_clip;
+    double gp_step;             /* 1.0; <= 0 means 1/(it+1)          gp_step (GP only)   */
+    int32_t gp_keep_paths;      /* 3 (yaml: 2); 1..3 supported       gp_keep_paths       */
+    int32_t _pad2;
 } trx_params;
 
 /* Per-env state of B vectorised envs: device pointers, caller-owned.
@@ -85,6 +89,9 @@ typedef struct trx_state {
     double* tstt;
     double* initial_tstt;
     double* unassigned;
+    void* gp;       /* TRX_METHOD_GP only: per-env path sets, i.e. RepairEnv.od_paths /
+                     * od_path_flows (repair_env.py:199-200, 351-404), trx_gp_state_bytes()
+                     * per env, caller-owned, kept between calls (cleared by trx_reset) */
 } trx_state;
 
 /* ---------------------------------------------------------------- misc */
@@ -108,6 +115,10 @@ int trx_graph_info(const trx_graph* g, int32_t* num_nodes, int32_t* num_edges, i
                    double* total_demand);
 /* Device scratch bytes needed by trx_reset/step/assign for B envs. */
 int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs);
+/* Bytes of trx_state.gp for num_envs envs with gp_keep_paths = keep_paths
+ * (envs are contiguous rows of equal size: row b starts at b * bytes(1)).
+ * GP needs N <= 32, E <= 128 and 1 <= keep_paths <= 3 (else TRX_EUNSUP). */
+int64_t trx_gp_state_bytes(const trx_graph* g, int32_t num_envs, int32_t keep_paths);
 
 /* ----------------------------------------------------------- hot path
  * trx_assign: RepairEnv.compute_flow_assignment (repair_env.py:299-345) for

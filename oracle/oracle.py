@@ -259,3 +259,104 @@ def observation(src, dst, N, t0, cap0, capacities, damaged, goal, flow, tstt, to
     eid = np.arange(E, dtype=np.float32) / max(E - 1, 1)
     edge = np.stack([t0_norm.astype(np.float32), cap_norm.astype(np.float32), vc, damaged, goal, eid], axis=1)
     return node.astype(np.float32), edge.astype(np.float32), damaged.astype(np.float32)
+
+
+# ------------------------------------------- path-based (GP) assignment oracle
+class GPPaths:
+    """Per-env path sets of the GP assignment: RepairEnv.od_paths /
+    od_path_flows (repair_env.py:351-419).  Keys (0-based (o, d)) keep their
+    insertion order; each key holds [edge-id tuple] paths and float64 flows."""
+
+    def __init__(self):
+        self.paths = {}
+        self.flows = {}
+
+    def copy(self):
+        c = GPPaths()
+        c.paths = {k: list(v) for k, v in self.paths.items()}
+        c.flows = {k: list(v) for k, v in self.flows.items()}
+        return c
+
+
+def _f32_path_cost(t, path):
+    """_path_cost (repair_env.py:346-349): float(np.sum(t[path])) -- numpy's
+    float32 pairwise sum over the path's links in path order."""
+    if not path:
+        return float("inf")
+    return float(np.sum(t[list(path)]))
+
+
+def gp_assign(og: OracleGraph, cap, damaged, flow, state: GPPaths, iters, gp_step=1.0, keep=3, reset=False,
+              alpha=0.15, beta=4.0, penalty=1e4):
+    """One env's _compute_flow_assignment_gp (repair_env.py:351-419) followed by
+    compute_tstt, restated over the oracle's scipy-order shortest paths.
+    Mutates `state`; returns (flow, t, tstt, unassigned)."""
+    cap = np.ascontiguousarray(cap, np.float32)
+    damaged = np.ascontiguousarray(damaged, np.float32)
+    t = og.bpr(flow, cap, damaged, alpha, beta)
+    if reset or not state.paths:
+        state.paths.clear()
+        state.flows.clear()
+    # OD entries grouped by origin, dict order inside an origin (the reference
+    # scans origins ascending and filters the dict for each)
+    by_origin = {}
+    for o, d, v in zip(og.od_o.tolist(), og.od_d.tolist(), og.od_v.tolist()):
+        by_origin.setdefault(o, []).append((d, v))
+    eid = {(int(u), int(v)): e for e, (u, v) in enumerate(zip(og.src, og.dst))}
+    unassigned = 0.0
+    for it in range(iters):
+        unassigned = 0.0
+        step = gp_step if gp_step > 0 else 1.0 / (it + 1.0)
+        _, pred = og.all_pairs(t)
+        for origin in sorted(by_origin):
+            for dest, demand in by_origin[origin]:
+                if dest == origin or pred[origin, dest] < 0:
+                    unassigned += demand
+                    continue
+                nodes = [dest]
+                while nodes[-1] != origin:
+                    nodes.append(int(pred[origin, nodes[-1]]))
+                nodes.reverse()
+                sp = tuple(eid[(nodes[i], nodes[i + 1])] for i in range(len(nodes) - 1))
+                key = (origin, dest)
+                if key not in state.paths:
+                    state.paths[key] = [sp]
+                    state.flows[key] = [float(demand)]
+                    continue
+                paths, flows = state.paths[key], state.flows[key]
+                if sp not in paths:
+                    paths.append(sp)
+                    flows.append(0.0)
+                costs = [_f32_path_cost(t, p) for p in paths]
+                best = int(np.argmin(costs))
+                if len(flows) > 1:
+                    moved = 0.0
+                    for i in range(len(flows)):
+                        if i != best:
+                            tr = step * flows[i]
+                            flows[i] -= tr
+                            moved += tr
+                    flows[best] += moved
+                if keep > 0 and len(paths) > keep:
+                    order = np.argsort(costs)[:keep]
+                    new_p = [paths[i] for i in order]
+                    new_f = [flows[i] for i in order]
+                    tot = float(np.sum(new_f))
+                    if tot > 0:
+                        new_f = [f * demand / tot for f in new_f]
+                    else:
+                        new_f = [0.0] * len(new_f)
+                        new_f[0] = float(demand)
+                    state.paths[key], state.flows[key] = new_p, new_f
+        new_flow = np.zeros(og.E, np.float32)
+        for key, paths in state.paths.items():
+            for p, f in zip(paths, state.flows[key]):
+                if f <= 0:
+                    continue
+                for e in p:
+                    new_flow[e] += f
+        flow = new_flow
+        t = og.bpr(flow, cap, damaged, alpha, beta)
+    td = max(og.total_demand, 1.0)
+    tstt = pairwise_sum_f32(flow * t) / td + (penalty * (unassigned / td) if unassigned > 0 else 0.0)
+    return flow, t, tstt, unassigned

@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
             const bool on = zi < Z;  // a half without a tree keeps every label at +inf
             const int origin = on ? g.b_origin[zi] : -1;
             TRX_BIG_COUNT(0, (Z - z0) < TPW ? (Z - z0) : TPW);
-            unsigned long long clk0 = TRX_BIG_CLOCK();
+            [[maybe_unused]] unsigned long long clk0 = TRX_BIG_CLOCK();
             for (int v = lt; v <= N; v += G) dist[v] = v == origin ? 0.0 : kInfD;
             for (int v = lt; v < N; v += G) pe[v] = -1;
             wave_sync();
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
                 }
                 dir ^= 1;
             }
-            unsigned long long clk1 = TRX_BIG_CLOCK();
+            [[maybe_unused]] unsigned long long clk1 = TRX_BIG_CLOCK();
             TRX_BIG_COUNT(3, clk1 - clk0);
             // ---------------- predecessors: smallest-label achieving tail
             bool amb = false;
@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
             }
             wave_sync();
             const uint64_t ambm = __ballot(amb);
-            unsigned long long clk2 = TRX_BIG_CLOCK();
+            [[maybe_unused]] unsigned long long clk2 = TRX_BIG_CLOCK();
             TRX_BIG_COUNT(4, clk2 - clk1);
             if (ambm != 0) {  // equal-label tie: scipy's heap order decides
                 const uint64_t mine = G == 64 ? ambm : (ambm >> (half * G)) & ((1ull << G) - 1);

@@ -55,8 +55,11 @@ int upload(trx_graph* g, const std::vector<T>& host, const T** out) {
 int check_params(const trx_params* p) {
     if (!p) return fail(TRX_EINVAL, "params is NULL");
     if (p->iters <= 0) return fail(TRX_EINVAL, "assignment_iters must be > 0 to update TSTT.");  // repair_env.py:300-301
-    if (p->method < TRX_METHOD_MSA || p->method > TRX_METHOD_CFW)
+    if (p->method < TRX_METHOD_MSA || p->method > TRX_METHOD_GP)
         return fail(TRX_EINVAL, "unsupported assignment_method %d", p->method);
+    if (p->method == TRX_METHOD_GP && (p->gp_keep_paths < 1 || p->gp_keep_paths > trx::kGpMaxPaths - 1))
+        return fail(TRX_EUNSUP, "gp_keep_paths %d: this build supports 1..%d", p->gp_keep_paths,
+                    trx::kGpMaxPaths - 1);
     if (!(p->bpr_beta >= 0.0f && p->bpr_beta <= 16.0f) || p->bpr_beta != std::floor(p->bpr_beta))
         return fail(TRX_EUNSUP, "bpr_beta %g: only integer BPR powers 0..16 are supported (the reference uses 4)",
                     (double)p->bpr_beta);
@@ -83,7 +86,14 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
     if (!ws) return fail(TRX_EINVAL, "workspace is NULL (size it with trx_workspace_bytes)");
     hipError_t e = hipSetDevice(g->device);
     if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
-    if (g->dg.N <= trx::kSmallMaxNodes)
+    if (p->method == TRX_METHOD_GP) {
+        if (g->dg.N > trx::kSmallMaxNodes || g->dg.E > 128 || g->dg.Z > 256)
+            return fail(TRX_EUNSUP, "GP assignment supports N <= %d, E <= 128 (got N=%d E=%d)",
+                        trx::kSmallMaxNodes, g->dg.N, g->dg.E);
+        if (!s->gp) return fail(TRX_EINVAL, "state.gp is NULL (size it with trx_gp_state_bytes)");
+        e = trx::launch_gp_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
+                                  static_cast<hipStream_t>(stream));
+    } else if (g->dg.N <= trx::kSmallMaxNodes)
         e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
                                         static_cast<hipStream_t>(stream));
     else
@@ -332,6 +342,7 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     d.E = E;
     d.Z = Z;
     d.NP = NP;
+    d.P = P;
     d.KMAX = KMAX;
     d.big_g = big_g;
     d.total_demand = total;
@@ -393,6 +404,15 @@ int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs) {
     if (g->dg.N <= trx::kSmallMaxNodes) return 256;  // all per-env work lives in LDS
     // large graphs: one exact-heap scratch slot per wave (rarely touched)
     return (int64_t)std::max<size_t>(256, trx::big_workspace_bytes(g->dg, num_envs));
+}
+
+int64_t trx_gp_state_bytes(const trx_graph* g, int32_t num_envs, int32_t keep_paths) {
+    if (!g || num_envs < 0) return fail(TRX_EINVAL, "bad arguments");
+    if (keep_paths < 1 || keep_paths > trx::kGpMaxPaths - 1)
+        return fail(TRX_EUNSUP, "gp_keep_paths %d: this build supports 1..%d", keep_paths, trx::kGpMaxPaths - 1);
+    if (g->dg.N > trx::kSmallMaxNodes || g->dg.E > 128)
+        return fail(TRX_EUNSUP, "GP assignment supports N <= %d, E <= 128", trx::kSmallMaxNodes);
+    return (int64_t)num_envs * (int64_t)trx::gp_layout(g->dg.P, keep_paths).total;
 }
 
 int trx_assign(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, const uint8_t* env_mask, void* ws,

@@ -72,7 +72,7 @@ __device__ __forceinline__ float pairwise_sum(const float* a, int n) { return pa
 
 // Same recursion for any n, evaluated iteratively (explicit post-order stack)
 // so that large-graph kernels do not inline 2^depth copies of the block sum.
-__device__ __noinline__ float pairwise_sum_any(const float* a, int n) {
+[[maybe_unused]] __device__ __noinline__ float pairwise_sum_any(const float* a, int n) {
     if (n <= 128) return pairwise_block(a, n);
     int off[32], cnt[32];
     float lft[32];

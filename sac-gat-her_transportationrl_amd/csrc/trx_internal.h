@@ -18,6 +18,7 @@ constexpr int kBigMaxNodes = 16382;  // node id 16382 < 2^14 - 1; N itself is th
 // Device-resident, immutable graph description (built by trx_graph_create).
 struct DevGraph {
     int N, E, Z, NP;            // nodes, edges, origins (zones with demand), padded nodes
+    int P;                      // OD entries
     const int32_t* src;         // [E]
     const int32_t* dst;         // [E]
     const float* t0;            // [E]
@@ -74,6 +75,32 @@ struct FibBig {
     int16_t* roots;  // [32]
 };
 
+// Path-based (GP) assignment state: one row per env (trx_state.gp).
+constexpr int kGpMaxHops = 32;   // links per path (N <= 32)
+constexpr int kGpMaxPaths = 4;   // gp_keep_paths + 1 while a new path is priced
+struct GpLayout {
+    size_t nkeys, ord, np, flow, mask, len, edges, total;
+};
+__host__ __device__ inline GpLayout gp_layout(int P, int keep) {
+    const size_t KP = (size_t)keep + 1;
+    GpLayout o{};
+    size_t off = 0;
+    auto take = [&off](size_t b) {
+        size_t r = off;
+        off = (off + b + 15) & ~(size_t)15;
+        return r;
+    };
+    o.nkeys = take(16);                      // i32 keys inserted so far
+    o.ord = take((size_t)P * 2);             // i16 key ids in insertion (dict) order
+    o.np = take((size_t)P);                  // u8 paths per key
+    o.flow = take((size_t)P * KP * 8);       // f64 path flows
+    o.mask = take((size_t)P * KP * 16);      // uint4 link bitmask per path (E <= 128)
+    o.len = take((size_t)P * KP);            // u8 links per path
+    o.edges = take((size_t)P * KP * kGpMaxHops);  // u8 link ids in path order
+    o.total = (off + 255) & ~(size_t)255;
+    return o;
+}
+
 enum RunMode { kModeAssign = 0, kModeReset = 1, kModeStep = 2 };
 
 struct LaunchCfg {
@@ -96,6 +123,9 @@ hipError_t launch_env_kernel_big(const DevGraph& g, const trx_params& p, const t
                                  const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                  const uint8_t* env_mask, void* workspace, hipStream_t stream);
 
+hipError_t launch_gp_kernel(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
+                            const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                            const uint8_t* env_mask, hipStream_t stream);
 hipError_t launch_observe_big(const DevGraph& g, int num_envs, const trx_state& s, float* node_x, float* edge_x,
                               float* mask, hipStream_t stream);
 hipError_t launch_observe_kernel(const DevGraph& g, int num_envs, const trx_state& s, float* node_x, float* edge_x,

@@ -14,13 +14,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
-METHODS = {"msa": 0, "fw": 1, "cfw": 2}
+METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
+ABI_VERSION = 2
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
 # Every symbol include/trafficrl.h declares (tests check the export table).
 EXPORTS = (
     "trx_abi_version", "trx_last_error", "trx_graph_create", "trx_graph_destroy", "trx_graph_info",
-    "trx_workspace_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe", "trx_gat_forward",
+    "trx_workspace_bytes", "trx_gp_state_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe", "trx_gat_forward",
     "trx_gat_backward", "trx_per_update", "trx_per_sample", "trx_graph_patch_memsets", "trx_gat_layer_infer",
     "trx_edge_head_infer",
 )
@@ -35,12 +36,29 @@ class TrxParams(ctypes.Structure):
         ("reward_mode", ctypes.c_int32), ("_pad1", ctypes.c_int32),
         ("reward_alpha", ctypes.c_double), ("reward_beta", ctypes.c_double),
         ("reward_gamma", ctypes.c_double), ("reward_clip", ctypes.c_double),
+        ("gp_step", ctypes.c_double), ("gp_keep_paths", ctypes.c_int32), ("_pad2", ctypes.c_int32),
     ]
 
 
 class TrxState(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in
-                ("flow", "capacity", "damaged", "goal", "t", "tstt", "initial_tstt", "unassigned")]
+                ("flow", "capacity", "damaged", "goal", "t", "tstt", "initial_tstt", "unassigned", "gp")]
+
+
+GP_MAX_HOPS = 32  # kGpMaxHops (csrc/trx_internal.h)
+
+
+def gp_layout(P: int, keep: int) -> dict:
+    """Byte offsets of one env's GP path-set row (gp_layout, csrc/trx_internal.h)."""
+    KP = keep + 1
+    off = 0
+    out = {}
+    for name, nbytes in (("nkeys", 16), ("ord", P * 2), ("np", P), ("flow", P * KP * 8), ("mask", P * KP * 16),
+                         ("len", P * KP), ("edges", P * KP * GP_MAX_HOPS)):
+        out[name] = off
+        off = (off + nbytes + 15) & ~15
+    out["total"] = (off + 255) & ~255
+    return out
 
 
 _vp = ctypes.c_void_p
@@ -97,6 +115,8 @@ def load():
                                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]
     L.trx_workspace_bytes.argtypes = [_vp, ctypes.c_int32]
     L.trx_workspace_bytes.restype = ctypes.c_int64
+    L.trx_gp_state_bytes.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32]
+    L.trx_gp_state_bytes.restype = ctypes.c_int64
     L.trx_assign.argtypes = [_vp, ctypes.POINTER(TrxParams), ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp]
     L.trx_reset.argtypes = [_vp, ctypes.POINTER(TrxParams), ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp]
     L.trx_step.argtypes = [_vp, ctypes.POINTER(TrxParams), ctypes.c_int32, ctypes.POINTER(TrxState), _vp, _vp, _vp,
@@ -115,8 +135,8 @@ def load():
                  "trx_observe", "trx_gat_forward", "trx_gat_backward", "trx_per_update", "trx_per_sample",
                  "trx_graph_patch_memsets", "trx_gat_layer_infer", "trx_edge_head_infer"):
         getattr(L, name).restype = ctypes.c_int
-    if L.trx_abi_version() != 1:
-        raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != 1")
+    if L.trx_abi_version() != ABI_VERSION:
+        raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")
     _lib = L
     return L
 

@@ -52,15 +52,20 @@ class WhatIfBatch:
         # shares the graph handle and params; only state tensors are allocated
         v = VecRepairEnv(self.graph.graph_data, self.rows, device=self.device, graph=self.graph, reset=False,
                          assignment_iters=self.params.iters,
-                         assignment_method={0: "msa", 1: "fw", 2: "cfw"}[self.params.method])
+                         assignment_method={0: "msa", 1: "fw", 2: "cfw", 3: "gp"}[self.params.method],
+                         gp_step=self.params.gp_step, gp_keep_paths=max(1, self.params.gp_keep_paths))
         v.params = self.params
         self._vec = v
 
-    def tstt(self, cap: torch.Tensor, dmg: torch.Tensor, flow: torch.Tensor) -> torch.Tensor:
-        """Run warm-started assignments for rows [R,E]; return tstt[R] (f64)."""
+    def tstt(self, cap: torch.Tensor, dmg: torch.Tensor, flow: torch.Tensor, gp_row=None) -> torch.Tensor:
+        """Run warm-started assignments for rows [R,E]; return tstt[R] (f64).
+        GP: every row starts from the path sets `gp_row` (one env's state row),
+        like the reference's deepcopy/restore of od_paths (baselines 46-65)."""
         R = cap.shape[0]
         self.ensure(R)
         v = self._vec
+        if v.gp_state is not None:
+            v.gp_state.view(v.num_envs, -1)[:R].copy_(gp_row[None].expand(R, -1))
         v.capacity[:R].copy_(cap)
         v.damaged[:R].copy_(dmg)
         v.flow[:R].copy_(flow)
@@ -93,7 +98,10 @@ def select_greedy_one_step(env: RepairEnv, state: EnvState) -> int:
     wb = _batches.get(key)
     if wb is None or wb.graph is not env.graph:
         wb = _batches[key] = WhatIfBatch(env.graph, env._vec.params, dev, max(D, 32))
-    ts = wb.tstt(cap, dmg, flow).cpu().numpy()
+    gp_row = None if env._vec.gp_state is None else env._vec.gp_state.view(1, -1)[0]
+    if env._gp_dirty:
+        env._push()
+    ts = wb.tstt(cap, dmg, flow, gp_row).cpu().numpy()
     return int(candidates[int(np.argmin(ts))])  # first strict minimum, like `if env.tstt < best_tstt`
 
 

@@ -74,8 +74,6 @@ class RepairEnv:
         self.bpr_beta = bpr_beta
         self.assignment_iters = assignment_iters
         self.assignment_method = assignment_method.lower()
-        if self.assignment_method == "gp":
-            raise NotImplementedError("assignment_method='gp' (path-based, repair_env.py:352-419) is not ported yet")
         self.sp_backend = (sp_backend or "auto").lower()
         self.force_gpu_sp = bool(force_gpu_sp)
         self.use_cugraph = use_cugraph
@@ -103,7 +101,11 @@ class RepairEnv:
             graph_data, 1, device=dev, damaged_ratio=damaged_ratio, bpr_alpha=bpr_alpha, bpr_beta=bpr_beta,
             assignment_iters=assignment_iters, assignment_method=self.assignment_method, reward_mode=reward_mode,
             reward_alpha=reward_alpha, reward_beta=reward_beta, reward_gamma=reward_gamma, reward_clip=reward_clip,
-            capacity_damage=capacity_damage, unassigned_penalty=unassigned_penalty, seeds=[seed], reset=False)
+            capacity_damage=capacity_damage, unassigned_penalty=unassigned_penalty, gp_step=gp_step,
+            gp_keep_paths=gp_keep_paths, seeds=[seed], reset=False)
+        self._gp_cache = None    # GP path sets decoded from the device (od_paths, od_path_flows)
+        self._gp_dirty = False   # set when a caller assigns od_paths / od_path_flows
+        self._od_host = [{}, {}]
         self.graph: TrafficGraph = self._vec.graph
         self._sampler: DamageSampler = self._vec.samplers[0]
         self.rng = self._sampler.rng
@@ -128,8 +130,6 @@ class RepairEnv:
         self.unassigned_demand = 0.0
         self.is_reset = True
         self.tstt = None
-        self.od_paths: Dict = {}
-        self.od_path_flows: Dict = {}
         self.is_damaged = np.zeros(self.num_edges, dtype=np.float32)
         self.goal_mask = np.zeros(self.num_edges, dtype=np.float32)
         self.flow = np.zeros(self.num_edges, dtype=np.float32)
@@ -140,9 +140,36 @@ class RepairEnv:
         self._init_betweenness()
         self.reset(damaged_ratio=damaged_ratio)
 
+    # ------------------------------------------------------ GP path sets
+    # RepairEnv.od_paths / od_path_flows (repair_env.py:199-200, 351-404).  With
+    # assignment_method="gp" they live on the device; reading decodes them,
+    # assigning (e.g. the greedy baseline's deepcopy restore,
+    # src/baselines/__init__.py:46-65) uploads them before the next kernel call.
+    def _gp_get(self, i):
+        if self._vec.gp_state is None:
+            return self._od_host[i]
+        if self._gp_cache is None:
+            self._gp_cache = list(self._vec.gp_paths(0))
+        return self._gp_cache[i]
+
+    def _gp_set(self, i, value):
+        if self._vec.gp_state is None:
+            self._od_host[i] = value
+            return
+        if self._gp_cache is None:
+            self._gp_cache = list(self._vec.gp_paths(0))
+        self._gp_cache[i] = value
+        self._gp_dirty = True
+
+    od_paths = property(lambda self: self._gp_get(0), lambda self, v: self._gp_set(0, v))
+    od_path_flows = property(lambda self: self._gp_get(1), lambda self, v: self._gp_set(1, v))
+
     # ------------------------------------------------------ host <-> device
     def _push(self):
         v = self._vec
+        if self._gp_dirty:
+            v.set_gp_paths(0, self._gp_cache[0], self._gp_cache[1])
+            self._gp_dirty = False
         v.flow[0].copy_(torch.from_numpy(np.asarray(self.flow, np.float32)))
         v.capacity[0].copy_(torch.from_numpy(np.asarray(self.capacities, np.float32)))
         v.damaged[0].copy_(torch.from_numpy(np.asarray(self.is_damaged, np.float32)))
@@ -152,6 +179,7 @@ class RepairEnv:
 
     def _pull(self):
         v = self._vec
+        self._gp_cache = None
         self.flow = v.flow[0].cpu().numpy().copy()
         self.capacities = v.capacity[0].cpu().numpy().copy()
         self.is_damaged = v.damaged[0].cpu().numpy().copy()
@@ -174,8 +202,9 @@ class RepairEnv:
         self._vec.reset(damaged=torch.from_numpy(mask)[None], observe=False)
         self._pull()
         self.initial_tstt = self.tstt
-        self.od_paths = {}
-        self.od_path_flows = {}
+        if self._vec.gp_state is None:  # GP: the reset assignment rebuilt the device path sets
+            self.od_paths = {}
+            self.od_path_flows = {}
         self.is_reset = False
         return self.get_state()
 

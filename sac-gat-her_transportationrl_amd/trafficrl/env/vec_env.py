@@ -52,6 +52,8 @@ class VecRepairEnv:
         reward_clip: float = 0.0,
         capacity_damage: float = 1e-3,
         unassigned_penalty: float = 2e7,
+        gp_step: float = 1.0,
+        gp_keep_paths: int = 3,
         fixed_damage: bool = False,
         fixed_damage_seed: Optional[int] = None,
         seed: int = 0,
@@ -60,7 +62,7 @@ class VecRepairEnv:
         reset: bool = True,
     ):
         if assignment_method.lower() not in _lib.METHODS:
-            raise ValueError(f"assignment_method {assignment_method!r} not supported (msa, fw, cfw)")
+            raise ValueError(f"assignment_method {assignment_method!r} not supported (msa, fw, cfw, gp)")
         if int(assignment_iters) <= 0:
             raise ValueError("assignment_iters must be > 0 to update TSTT.")
         dev = torch.device(device)
@@ -85,7 +87,8 @@ class VecRepairEnv:
             method=_lib.METHODS[self.assignment_method], iters=self.assignment_iters, bpr_alpha=bpr_alpha,
             bpr_beta=bpr_beta, capacity_damage=capacity_damage, unassigned_penalty=unassigned_penalty,
             reward_mode=_lib.REWARD_MODES[reward_mode], reward_alpha=reward_alpha, reward_beta=reward_beta,
-            reward_gamma=reward_gamma, reward_clip=reward_clip)
+            reward_gamma=reward_gamma, reward_clip=reward_clip, gp_step=float(gp_step),
+            gp_keep_paths=int(gp_keep_paths))
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         f64 = dict(dtype=torch.float64, device=dev)
@@ -102,10 +105,15 @@ class VecRepairEnv:
         self.valid = torch.zeros(B, dtype=torch.uint8, device=dev)
         self._obs_bufs = None
         self.workspace = torch.empty(self.graph.workspace_bytes(B), dtype=torch.uint8, device=dev)
+        # GP: per-env path sets (RepairEnv.od_paths / od_path_flows) live on the device
+        self.gp_state = None
+        if self.assignment_method == "gp":
+            self.gp_state = torch.zeros(self.graph.gp_state_bytes(B, gp_keep_paths), dtype=torch.uint8, device=dev)
         self._state = _lib.TrxState(
             flow=self.flow.data_ptr(), capacity=self.capacity.data_ptr(), damaged=self.damaged.data_ptr(),
             goal=self.goal.data_ptr(), t=self.t.data_ptr(), tstt=self.tstt.data_ptr(),
-            initial_tstt=self.initial_tstt.data_ptr(), unassigned=self.unassigned.data_ptr())
+            initial_tstt=self.initial_tstt.data_ptr(), unassigned=self.unassigned.data_ptr(),
+            gp=0 if self.gp_state is None else self.gp_state.data_ptr())
         self.edge_index = torch.as_tensor(self.graph.edge_index, device=dev)
         self._seeds = list(seeds) if seeds is not None else [seed + i for i in range(B)]
         self._fixed = (fixed_damage, fixed_damage_seed)
@@ -200,6 +208,67 @@ class VecRepairEnv:
                    "trx_observe")
         log_tstt = torch.log10(torch.clamp(self.tstt, min=1.0))
         return VecObs(node_x, edge_x, mask, log_tstt)
+
+    # ------------------------------------------------------ GP path sets
+    def _gp_rows(self):
+        if self.gp_state is None:
+            raise ValueError("path sets exist only for assignment_method='gp'")
+        P = len(self.graph.od_o)
+        lay = _lib.gp_layout(P, int(self.params.gp_keep_paths))
+        return self.gp_state.view(self.num_envs, lay["total"]), lay, P
+
+    def gp_paths(self, b: int):
+        """Env b's (od_paths, od_path_flows) as the reference's dicts
+        (repair_env.py:374-404): 1-based (o, d) keys in insertion order, paths
+        as link-id tuples in path order, float64 flows."""
+        rows, lay, P = self._gp_rows()
+        row = rows[b].cpu().numpy()
+        KP = int(self.params.gp_keep_paths) + 1
+        nkeys = int(row[lay["nkeys"]:lay["nkeys"] + 4].view(np.int32)[0])
+        order = row[lay["ord"]:lay["ord"] + 2 * P].view(np.int16)[:nkeys]
+        npath = row[lay["np"]:lay["np"] + P]
+        flows = row[lay["flow"]:lay["flow"] + 8 * P * KP].view(np.float64).reshape(P, KP)
+        lens = row[lay["len"]:lay["len"] + P * KP].reshape(P, KP)
+        edges = row[lay["edges"]:lay["edges"] + P * KP * _lib.GP_MAX_HOPS].reshape(P, KP, _lib.GP_MAX_HOPS)
+        key_of = self.graph.od_key_order()
+        paths, pflows = {}, {}
+        for q in order.tolist():
+            key = key_of[q]
+            n = int(npath[q])
+            paths[key] = [tuple(int(e) for e in edges[q, i, :lens[q, i]]) for i in range(n)]
+            pflows[key] = [float(flows[q, i]) for i in range(n)]
+        return paths, pflows
+
+    def set_gp_paths(self, b: int, paths: dict, pflows: dict):
+        """Load env b's path sets from reference-style dicts (inverse of gp_paths)."""
+        rows, lay, P = self._gp_rows()
+        KP = int(self.params.gp_keep_paths) + 1
+        row = np.zeros(lay["total"], np.uint8)
+        q_of = {k: q for q, k in enumerate(self.graph.od_key_order())}
+        order = np.zeros(P, np.int16)
+        npath = np.zeros(P, np.uint8)
+        flows = np.zeros((P, KP), np.float64)
+        masks = np.zeros((P, KP, 4), np.uint32)
+        lens = np.zeros((P, KP), np.uint8)
+        edges = np.zeros((P, KP, _lib.GP_MAX_HOPS), np.uint8)
+        for k, key in enumerate(paths):
+            q = q_of[key]
+            order[k] = q
+            npath[q] = len(paths[key])
+            for i, (pth, f) in enumerate(zip(paths[key], pflows[key])):
+                flows[q, i] = f
+                lens[q, i] = len(pth)
+                edges[q, i, :len(pth)] = pth
+                for e in pth:
+                    masks[q, i, e // 32] |= np.uint32(1 << (e % 32))
+        row[lay["nkeys"]:lay["nkeys"] + 4] = np.array([len(paths)], np.int32).view(np.uint8)
+        row[lay["ord"]:lay["ord"] + 2 * P] = order.view(np.uint8)
+        row[lay["np"]:lay["np"] + P] = npath
+        row[lay["flow"]:lay["flow"] + 8 * P * KP] = flows.reshape(-1).view(np.uint8)
+        row[lay["mask"]:lay["mask"] + 16 * P * KP] = masks.reshape(-1).view(np.uint8)
+        row[lay["len"]:lay["len"] + P * KP] = lens.reshape(-1)
+        row[lay["edges"]:lay["edges"] + P * KP * _lib.GP_MAX_HOPS] = edges.reshape(-1)
+        rows[b].copy_(torch.from_numpy(row))
 
     def is_goal_complete(self) -> torch.Tensor:
         return (self.goal * self.damaged).sum(dim=1) == 0

@@ -67,6 +67,20 @@ class TrafficGraph:
             _lib.check(int(b), "trx_workspace_bytes")
         return int(b)
 
+    def od_key_order(self):
+        """1-based (o, d) keys in the device's OD order: grouped by origin
+        ascending, dict order inside an origin (repair_env.py:490-491)."""
+        if not hasattr(self, "_od_keys"):
+            idx = sorted(range(len(self.od_o)), key=lambda k: (int(self.od_o[k]), k))
+            self._od_keys = [(int(self.od_o[k]) + 1, int(self.od_d[k]) + 1) for k in idx]
+        return self._od_keys
+
+    def gp_state_bytes(self, num_envs: int, keep_paths: int) -> int:
+        b = _lib.load().trx_gp_state_bytes(self._h, int(num_envs), int(keep_paths))
+        if b < 0:
+            _lib.check(int(b), "trx_gp_state_bytes")
+        return int(b)
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value and _lib._lib is not None:

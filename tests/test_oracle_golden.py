@@ -196,3 +196,39 @@ def test_oracle_anaheim_synth_scipy_preds():
     for k in range(len(z["seeds"])):
         _, p = og.all_pairs(z["t"][k])
         np.testing.assert_array_equal(p[z["origins"]], z["pred"][k])
+
+
+# ------------------------------------------------ GP path assignment oracle
+GP_CASES = {"s1k2i30": (1.0, 2, 30), "s1k3i10": (1.0, 3, 10), "s0k3i10": (0.0, 3, 10), "s05k2i8": (0.5, 2, 8)}
+
+
+@pytest.mark.parametrize("tag", sorted(GP_CASES))
+def test_oracle_gp_reset_and_steps_bitexact(tag, oracle_graph):
+    """GP restatement (oracle.gp_assign) == reference on seed-42 resets and on
+    4 random-seed reset + 3-step trajectories (path sets carried across steps)."""
+    step, keep, iters = GP_CASES[tag]
+    og = oracle_graph
+    z = np.load(golden("sf_gp_crpow.npz"))
+    d = z[f"reset_{tag}_damaged"]
+    cap = np.where(d > 0, np.float32(1e-3), og.cap0).astype(np.float32)
+    f, t, ts, un = O.gp_assign(og, cap, d, np.zeros(og.E, np.float32), O.GPPaths(), iters, step, keep, reset=True)
+    np.testing.assert_array_equal(f, z[f"reset_{tag}_flow"])
+    np.testing.assert_array_equal(t, z[f"reset_{tag}_t"])
+    assert ts == float(z[f"reset_{tag}_tstt"])
+    dm = z[f"steps_{tag}_damaged"]
+    for i in range(len(dm)):
+        d = dm[i].copy()
+        cap = np.where(d > 0, np.float32(1e-3), og.cap0).astype(np.float32)
+        st = O.GPPaths()
+        f, _, ts, _ = O.gp_assign(og, cap, d, np.zeros(og.E, np.float32), st, iters, step, keep, reset=True)
+        np.testing.assert_array_equal(f, z[f"steps_{tag}_flow"][i])
+        for j in range(3):
+            a = int(z[f"steps_{tag}_actions"][i, j])
+            if d[a] == 0:
+                assert z[f"steps_{tag}_step_reward"][i, j] == -1.0
+                continue
+            d[a] = 0.0
+            cap[a] = og.cap0[a]
+            f, _, ts, _ = O.gp_assign(og, cap, d, f, st, iters, step, keep)
+            np.testing.assert_array_equal(f, z[f"steps_{tag}_step_flow"][i, j])
+            assert ts == z[f"steps_{tag}_step_tstt"][i, j]
