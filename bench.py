@@ -150,13 +150,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU; TRX_DIST_BACKEND=gloo rehearses the multi-rank path on
+    # fewer GPUs than ranks (ranks then share devices: local % device_count)
+    backend = os.environ.get("TRX_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()) if world > 1 else 0)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
 
     from trafficrl.env import VecRepairEnv
 
