@@ -33,6 +33,11 @@ from torch import nn
 import torch.nn.functional as F
 
 from .. import _lib
+from .skinny import perm_gather, skinny_linear
+
+# in-feature widths up to which a projection's weight gradient takes the
+# split-K path (trafficrl/models/skinny.py)
+_SKINNY_IN = 8
 
 
 # --------------------------------------------------------------- graph CSR
@@ -52,6 +57,7 @@ class GraphCSR:
     kept_idx: Optional[torch.Tensor]  # [E_kept] int64 kept input edges, None when no input self loops
     in_pad: torch.Tensor    # [N, D] int64 kept-edge ids entering each node, padded with E_kept (zero row)
     dst_kept: torch.Tensor  # [E_kept] int64 destination of each kept edge
+    inv_perm: torch.Tensor  # [Et] int64 inverse of perm (PyG-order edge id -> CSR position)
 
 
 _csr_cache: Dict[Tuple, GraphCSR] = {}
@@ -95,8 +101,11 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int) -> GraphCSR:
     slot = torch.arange(Ek, device=dev) - kstart[dk[order]]
     in_pad = torch.full((num_nodes, D), Ek, dtype=torch.int64, device=dev)
     in_pad[dk[order], slot] = order
+    inv_perm = torch.empty_like(perm)
+    inv_perm[perm] = torch.arange(Et, device=dev)
     g = GraphCSR(num_nodes, keep, src_all, dst_all, perm, rowptr.to(torch.int32), col.to(torch.int32),
-                 sptr.to(torch.int32), sperm.to(torch.int32), sdst.to(torch.int32), deg_in, kept_idx, in_pad, dk)
+                 sptr.to(torch.int32), sperm.to(torch.int32), sdst.to(torch.int32), deg_in, kept_idx, in_pad, dk,
+                 inv_perm)
     if len(_csr_cache) > 64:
         _csr_cache.clear()
     _csr_cache[key] = g
@@ -223,20 +232,30 @@ class GATConv(nn.Module):
         H, C = self.heads, self.out_channels
         N = x.size(0)
         g = build_csr(edge_index, N)
-        xh = self.lin(x)                                   # [N, H*C]  (MFMA GEMM)
-        xh3 = xh.view(N, H, C).float()
-        a_src = (xh3 * self.att_src).sum(-1)               # [N, H]
-        a_dst = (xh3 * self.att_dst).sum(-1)
+        if self.in_channels <= _SKINNY_IN:
+            xh = skinny_linear(x, self.lin.weight)         # [N, H*C]  (4 input features)
+        else:
+            xh = self.lin(x)                               # [N, H*C]  (MFMA GEMM)
+        # per-head attention dot products <xh_h, att_h> for src and dst as ONE
+        # float32 product with a block-diagonal [H*C, 2H] matrix (skinny:
+        # split-K weight gradient); same fp32 values as (xh3 * att).sum(-1)
+        eye = torch.eye(H, device=xh.device, dtype=torch.float32)
+        A = torch.cat([(self.att_src.view(H, C, 1).float() * eye.view(H, 1, H)).reshape(H * C, H),
+                       (self.att_dst.view(H, C, 1).float() * eye.view(H, 1, H)).reshape(H * C, H)], 1)
+        with torch.autocast("cuda", enabled=False):
+            a_sd = skinny_linear(xh.float(), A.t())        # [N, 2H]
+        a_src, a_dst = a_sd[:, :H], a_sd[:, H:]
         if self.lin_edge is not None and edge_attr is not None:
             ea = (edge_attr if g.kept_idx is None else edge_attr.index_select(0, g.kept_idx)).float()
             # fill_value='mean': loop attr = mean of the node's incoming edge attrs
             loop = _LoopMean.apply(ea, g)
             full = torch.cat([ea, loop], 0)
             M = (self.lin_edge.weight.view(H, C, -1).float() * self.att_edge.view(H, C, 1).float()).sum(1)
-            a_edge = full @ M.t()                          # [Et, H]
+            a_edge = skinny_linear(full, M)                # [Et, H]
         else:
             a_edge = torch.zeros(g.src_all.numel(), H, device=x.device)
-        out, alpha = gat_aggregate(xh, a_src, a_dst, a_edge[g.perm], g, H, C, self.negative_slope)
+        out, alpha = gat_aggregate(xh, a_src, a_dst, perm_gather(a_edge, g.perm, g.inv_perm), g, H, C,
+                                   self.negative_slope)
         if not self.concat:
             out = out.view(N, H, C).mean(1)
         if self.bias is not None:
@@ -319,7 +338,9 @@ class GATEncoder(nn.Module):
                 x_in = x
                 x = layer(x, edge_index, edge_attr=edge_attr)
                 if i == 0:
-                    x_in = self.input_proj(x_in)
+                    ip = self.input_proj
+                    x_in = (skinny_linear(x_in, ip.weight, ip.bias) if ip.in_features <= _SKINNY_IN
+                            else ip(x_in))
                 x = self.norms[i](x)
                 x = torch.relu(x + x_in)
                 continue

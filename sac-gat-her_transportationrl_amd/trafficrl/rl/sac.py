@@ -20,7 +20,7 @@ how the work maps to MI355X:
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Callable, Optional
+from typing import Callable, Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -29,6 +29,7 @@ import torch.nn.functional as F
 
 from ..models import fused
 from ..models.gat_encoder import GATEncoder, is_regular_batch
+from ..models.skinny import regular_gather, skinny_linear
 
 
 @dataclass
@@ -94,6 +95,32 @@ def is_regular_edges(edge_index: torch.Tensor, batch: torch.Tensor, num_graphs: 
     return r
 
 
+_regular_cache: Dict[Tuple, Tuple] = {}
+
+
+def regular_layout(edge_index: torch.Tensor, batch: torch.Tensor, num_graphs: int):
+    """(B, src_local, dst_local) when every graph of the batch has the same
+    edge list (local node ids) in its own contiguous block, else None.
+    Checked once per (edge_index, batch) pair and cached."""
+    if not is_regular_edges(edge_index, batch, num_graphs) or not is_regular_batch(batch, num_graphs):
+        return None
+    key = (edge_index.data_ptr(), edge_index._version, batch.data_ptr(), batch._version, num_graphs)
+    r = _regular_cache.get(key)
+    if r is None:
+        B, E, N = num_graphs, edge_index.shape[1], batch.numel()
+        m, n = E // B, N // B
+        if N % B:
+            r = False
+        else:
+            loc = edge_index.long() - (torch.arange(B, device=edge_index.device) * n).repeat_interleave(m)
+            loc = loc.view(2, B, m)
+            r = (B, loc[0, 0].contiguous(), loc[1, 0].contiguous()) if bool((loc == loc[:, :1]).all()) else False
+        if len(_regular_cache) > 64:
+            _regular_cache.clear()
+        _regular_cache[key] = r
+    return r if r is not False else None
+
+
 @torch.no_grad()
 def clip_grad_norm_listwise_(params, max_norm: float):
     """torch.nn.utils.clip_grad_norm_ with the reference's list semantics made
@@ -147,16 +174,26 @@ class _EdgeHead(nn.Module):
         self.embed, self.edge_in = embed, edge_in
         self.edge_mlp = nn.Sequential(nn.Linear(embed * 4 + edge_in, hidden), nn.ReLU(), nn.Linear(hidden, 1))
 
-    def edge_scores(self, node_emb, global_ctx, edge_attr, src, dst, edge_batch):
+    def edge_scores(self, node_emb, global_ctx, edge_attr, src, dst, edge_batch, regular=None):
+        """regular = (B, src_local, dst_local) for fixed-topology batches: the
+        gathers then scatter back with incidence products (models/skinny.py)."""
         W1, b1 = self.edge_mlp[0].weight, self.edge_mlp[0].bias
         d, k = self.embed, self.edge_in
         w_nodes = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)          # [2H, embed]
         p = node_emb @ w_nodes.t()                                    # per-node projections
         hdim = W1.shape[0]
-        z = p[src, :hdim] + p[dst, hdim:]
-        z = z + edge_attr @ W1[:, 2 * d:2 * d + k].t()
-        z = z + (global_ctx @ W1[:, 2 * d + k:].t() + b1)[edge_batch]
-        return self.edge_mlp[2](torch.relu(z)).squeeze(-1)
+        c = global_ctx @ W1[:, 2 * d + k:].t() + b1                   # [B, H] per-graph context
+        if regular is not None:
+            B, src_l, dst_l = regular
+            z = regular_gather(p[:, :hdim], src_l, B) + regular_gather(p[:, hdim:], dst_l, B)
+            z = z + skinny_linear(edge_attr, W1[:, 2 * d:2 * d + k])
+            z = z + c.unsqueeze(1).expand(B, src_l.numel(), hdim).reshape(-1, hdim)
+        else:
+            z = p[src, :hdim] + p[dst, hdim:]
+            z = z + skinny_linear(edge_attr, W1[:, 2 * d:2 * d + k])
+            z = z + c[edge_batch]
+        W2, b2 = self.edge_mlp[2].weight, self.edge_mlp[2].bias
+        return skinny_linear(torch.relu(z), W2, b2).squeeze(-1)
 
 
 class Actor(_EdgeHead):
@@ -180,7 +217,8 @@ class Actor(_EdgeHead):
                                                   return_attention=return_attention, num_graphs=B)
         src, dst = edge_index
         edge_batch = batch[src]
-        logits = self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, edge_batch).float()
+        logits = self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, edge_batch,
+                                  regular_layout(edge_index, batch, B)).float()
         logits = logits.masked_fill(action_mask <= 0, -1e9)
         per = logits.numel() // B if is_regular_edges(edge_index, batch, B) else None
         probs = segment_softmax(logits, edge_batch, B, per)
@@ -206,7 +244,8 @@ class Critic(_EdgeHead):
             return fused.edge_head_infer(self, emb, ctx, edge_attr, topo)
         node_emb, global_ctx, _ = self.encoder(node_x, edge_index, edge_attr, batch, num_graphs=B)
         src, dst = edge_index
-        return self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, batch[src]).float()
+        return self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, batch[src],
+                                regular_layout(edge_index, batch, B)).float()
 
 
 class DiscreteSAC:
