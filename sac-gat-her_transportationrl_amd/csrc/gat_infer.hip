@@ -63,13 +63,15 @@ __device__ __forceinline__ float wave_max_f(float v) {
 #undef TRX_DPPM
 __device__ __forceinline__ float leaky_f(float x, float slope) { return x > 0.0f ? x : x * slope; }
 
-// fp32 -> bf16 bits, round to nearest even (torch's conversion)
-__device__ __forceinline__ uint16_t f2bf(float x) {
-    uint32_t u = __float_as_uint(x);
-    if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
+// fp32 -> bf16 bits, round to nearest even (torch's conversion): gfx950's
+// v_cvt_pk_bf16_f32 (one instruction per pair) instead of integer arithmetic
+typedef float trx_f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 trx_b2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+    const trx_f2 v = {lo, hi};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, trx_b2));
 }
+__device__ __forceinline__ uint16_t f2bf(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ float bf16r(float x) { return bf2f(f2bf(x)); }
 
@@ -269,7 +271,6 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
             const int f0 = 4 * (lane + kWave * k);
             const float resv[4] = {res4[k].x, res4[k].y, res4[k].z, res4[k].w};
             float y4[4];
-            uint16_t ob[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float y = lnw_r[k][r] * (rstd * (v[k][r] - mean)) + lnb_r[k][r];
@@ -286,15 +287,14 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
                 else
                     y = y <= 0.0f ? (expf(y) - 1.0f) : y;
                 y4[r] = y;
-                ob[r] = f2bf(y);
                 if (a.pool) yt[i * HC + f0 + r] = y;
             }
             if (a.out_f32)
                 *reinterpret_cast<float4*>(a.out_f32 + (size_t)node * HC + f0) = make_float4(y4[0], y4[1], y4[2], y4[3]);
             if (a.out_bf16) {
                 uint2 u;
-                u.x = (uint32_t)ob[0] | ((uint32_t)ob[1] << 16);
-                u.y = (uint32_t)ob[2] | ((uint32_t)ob[3] << 16);
+                u.x = pk_bf16(y4[0], y4[1]);
+                u.y = pk_bf16(y4[2], y4[3]);
                 *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.out_bf16) + (size_t)node * HC + f0) = u;
             }
         }
