@@ -71,6 +71,7 @@ struct SmemQ {
     uint32_t insrc;  // [E] u8
     uint32_t eid;    // [NP*NP] i16
     uint32_t dem;    // [Z*N] f32
+    uint32_t t0;     // [E] f32 free-flow times (read by every BPR pass)
     uint32_t unas;   // [L] f32
     uint32_t act;    // [EPW] i32
     uint32_t red;    // [EPW*2] f64
@@ -105,6 +106,7 @@ __host__ __device__ inline SmemQ smemq_layout(int E, int N, int Z, int NP, int E
     o.insrc = take((uint32_t)E);
     o.eid = take((uint32_t)(NP * NP * 2));
     o.dem = take((uint32_t)(Z * N * 4));
+    o.t0 = take((uint32_t)(E * 4));
     o.unas = take((uint32_t)(L * 4));
     o.act = take((uint32_t)(EPW * 4));
     o.red = take((uint32_t)(EPW * 2 * 8));
@@ -155,13 +157,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
         int *nscan, *act;
         int16_t *inptr, *eid;
         FibLane* heap;
+        float* t0;
     } S = {(float*)(smem_raw + O.flow), (float*)(smem_raw + O.cap),   (float*)(smem_raw + O.dmg),
            (float*)(smem_raw + O.goal), (float*)(smem_raw + O.t),     (float*)(smem_raw + O.aux),
            (float*)(smem_raw + O.dprev), (float*)(smem_raw + O.w),    (float*)(smem_raw + O.dem),
            (float*)(smem_raw + O.unas), smem_raw + O.pred,            smem_raw + O.ord,
            smem_raw + O.insrc,          (double*)(smem_raw + O.dist), (double*)(smem_raw + O.red),
            (int*)(smem_raw + O.nscan),  (int*)(smem_raw + O.act),     (int16_t*)(smem_raw + O.inptr),
-           (int16_t*)(smem_raw + O.eid), (FibLane*)(smem_raw + O.heap)};
+           (int16_t*)(smem_raw + O.eid), (FibLane*)(smem_raw + O.heap), (float*)(smem_raw + O.t0)};
 #ifdef TRX_PHASE_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -191,6 +194,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
     for (int i = tid; i < Z * N; i += L) S.dem[i] = g.dem[i];
     for (int i = tid; i <= N; i += L) S.inptr[i] = (int16_t)g.in_ptr[i];
     for (int i = tid; i < E; i += L) S.insrc[i] = (uint8_t)g.in_src[i];
+    for (int i = tid; i < E; i += L) S.t0[i] = g.t0[i];
     __syncthreads();
 
     // ------------------------------------------------------- load state
@@ -221,7 +225,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
         S.goal[i] = gl;
         S.aux[i] = 0.0f;
         S.dprev[i] = 0.0f;
-        S.t[i] = S.act[el] ? bpr_cost(fl, cp, g.t0[e], dm, p.bpr_alpha, p.bpr_beta) : 0.0f;
+        S.t[i] = S.act[el] ? bpr_cost(fl, cp, S.t0[e], dm, p.bpr_alpha, p.bpr_beta) : 0.0f;
     }
     __syncthreads();
     TRX_STAMP(0);
@@ -461,7 +465,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
             if (nf != nf) nf = 0.0f;  // nan_to_num guard (repair_env.py:338-340)
             S.flow[i] = nf;
             S.aux[i] = 0.0f;
-            S.t[i] = bpr_cost(nf, S.cap[i], g.t0[e], S.dmg[i], p.bpr_alpha, p.bpr_beta);
+            S.t[i] = bpr_cost(nf, S.cap[i], S.t0[e], S.dmg[i], p.bpr_alpha, p.bpr_beta);
         }
         __syncthreads();
         TRX_STAMP(5);

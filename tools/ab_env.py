@@ -1,0 +1,31 @@
+"""A/B timing of the env kernel from two builds of libtrafficrl.so in one
+process each: python tools/ab_env.py <lib.so> [B] [reps]."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
+import torch  # noqa: E402
+from trafficrl import _lib  # noqa: E402
+
+_lib.LIB_PATH = os.path.abspath(sys.argv[1])
+from trafficrl.data import sioux_falls  # noqa: E402
+from trafficrl.env import VecRepairEnv  # noqa: E402
+
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=True, fixed_damage_seed=42)
+gen = torch.Generator(device="cuda").manual_seed(0)
+acts = [(torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32) for _ in range(2)]
+flow0, cap0, dmg0 = env.flow.clone(), env.capacity.clone(), env.damaged.clone()
+ms = []
+for r in range(reps):
+    env.flow.copy_(flow0); env.capacity.copy_(cap0); env.damaged.copy_(dmg0)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    env.step(acts[0], observe=False, check=False)
+    e.record()
+    torch.cuda.synchronize()
+    ms.append(s.elapsed_time(e))
+ms = sorted(ms)[2:-2]
+print(f"{os.path.basename(sys.argv[1])}: step kernel {sum(ms) / len(ms):.4f} ms (B={B})")
