@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 2
+#define TRX_ABI_VERSION 3
 
 /* error codes */
 #define TRX_OK 0
@@ -229,7 +229,8 @@ int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
  *   logit = bf16(bf16(relu(z)) . w2 + b2)
  * p [N, 2H] bf16 = node_emb @ [W_src; W_dst]^T, c [B, H] fp32 = bf16(ctx @ W_ctx^T) + b1.
  * softmax != 0: logits masked (mask <= 0 -> -1e9) and soft-maxed per graph
- * (Actor probs); else raw logits (Critic Q).  hidden <= 512, edge_dim <= 8. */
+ * (Actor probs); else raw logits (Critic Q).  hidden <= 512, edge_dim <= 8,
+ * nodes_per_graph * hidden <= 32768 (the graph's p rows are staged in LDS). */
 typedef struct trx_edge_head_args {
     int32_t num_graphs, edges_per_graph, hidden, edge_dim;
     const int32_t* src;         /* [B*E] global node ids */
@@ -244,8 +245,52 @@ typedef struct trx_edge_head_args {
     int32_t softmax;
     float* out;                 /* [B*E] probs (softmax) or logits */
     float* logits;              /* [B*E] masked logits when softmax, or NULL */
+    int32_t nodes_per_graph;    /* n: graph g's links join nodes [g*n, g*n + n) (regular batch) */
+    const float* u;             /* [B] uniforms in [0,1) or NULL: with softmax != 0, also draw one link
+                                   per graph from the probs (inverse CDF: the first link whose running
+                                   sum of exp(logit - max) exceeds u * total) into `action` */
+    int64_t* action;            /* [B] drawn graph-local link (u != NULL) */
 } trx_edge_head_args;
 int trx_edge_head_infer(const trx_edge_head_args* a, void* stream);
+
+/* Input stage of Actor/Critic (src/rl/sac.py:38-41) plus every layer's edge
+ * attention logits (src/models/gat_encoder.py:36-52: PyG GATConv with
+ * edge_dim and add_self_loops fill_value='mean') for regular batches:
+ *   x0 = LayerNorm(node_x), ea = LayerNorm(edge_x)                  (fp32)
+ *   loop[i] = mean of ea over the links entering i with src != dst (0 if none)
+ *   M_l[h, :] = sum_c lin_edge_l.weight[h*C + c, :] * att_edge_l[h, c]
+ *   a_edge[p, off_l + h] = bf16(bf16(full[p]) . bf16(M_l[h, :]))
+ * full[p] is ea of the link, or the node's loop attr, at CSR position p
+ * (pos_src); off_l = heads_0 + ... + heads_{l-1}.  bf16-autocast numerics.
+ * node_dim, edge_dim <= 8, num_layers <= 4, sum of heads <= 32,
+ * nodes_per_graph <= 64, edges_per_graph <= 1024.                          */
+#define TRX_MAX_GAT_LAYERS 4
+typedef struct trx_gat_prologue_args {
+    int32_t num_graphs, nodes_per_graph, edges_per_graph, node_dim, edge_dim;
+    const float* node_x;        /* [B*n, node_dim] raw node features */
+    const float* edge_x;        /* [B*e, edge_dim] raw link features */
+    const float* node_ln_w;     /* [node_dim] */
+    const float* node_ln_b;
+    float node_ln_eps;
+    const float* edge_ln_w;     /* [edge_dim] */
+    const float* edge_ln_b;
+    float edge_ln_eps;
+    const int32_t* src;         /* [B*e] global node ids of the input links */
+    const int32_t* dst;
+    const int32_t* rowptr;      /* [N+1] CSR by destination, self loops included */
+    const int32_t* pos_src;     /* [Et] per CSR position: input link id (>= 0) or -(node + 1) for a self loop */
+    int32_t num_layers;
+    int32_t heads[TRX_MAX_GAT_LAYERS];
+    int32_t channels[TRX_MAX_GAT_LAYERS];
+    const float* lin_edge_w[TRX_MAX_GAT_LAYERS];  /* [heads*channels, edge_dim] */
+    const float* att_edge[TRX_MAX_GAT_LAYERS];    /* [heads*channels] */
+    float* m_work;              /* [sum heads, edge_dim] scratch: the M rows */
+    float* x0;                  /* out [B*n, node_dim] */
+    float* ea;                  /* out [B*e, edge_dim] */
+    float* a_edge;              /* out [Et, sum heads], CSR order; a graph whose CSR range references
+                                   links or nodes of another graph gets NaN rows */
+} trx_gat_prologue_args;
+int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream);
 
 /* ------------------------------------------------- prioritized replay
  * Sum tree of src/train.py:27-91 (ReplayBuffer) on the device: tree[1] is the

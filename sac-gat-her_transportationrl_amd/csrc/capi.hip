@@ -543,11 +543,42 @@ int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
         return fail(TRX_EUNSUP, "edge_head_infer: edges_per_graph must be 1..4096");
     if (a->hidden < 1 || a->hidden > 512 || a->edge_dim < 1 || a->edge_dim > 8)
         return fail(TRX_EUNSUP, "edge_head_infer: hidden 1..512, edge_dim 1..8");
+    if (a->nodes_per_graph < 1 || (int64_t)a->nodes_per_graph * a->hidden > 32768)
+        return fail(TRX_EUNSUP, "edge_head_infer: nodes_per_graph must be 1..32768/hidden");
+    if (a->hidden % 4) return fail(TRX_EUNSUP, "edge_head_infer: hidden must be a multiple of 4");
+    if (trx::edge_head_infer_smem(*a) > 160 * 1024)
+        return fail(TRX_EUNSUP, "edge_head_infer: graph too large for LDS (nodes_per_graph, edges_per_graph)");
     if (!a->src || !a->dst || !a->p || !a->c || !a->ea || !a->we || !a->w2 || !a->b2 || !a->out || (a->softmax && !a->mask))
         return fail(TRX_EINVAL, "edge_head_infer: NULL buffer");
+    if (a->u && (!a->softmax || !a->action)) return fail(TRX_EINVAL, "edge_head_infer: u needs softmax and action");
     if (a->num_graphs == 0) return TRX_OK;
     hipError_t e = trx::launch_edge_head_infer(*a, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "edge_head_infer launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_prologue_infer: NULL args");
+    if (a->num_graphs < 0) return fail(TRX_EINVAL, "gat_prologue_infer: num_graphs < 0");
+    if (a->nodes_per_graph < 1 || a->nodes_per_graph > 64 || a->edges_per_graph < 0 || a->edges_per_graph > 1024)
+        return fail(TRX_EUNSUP, "gat_prologue_infer: nodes_per_graph 1..64, edges_per_graph 0..1024");
+    if (a->node_dim < 1 || a->node_dim > 8 || a->edge_dim < 1 || a->edge_dim > 8)
+        return fail(TRX_EUNSUP, "gat_prologue_infer: node_dim and edge_dim must be 1..8");
+    if (a->num_layers < 1 || a->num_layers > TRX_MAX_GAT_LAYERS)
+        return fail(TRX_EUNSUP, "gat_prologue_infer: num_layers must be 1..%d", TRX_MAX_GAT_LAYERS);
+    int A = 0;
+    for (int l = 0; l < a->num_layers; ++l) {
+        if (a->heads[l] < 1 || a->channels[l] < 1) return fail(TRX_EINVAL, "gat_prologue_infer: heads/channels < 1");
+        if (!a->lin_edge_w[l] || !a->att_edge[l]) return fail(TRX_EINVAL, "gat_prologue_infer: NULL layer weights");
+        A += a->heads[l];
+    }
+    if (A > 32) return fail(TRX_EUNSUP, "gat_prologue_infer: sum of heads must be <= 32");
+    if (!a->node_x || !a->edge_x || !a->node_ln_w || !a->node_ln_b || !a->edge_ln_w || !a->edge_ln_b || !a->src ||
+        !a->dst || !a->rowptr || !a->pos_src || !a->m_work || !a->x0 || !a->ea || !a->a_edge)
+        return fail(TRX_EINVAL, "gat_prologue_infer: NULL buffer");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_gat_prologue(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_prologue_infer launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
 

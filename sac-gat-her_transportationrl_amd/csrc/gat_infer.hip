@@ -74,8 +74,39 @@ __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
 __device__ __forceinline__ uint16_t f2bf(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ __forceinline__ float bf16r(float x) { return bf2f(f2bf(x)); }
+// native 16-byte vector: register arrays of HIP's struct uint4 are not promoted
+// out of scratch when written conditionally, this one is
+typedef unsigned int trx_u4 __attribute__((ext_vector_type(4)));
 
 }  // namespace
+
+#ifdef TRX_PHASE_STAMPS
+// Diagnostic build only (make stamps): per-phase cycle totals of the layer
+// kernel, thread 0 of each workgroup, rows 0 = layer 0, 1 = HC 1024, 2 = other.
+__device__ unsigned long long trx_infer_cycles[3][8];
+#define TRX_ISTAMP(slot)                                                      \
+    do {                                                                      \
+        if (threadIdx.x == 0) {                                               \
+            unsigned long long now_ = __builtin_amdgcn_s_memtime();            \
+            atomicAdd(&trx_infer_cycles[IN > 0 ? 0 : (HC == 1024 ? 1 : 2)][slot], now_ - stamp_prev_); \
+            stamp_prev_ = now_;                                               \
+        }                                                                     \
+    } while (0)
+extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_infer_cycles), sizeof(unsigned long long) * 24) != hipSuccess)
+        return -2;
+    if (reset) {
+        unsigned long long z[24] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(trx_infer_cycles), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#else
+#define TRX_ISTAMP(slot) \
+    do {                 \
+    } while (0)
+#endif
 
 // ------------------------------------------------------------- layer kernel
 // IN: 0 = xh given (layers >= 1), else the layer-0 input width (4).
@@ -86,9 +117,28 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
     const int g = blockIdx.x;
     const int n = a.nodes_per_graph, H = a.heads, C = a.channels;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+#ifdef TRX_PHASE_STAMPS
+    unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
     const int node0 = g * n;
     const int ebeg = a.rowptr[node0];
     const int ne = a.rowptr[node0 + n] - ebeg;
+    // 0a. xh rows of the graph (layers >= 1): all loads of a batch in flight before the LDS stores
+#ifndef TRX_STAGE_BATCH
+#define TRX_STAGE_BATCH 12
+#endif
+    constexpr int kStageBatch = TRX_STAGE_BATCH;
+    trx_u4 stg[kStageBatch];
+    const int nq = IN == 0 ? n * HC / 8 : 0;
+    const trx_u4* xsrc = IN == 0 ? reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.xh) + (size_t)node0 * HC)
+                                 : nullptr;
+    if (IN == 0) {
+#pragma unroll
+        for (int j = 0; j < kStageBatch; ++j) {
+            const int v = tid + kInferThreads * j;
+            if (v < nq) stg[j] = xsrc[v];
+        }
+    }
     if (ne > a.max_graph_edges || ne < 0) {  // LDS was sized for max_graph_edges: poison, do not overrun
         for (int idx = tid; idx < n * HC; idx += kInferThreads) {
             if (a.out_f32) a.out_f32[(size_t)node0 * HC + idx] = __builtin_nanf("");
@@ -99,94 +149,120 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
         return;
     }
 
-    const int SL = C < 64 ? C : 64, S = C / SL;          // attention dot-product segments
     uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // [n][HC] bf16
     float* as_ = reinterpret_cast<float*>(xs + n * HC);  // [n*H]
     float* ad_ = as_ + n * H;                            // [n*H]
-    const int alsz = a.max_graph_edges * H > 2 * n * H * S ? a.max_graph_edges * H : 2 * n * H * S;
     float* al = ad_ + n * H;        // [me*H] edge logits, then attention weights (in place)
-    float* part = al;               // [2*n*H*S] partial dot products (step 2 only, aliases al)
-    int* cl = reinterpret_cast<int*>(al + alsz);         // [me] source, graph-local
+    int* cl = reinterpret_cast<int*>(al + a.max_graph_edges * H);  // [me] source, graph-local
     int* rp = cl + a.max_graph_edges;                    // [n+1] graph-local row pointers
     float* x0l = reinterpret_cast<float*>(rp + n + 1);   // [n*IN]
     float* yt = x0l + n * IN;                            // [n][HC] (pool only)
 
-    // 0. graph-local CSR slice, edge logits, layer-0 inputs
-    for (int v = tid; v <= n; v += kInferThreads) rp[v] = a.rowptr[node0 + v] - ebeg;
-    for (int v = tid; v < ne; v += kInferThreads) cl[v] = a.col[ebeg + v] - node0;
-    if (IN > 0)
-        for (int v = tid; v < n * IN; v += kInferThreads) x0l[v] = bf16r(a.x0[(size_t)node0 * IN + v]);
+    // 0b. graph-local CSR slice, this layer's edge logits, layer-0 inputs: every
+    //     load of the phase issued before the first LDS store (one HBM round trip)
+    const int rpv = tid <= n ? a.rowptr[node0 + tid] : 0;
+    const int clv = tid < ne ? a.col[ebeg + tid] : 0;  // ne <= max_graph_edges <= 256
+    constexpr int kAlRegs = 4;
+    float alv[kAlRegs];
+#pragma unroll
+    for (int j = 0; j < kAlRegs; ++j) {
+        const int v = tid + kInferThreads * j, e = v / H, h = v - (v / H) * H;
+        alv[j] = v < ne * H ? a.a_edge[(size_t)(ebeg + e) * a.a_edge_stride + a.a_edge_offset + h] : 0.0f;
+    }
+    const float x0v = IN > 0 && tid < n * IN ? a.x0[(size_t)node0 * IN + tid] : 0.0f;  // n*IN <= 128
+    if (tid <= n) rp[tid] = rpv - ebeg;
+    if (tid < ne) cl[tid] = clv - node0;
+#pragma unroll
+    for (int j = 0; j < kAlRegs; ++j) {
+        const int v = tid + kInferThreads * j;
+        if (v < ne * H) al[v] = alv[j];
+    }
+    for (int v = tid + kInferThreads * kAlRegs; v < ne * H; v += kInferThreads) {
+        const int e = v / H, h = v - e * H;
+        al[v] = a.a_edge[(size_t)(ebeg + e) * a.a_edge_stride + a.a_edge_offset + h];
+    }
+    if (IN > 0 && tid < n * IN) x0l[tid] = bf16r(x0v);
     if (IN == 0) {
-        const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.xh) + (size_t)node0 * HC);
-        uint4* dst4 = reinterpret_cast<uint4*>(xs);
-        for (int v = tid; v < n * HC / 8; v += kInferThreads) dst4[v] = src[v];
+        trx_u4* dst4 = reinterpret_cast<trx_u4*>(xs);
+#pragma unroll
+        for (int j = 0; j < kStageBatch; ++j) {
+            const int v = tid + kInferThreads * j;
+            if (v < nq) dst4[v] = stg[j];
+        }
+        for (int v = tid + kInferThreads * kStageBatch; v < nq; v += kInferThreads) dst4[v] = xsrc[v];
     }
     __syncthreads();
+    TRX_ISTAMP(0);
 
-    // 1. layer 0: xh = bf16(bf16(x0) @ w0^T), weights of a thread's columns in registers
+    // 1. layer 0: xh = bf16(bf16(x0) @ w0^T); a thread owns 4 consecutive columns
+    //    (weights in registers) and writes them packed
     if (IN > 0) {
         constexpr int INR = IN > 0 ? IN : 1;
+        for (int q = tid; q < HC / 4; q += kInferThreads) {
+            float w[4][INR];
 #pragma unroll
-        for (int m = 0; m < KC; ++m) {
-            const int f = tid + kInferThreads * m;
-            float w[INR];
+            for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int j = 0; j < IN; ++j) w[j] = a.w0[(size_t)f * IN + j];
+                for (int j = 0; j < IN; ++j) w[r][j] = a.w0[(size_t)(4 * q + r) * IN + j];
             for (int i = 0; i < n; ++i) {
-                float acc = 0.0f;
+                float xv[INR];
 #pragma unroll
-                for (int j = 0; j < IN; ++j) acc += x0l[i * IN + j] * w[j];
-                xs[i * HC + f] = f2bf(acc);
+                for (int j = 0; j < IN; ++j) xv[j] = x0l[i * IN + j];
+                float acc[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    acc[r] = 0.0f;
+#pragma unroll
+                    for (int j = 0; j < IN; ++j) acc[r] += xv[j] * w[r][j];
+                }
+                uint2 u;
+                u.x = pk_bf16(acc[0], acc[1]);
+                u.y = pk_bf16(acc[2], acc[3]);
+                *reinterpret_cast<uint2*>(xs + i * HC + 4 * q) = u;
             }
         }
         __syncthreads();
     }
+    TRX_ISTAMP(1);
 
-    // 2. attention dot products <xh[i,h,:], att[h,:]>: every thread takes
-    //    (node, head, 64-wide segment) units, partials are combined in order
+    // 2. attention dot products <xh[i,h,:], att[h,:]>: one wave per (node, head)
+    //    pair, lane owns channels 4*lane .. 4*lane+3 (C <= 256; conflict-free LDS
+    //    reads), wave sums.  Pairs t = h*n + i in contiguous per-wave ranges.
     {
-        for (int u = tid; u < n * H * S; u += kInferThreads) {
-            const int sg = u % S, ih = u / S, i = ih / H, h = ih - (ih / H) * H;
-            const uint16_t* xr = xs + i * HC + h * C + sg * SL;
-            const float4* s_att = reinterpret_cast<const float4*>(a.att_src + h * C + sg * SL);
-            const float4* d_att = reinterpret_cast<const float4*>(a.att_dst + h * C + sg * SL);
-            float s1 = 0.0f, s2 = 0.0f;
-            for (int c = 0; c < SL; c += 8) {
-                const uint4 q = *reinterpret_cast<const uint4*>(xr + c);
-                const float4 sa0 = s_att[c / 4], sa1 = s_att[c / 4 + 1];
-                const float4 da0 = d_att[c / 4], da1 = d_att[c / 4 + 1];
-                const float v[8] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
-                                    __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u),
-                                    __uint_as_float(q.z << 16), __uint_as_float(q.z & 0xffff0000u),
-                                    __uint_as_float(q.w << 16), __uint_as_float(q.w & 0xffff0000u)};
-                const float sa[8] = {sa0.x, sa0.y, sa0.z, sa0.w, sa1.x, sa1.y, sa1.z, sa1.w};
-                const float da[8] = {da0.x, da0.y, da0.z, da0.w, da1.x, da1.y, da1.z, da1.w};
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    s1 += v[r] * sa[r];
-                    s2 += v[r] * da[r];
+        const int P = n * H, per = (P + kInferWaves - 1) / kInferWaves;
+        const int t0 = wave * per, t1 = t0 + per < P ? t0 + per : P;
+        const int c = 4 * lane;
+        const bool cok = c < C;
+        int hcur = -1;
+        float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), da = sa;
+        for (int t = t0; t < t1; ++t) {
+            const int h = t / n, i = t - h * n;
+            if (h != hcur) {
+                hcur = h;
+                if (cok) {
+                    sa = *reinterpret_cast<const float4*>(a.att_src + h * C + c);
+                    da = *reinterpret_cast<const float4*>(a.att_dst + h * C + c);
                 }
             }
-            part[2 * u] = s1;
-            part[2 * u + 1] = s2;
-        }
-        __syncthreads();
-        for (int t = tid; t < n * H; t += kInferThreads) {
             float s1 = 0.0f, s2 = 0.0f;
-            for (int sg = 0; sg < S; ++sg) {
-                s1 += part[2 * (t * S + sg)];
-                s2 += part[2 * (t * S + sg) + 1];
+            if (cok) {
+                const uint2 u = *reinterpret_cast<const uint2*>(xs + i * HC + h * C + c);
+                const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
+                const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
+                s1 = (v0 * sa.x + v1 * sa.y) + (v2 * sa.z + v3 * sa.w);
+                s2 = (v0 * da.x + v1 * da.y) + (v2 * da.z + v3 * da.w);
             }
-            as_[t] = s1;  // t = i*H + h
-            ad_[t] = s2;
-        }
-        __syncthreads();
-        for (int v = tid; v < ne * H; v += kInferThreads) {  // edge logits of this layer into al
-            const int e = v / H, h = v - e * H;
-            al[v] = a.a_edge[(size_t)(ebeg + e) * a.a_edge_stride + a.a_edge_offset + h];
+            s1 = wave_sum_f(s1);
+            s2 = wave_sum_f(s2);
+            if (lane == 0) {
+                as_[i * H + h] = s1;
+                ad_[i * H + h] = s2;
+            }
         }
     }
     __syncthreads();
+    TRX_ISTAMP(2);
+    TRX_ISTAMP(3);
 
     // 3. softmax over in-edges: one thread per (node, head), LDS only
     for (int t = tid; t < n * H; t += kInferThreads) {
@@ -203,6 +279,7 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
             al[p * H + h] = __expf(leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope) - m) / denom;
     }
     __syncthreads();
+    TRX_ISTAMP(4);
 
     // 4. aggregation + epilogue, one wave per node; lane owns chunks q = lane + 64k.
     //    Per-column constants live in registers across the wave's nodes.
@@ -299,8 +376,10 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
             }
         }
     }
+    TRX_ISTAMP(5);
     if (a.pool) {
         __syncthreads();
+        TRX_ISTAMP(6);
         for (int f = tid; f < HC; f += kInferThreads) {
             float s = 0.0f, mx = -__builtin_huge_valf();
             for (int i = 0; i < n; ++i) {
@@ -311,63 +390,138 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
             a.pool[(size_t)g * 2 * HC + f] = s / (float)n;
             a.pool[(size_t)g * 2 * HC + HC + f] = mx;
         }
+        TRX_ISTAMP(7);
     }
 }
 
 // --------------------------------------------------------- edge scorer
-// One workgroup per graph, one wave per link; lane owns hidden units
-// k = lane + 64m (hidden <= 512), whose weights stay in registers.
-template <int MK>  // hidden <= 64 * MK
+// One workgroup per graph.  The graph's p rows (n x 2H bf16, contiguous in
+// HBM), link endpoints, features and mask are staged in LDS by one batch of
+// coalesced loads (no dependent index -> row loads per link); then one wave per
+// link, lane owning 4 consecutive hidden units per 256-wide chunk (weights in
+// registers), and a wave reduction of the 256->1 product.
+constexpr int kEdgeED = 8;  // edge_dim <= 8
+
+template <int MQ>  // hidden <= 256 * MQ, hidden % 4 == 0
 __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge_head_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* lg = reinterpret_cast<float*>(smem);  // [E]
+    constexpr int ED = kEdgeED;
     const int g = blockIdx.x;
-    const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim;
+    const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-    const uint16_t* p = static_cast<const uint16_t*>(a.p);
-    constexpr int ED = 8;  // edge_dim <= 8
-    float we_r[MK][ED], w2_r[MK], c_r[MK];
+    uint16_t* pr = reinterpret_cast<uint16_t*>(smem);               // [n][2*Hd] bf16
+    float* eal = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);  // [E][ED] bf16-rounded features
+    float* lg = eal + (size_t)E * ED;                                // [E] logits
+    float* mk = lg + E;                                              // [E] mask
+    int* sl = reinterpret_cast<int*>(mk + E);                        // [E] graph-local src
+    int* dl = sl + E;                                                // [E] graph-local dst
+    int* badl = dl + E;                                              // [1] link outside the node block
+    if (tid == 0) *badl = 0;
+    __syncthreads();
+
+    // stage: the loads of a batch are all issued before its LDS stores
+    const int64_t node0 = (int64_t)g * n;
+    const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.p) + node0 * 2 * Hd);
+    trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
+    const int nq = n * 2 * Hd / 8;
+#ifndef TRX_EH_ROWS
+#define TRX_EH_ROWS 4
+#endif
+    constexpr int kRowRegs = TRX_EH_ROWS;
+    trx_u4 rows[kRowRegs];
 #pragma unroll
-    for (int m = 0; m < MK; ++m) {
-        const int k = lane + kWave * m;
-        const bool ok = k < Hd;
-        w2_r[m] = ok ? a.w2[k] : 0.0f;
-        c_r[m] = ok ? a.c[(size_t)g * Hd + k] : 0.0f;
-#pragma unroll
-        for (int j = 0; j < ED; ++j) we_r[m][j] = (ok && j < D) ? a.we[k * D + j] : 0.0f;
+    for (int j = 0; j < kRowRegs; ++j) {
+        const int v = tid + kInferThreads * j;
+        if (v < nq) rows[j] = src4[v];
     }
+    constexpr int kEaRegs = 4;
+    float eav[kEaRegs];
+#pragma unroll
+    for (int j = 0; j < kEaRegs; ++j) {
+        const int v = tid + kInferThreads * j, e = v / ED, jj = v - (v / ED) * ED;
+        eav[j] = v < E * ED && jj < D ? a.ea[((int64_t)g * E + e) * D + jj] : 0.0f;
+    }
+    int badf = 0;
+    for (int e = tid; e < E; e += kInferThreads) {
+        const int64_t eg = (int64_t)g * E + e;
+        const int64_t s = a.src[eg] - node0, d = a.dst[eg] - node0;
+        const float mv = a.softmax ? a.mask[eg] : 1.0f;
+        badf |= (s < 0) | (s >= n) | (d < 0) | (d >= n);
+        sl[e] = (int)s;
+        dl[e] = (int)d;
+        mk[e] = mv;
+    }
+#pragma unroll
+    for (int j = 0; j < kRowRegs; ++j) {
+        const int v = tid + kInferThreads * j;
+        if (v < nq) dst4[v] = rows[j];
+    }
+    for (int v = tid + kInferThreads * kRowRegs; v < nq; v += kInferThreads) dst4[v] = src4[v];
+#pragma unroll
+    for (int j = 0; j < kEaRegs; ++j) {
+        const int v = tid + kInferThreads * j;
+        if (v < E * ED) eal[v] = bf16r(eav[j]);
+    }
+    for (int v = tid + kInferThreads * kEaRegs; v < E * ED; v += kInferThreads) {
+        const int e = v / ED, j = v - (v / ED) * ED;
+        eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
+    }
+    float we_r[MQ][4][ED], w2_r[MQ][4], c_r[MQ][4];
+#pragma unroll
+    for (int m = 0; m < MQ; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = 256 * m + 4 * lane + r;
+            const bool ok = k < Hd;
+            w2_r[m][r] = ok ? a.w2[k] : 0.0f;
+            c_r[m][r] = ok ? a.c[(int64_t)g * Hd + k] : 0.0f;
+#pragma unroll
+            for (int j = 0; j < ED; ++j) we_r[m][r][j] = (ok && j < D) ? a.we[k * D + j] : 0.0f;
+        }
     const float b2 = a.b2[0];
-    constexpr int EU = 2;  // links per wave iteration: independent loads in flight together
+    if (badf) *badl = 1;
+    __syncthreads();
+    if (*badl) {  // a link leaves the graph's node block: poison, never read outside LDS
+        for (int e = tid; e < E; e += kInferThreads) {
+            a.out[(int64_t)g * E + e] = __builtin_nanf("");
+            if (a.softmax && a.logits) a.logits[(int64_t)g * E + e] = __builtin_nanf("");
+        }
+        return;
+    }
+
+    constexpr int EU = 2;  // links per wave iteration
     for (int e0 = wave * EU; e0 < E; e0 += kInferWaves * EU) {
-        float ear[EU][ED];
-        const uint16_t* ps[EU];
-        const uint16_t* pd[EU];
+        float part[EU];
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const int e = e0 + u < E ? e0 + u : E - 1;
-            const int eg = g * E + e;
+            const float4 ea0 = *reinterpret_cast<const float4*>(eal + e * ED);
+            const float4 ea1 = *reinterpret_cast<const float4*>(eal + e * ED + 4);
+            const float ear[ED] = {ea0.x, ea0.y, ea0.z, ea0.w, ea1.x, ea1.y, ea1.z, ea1.w};
+            const uint16_t* ps = pr + sl[e] * 2 * Hd;
+            const uint16_t* pd = pr + dl[e] * 2 * Hd + Hd;
+            part[u] = 0.0f;
 #pragma unroll
-            for (int j = 0; j < ED; ++j) ear[u][j] = j < D ? bf16r(a.ea[(size_t)eg * D + j]) : 0.0f;
-            ps[u] = p + (size_t)a.src[eg] * 2 * Hd;
-            pd[u] = p + (size_t)a.dst[eg] * 2 * Hd + Hd;
-        }
-        float part[EU];
+            for (int m = 0; m < MQ; ++m) {
+                const int k0 = 256 * m + 4 * lane;
+                if (k0 < Hd) {
+                    const uint2 us = *reinterpret_cast<const uint2*>(ps + k0);
+                    const uint2 ud = *reinterpret_cast<const uint2*>(pd + k0);
+                    const float psv[4] = {__uint_as_float(us.x << 16), __uint_as_float(us.x & 0xffff0000u),
+                                          __uint_as_float(us.y << 16), __uint_as_float(us.y & 0xffff0000u)};
+                    const float pdv[4] = {__uint_as_float(ud.x << 16), __uint_as_float(ud.x & 0xffff0000u),
+                                          __uint_as_float(ud.y << 16), __uint_as_float(ud.y & 0xffff0000u)};
 #pragma unroll
-        for (int u = 0; u < EU; ++u) part[u] = 0.0f;
+                    for (int r = 0; r < 4; ++r) {
+                        float ew = 0.0f;
 #pragma unroll
-        for (int m = 0; m < MK; ++m) {
-            const int k = lane + kWave * m;
-            if (k < Hd) {
-#pragma unroll
-                for (int u = 0; u < EU; ++u) {
-                    float ew = 0.0f;
-#pragma unroll
-                    for (int j = 0; j < ED; ++j)
-                        if (j < D) ew += ear[u][j] * we_r[m][j];
-                    const float z1 = bf16r(bf2f(ps[u][k]) + bf2f(pd[u][k]));
-                    const float z2 = bf16r(z1 + bf16r(ew));
-                    const float z3 = z2 + c_r[m];
-                    part[u] += bf16r(fmaxf(z3, 0.0f)) * w2_r[m];
+                        for (int j = 0; j < ED; ++j)
+                            if (j < D) ew += ear[j] * we_r[m][r][j];
+                        const float z1 = bf16r(psv[r] + pdv[r]);
+                        const float z2 = bf16r(z1 + bf16r(ew));
+                        const float z3 = z2 + c_r[m][r];
+                        part[u] += bf16r(fmaxf(z3, 0.0f)) * w2_r[m][r];
+                    }
                 }
             }
         }
@@ -379,38 +533,184 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
     }
     __syncthreads();
     if (!a.softmax) {
-        for (int e = tid; e < E; e += kInferThreads) a.out[(size_t)g * E + e] = lg[e];
+        for (int e = tid; e < E; e += kInferThreads) a.out[(int64_t)g * E + e] = lg[e];
         return;
     }
     if (wave != 0) return;
+    for (int e = lane; e < E; e += kWave) lg[e] = mk[e] <= 0.0f ? -1e9f : lg[e];  // masked logits, in place
     if (a.logits)
-        for (int e = lane; e < E; e += kWave)
-            a.logits[(size_t)g * E + e] = a.mask[(size_t)g * E + e] <= 0.0f ? -1e9f : lg[e];
+        for (int e = lane; e < E; e += kWave) a.logits[(int64_t)g * E + e] = lg[e];
     float m = -__builtin_huge_valf();
-    for (int e0 = 0; e0 < E; e0 += kWave) {
-        const int e = e0 + lane;
-        float x = -__builtin_huge_valf();
-        if (e < E) x = a.mask[(size_t)g * E + e] <= 0.0f ? -1e9f : lg[e];
-        m = fmaxf(m, wave_max_f(x));
-    }
+    for (int e0 = 0; e0 < E; e0 += kWave) m = fmaxf(m, wave_max_f(e0 + lane < E ? lg[e0 + lane] : -__builtin_huge_valf()));
     float ssum = 0.0f;
-    for (int e0 = 0; e0 < E; e0 += kWave) {
-        const int e = e0 + lane;
-        float ex = 0.0f;
-        if (e < E) ex = expf((a.mask[(size_t)g * E + e] <= 0.0f ? -1e9f : lg[e]) - m);
-        ssum += wave_sum_f(ex);
-    }
+    for (int e0 = 0; e0 < E; e0 += kWave) ssum += wave_sum_f(e0 + lane < E ? expf(lg[e0 + lane] - m) : 0.0f);
     const float denom = ssum + 1e-16f;
-    for (int e0 = 0; e0 < E; e0 += kWave) {
-        const int e = e0 + lane;
-        if (e < E) a.out[(size_t)g * E + e] = expf((a.mask[(size_t)g * E + e] <= 0.0f ? -1e9f : lg[e]) - m) / denom;
+    for (int e = lane; e < E; e += kWave) a.out[(int64_t)g * E + e] = expf(lg[e] - m) / denom;
+    if (a.u && lane == 0) {  // one categorical draw per graph (inverse CDF over the same exp terms)
+        const float target = a.u[g] * ssum;
+        float acc = 0.0f;
+        int pick = -1, last = 0;
+        for (int e = 0; e < E; ++e) {
+            const float ex = expf(lg[e] - m);
+            if (ex > 0.0f) last = e;
+            acc += ex;
+            if (pick < 0 && acc > target) pick = e;
+        }
+        a.action[g] = pick >= 0 ? pick : last;  // u * total above the serial sum: last link with mass
     }
+}
+
+// -------------------------------------------------------------- prologue
+// M rows of every layer: one wave per (layer, head, feature), lanes over channels.
+__global__ void __launch_bounds__(kWave) edge_att_weights_kernel(trx_gat_prologue_args a) {
+    const int lane = threadIdx.x, D = a.edge_dim;
+    int l = 0, oo = blockIdx.x, row0 = 0;
+    while (oo >= a.heads[l] * D) {
+        oo -= a.heads[l] * D;
+        row0 += a.heads[l];
+        ++l;
+    }
+    const int h = oo / D, j = oo - (oo / D) * D, C = a.channels[l];
+    float s = 0.0f;
+    for (int c = lane; c < C; c += kWave) s += a.lin_edge_w[l][(size_t)(h * C + c) * D + j] * a.att_edge[l][h * C + c];
+    s = wave_sum_f(s);
+    if (lane == 0) a.m_work[(row0 + h) * D + j] = s;
+}
+
+constexpr int kProMD = 8;  // node_dim, edge_dim <= 8; LDS rows padded to 8 floats
+
+// x[0..d) -> LayerNorm (biased variance, like torch); compile-time bounded loops
+__device__ __forceinline__ void layer_norm_row(float (&x)[kProMD], int d, const float* w, const float* b, float eps) {
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kProMD; ++j)
+        if (j < d) s += x[j];
+    const float mu = s / (float)d;
+    float v = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kProMD; ++j)
+        if (j < d) {
+            const float t = x[j] - mu;
+            v += t * t;
+        }
+    const float r = rsqrtf(v / (float)d + eps);
+#pragma unroll
+    for (int j = 0; j < kProMD; ++j)
+        if (j < d) x[j] = (x[j] - mu) * r * w[j] + b[j];
+}
+
+// One wave per graph: input LayerNorms, self-loop means, a_edge of every
+// layer in CSR order.  The self-loop sums walk the links in order, broadcast
+// 64 at a time with readlane (no LDS round trip per link).
+__global__ void __launch_bounds__(kWave) gat_prologue_kernel(trx_gat_prologue_args a, int A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int MD = kProMD;
+    const int g = blockIdx.x, lane = threadIdx.x;
+    const int n = a.nodes_per_graph, E = a.edges_per_graph, ND = a.node_dim, D = a.edge_dim;
+    float* ean = reinterpret_cast<float*>(smem);  // [E][8] normalised link features
+    float* lp = ean + E * MD;                     // [n][8] self-loop attrs
+    float* Ml = lp + n * MD;                      // [A][8] bf16-rounded M rows
+    int* ld = reinterpret_cast<int*>(Ml + A * MD);  // [E] graph-local dst of kept links, else -1
+    const int64_t node0 = (int64_t)g * n, link0 = (int64_t)g * E;
+    const int p0 = a.rowptr[node0], p1 = a.rowptr[node0 + n];
+    for (int v = lane; v < A * D; v += kWave) {
+        const int k = v / D, j = v - (v / D) * D;
+        Ml[k * MD + j] = bf16r(a.m_work[v]);
+    }
+    for (int l = lane; l < E; l += kWave) {
+        float x[MD];
+#pragma unroll
+        for (int j = 0; j < MD; ++j) x[j] = j < D ? a.edge_x[(link0 + l) * D + j] : 0.0f;
+        const int64_t s = a.src[link0 + l] - node0, d = a.dst[link0 + l] - node0;
+        layer_norm_row(x, D, a.edge_ln_w, a.edge_ln_b, a.edge_ln_eps);
+#pragma unroll
+        for (int j = 0; j < MD; ++j)
+            if (j < D) {
+                ean[l * MD + j] = x[j];
+                a.ea[(link0 + l) * D + j] = x[j];
+            }
+        ld[l] = (s == d || d < 0 || d >= n) ? -1 : (int)d;
+    }
+    for (int i = lane; i < n; i += kWave) {
+        float x[MD];
+#pragma unroll
+        for (int j = 0; j < MD; ++j) x[j] = j < ND ? a.node_x[(node0 + i) * ND + j] : 0.0f;
+        layer_norm_row(x, ND, a.node_ln_w, a.node_ln_b, a.node_ln_eps);
+#pragma unroll
+        for (int j = 0; j < MD; ++j)
+            if (j < ND) a.x0[(node0 + i) * ND + j] = x[j];
+    }
+    __syncthreads();
+    {  // self-loop attr of node i = lane: mean over kept in-links, in link order (n <= 64)
+        float s[MD];
+#pragma unroll
+        for (int j = 0; j < MD; ++j) s[j] = 0.0f;
+        int cnt = 0;
+        for (int c0 = 0; c0 < E; c0 += kWave) {
+            const int l = c0 + lane;
+            const int myd = l < E ? ld[l] : -1;
+            float myv[MD];
+#pragma unroll
+            for (int j = 0; j < MD; ++j) myv[j] = (l < E && j < D) ? ean[l * MD + j] : 0.0f;
+            const int lim = E - c0 < kWave ? E - c0 : kWave;
+            for (int k = 0; k < lim; ++k) {
+                const bool hit = __builtin_amdgcn_readlane(myd, k) == lane;
+                cnt += hit;
+#pragma unroll
+                for (int j = 0; j < MD; ++j) {
+                    const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(myv[j]), k));
+                    if (hit && j < D) s[j] += v;
+                }
+            }
+        }
+        if (lane < n) {
+            const float deg = cnt > 0 ? (float)cnt : 1.0f;
+#pragma unroll
+            for (int j = 0; j < MD; ++j)
+                if (j < D) lp[lane * MD + j] = s[j] / deg;
+        }
+    }
+    __syncthreads();
+    for (int p = p0 + lane; p < p1; p += kWave) {
+        const int code = a.pos_src[p];
+        const int64_t li = (int64_t)code - link0, ni = -(int64_t)code - 1 - node0;
+        const bool ok = code >= 0 ? (li >= 0 && li < E) : (ni >= 0 && ni < n);
+        const float* fr = code >= 0 ? ean + (ok ? li : 0) * MD : lp + (ok ? ni : 0) * MD;
+        float f[MD];
+#pragma unroll
+        for (int j = 0; j < MD; ++j) f[j] = j < D ? bf16r(fr[j]) : 0.0f;
+        for (int k = 0; k < A; ++k) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < MD; ++j)
+                if (j < D) acc += f[j] * Ml[k * MD + j];
+            a.a_edge[(size_t)p * A + k] = ok ? bf16r(acc) : __builtin_nanf("");
+        }
+    }
+}
+
+size_t gat_prologue_smem(const trx_gat_prologue_args& a) {
+    int A = 0;
+    for (int l = 0; l < a.num_layers; ++l) A += a.heads[l];
+    return ((size_t)a.edges_per_graph * kProMD + (size_t)a.nodes_per_graph * kProMD + (size_t)A * kProMD +
+            a.edges_per_graph) * 4;
+}
+
+hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t stream) {
+    int A = 0;
+    for (int l = 0; l < a.num_layers; ++l) A += a.heads[l];
+    hipLaunchKernelGGL(edge_att_weights_kernel, dim3(A * a.edge_dim), dim3(kWave), 0, stream, a);
+    hipLaunchKernelGGL(gat_prologue_kernel, dim3(a.num_graphs), dim3(kWave), gat_prologue_smem(a), stream, a, A);
+    return hipGetLastError();
+}
+
+size_t edge_head_infer_smem(const trx_edge_head_args& a) {
+    return (size_t)a.nodes_per_graph * 2 * a.hidden * 2 + (size_t)a.edges_per_graph * (kEdgeED * 4 + 4 * 4) + 4;
 }
 
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a) {
     const int HC = a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
-    const int SL = a.channels < 64 ? a.channels : 64, S = a.channels / SL;
-    const size_t alsz = (size_t)me * H > 2 * (size_t)n * H * S ? (size_t)me * H : 2 * (size_t)n * H * S;
+    const size_t alsz = (size_t)me * H;
     size_t b = (size_t)n * HC * 2 + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 + (size_t)(n + 1) * 4 +
                (size_t)n * a.in_dim * 4;
     if (a.pool) b += (size_t)n * HC * 4;
@@ -453,11 +753,17 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 }
 
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream) {
-    const size_t smem = (size_t)a.edges_per_graph * sizeof(float);
+    const size_t smem = edge_head_infer_smem(a);
+    const void* fn = a.hidden <= 256 ? reinterpret_cast<const void*>(edge_head_infer_kernel<1>)
+                                     : reinterpret_cast<const void*>(edge_head_infer_kernel<2>);
+    if (smem > 64 * 1024) {  // opt in to more than 64 KB of dynamic LDS
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
     if (a.hidden <= 256)
-        hipLaunchKernelGGL(edge_head_infer_kernel<4>, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
+        hipLaunchKernelGGL(edge_head_infer_kernel<1>, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
     else
-        hipLaunchKernelGGL(edge_head_infer_kernel<8>, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
+        hipLaunchKernelGGL(edge_head_infer_kernel<2>, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
     return hipGetLastError();
 }
 

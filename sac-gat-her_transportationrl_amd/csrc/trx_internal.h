@@ -143,6 +143,9 @@ hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, cons
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a);
 hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream);
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
+size_t edge_head_infer_smem(const trx_edge_head_args& a);
+hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t stream);
+size_t gat_prologue_smem(const trx_gat_prologue_args& a);
 hipError_t patch_graph_memsets(hipGraph_t graph, int* n_patched);
 hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* pri, int n,
                              hipStream_t stream);

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 2
+ABI_VERSION = 3
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
 # Every symbol include/trafficrl.h declares (tests check the export table).
@@ -23,7 +23,7 @@ EXPORTS = (
     "trx_abi_version", "trx_last_error", "trx_graph_create", "trx_graph_destroy", "trx_graph_info",
     "trx_workspace_bytes", "trx_gp_state_bytes", "trx_assign", "trx_reset", "trx_step", "trx_observe", "trx_gat_forward",
     "trx_gat_backward", "trx_per_update", "trx_per_sample", "trx_graph_patch_memsets", "trx_gat_layer_infer",
-    "trx_edge_head_infer",
+    "trx_edge_head_infer", "trx_gat_prologue_infer",
 )
 
 
@@ -88,6 +88,24 @@ class TrxEdgeHeadArgs(ctypes.Structure):
         ("num_graphs", _i32), ("edges_per_graph", _i32), ("hidden", _i32), ("edge_dim", _i32),
         ("src", _vp), ("dst", _vp), ("p", _vp), ("c", _vp), ("ea", _vp), ("we", _vp), ("w2", _vp),
         ("b2", _vp), ("mask", _vp), ("softmax", _i32), ("out", _vp), ("logits", _vp),
+        ("nodes_per_graph", _i32), ("u", _vp), ("action", _vp),
+    ]
+
+
+MAX_GAT_LAYERS = 4
+
+
+class TrxGatPrologueArgs(ctypes.Structure):
+    """trx_gat_prologue_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("nodes_per_graph", _i32), ("edges_per_graph", _i32), ("node_dim", _i32),
+        ("edge_dim", _i32), ("node_x", _vp), ("edge_x", _vp),
+        ("node_ln_w", _vp), ("node_ln_b", _vp), ("node_ln_eps", _f32),
+        ("edge_ln_w", _vp), ("edge_ln_b", _vp), ("edge_ln_eps", _f32),
+        ("src", _vp), ("dst", _vp), ("rowptr", _vp), ("pos_src", _vp),
+        ("num_layers", _i32), ("heads", _i32 * MAX_GAT_LAYERS), ("channels", _i32 * MAX_GAT_LAYERS),
+        ("lin_edge_w", _vp * MAX_GAT_LAYERS), ("att_edge", _vp * MAX_GAT_LAYERS),
+        ("m_work", _vp), ("x0", _vp), ("ea", _vp), ("a_edge", _vp),
     ]
 
 
@@ -131,9 +149,10 @@ def load():
     L.trx_graph_patch_memsets.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32)]
     L.trx_gat_layer_infer.argtypes = [ctypes.POINTER(TrxGatLayerArgs), _vp]
     L.trx_edge_head_infer.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp]
+    L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
     for name in ("trx_graph_create", "trx_graph_destroy", "trx_graph_info", "trx_assign", "trx_reset", "trx_step",
                  "trx_observe", "trx_gat_forward", "trx_gat_backward", "trx_per_update", "trx_per_sample",
-                 "trx_graph_patch_memsets", "trx_gat_layer_infer", "trx_edge_head_infer"):
+                 "trx_graph_patch_memsets", "trx_gat_layer_infer", "trx_edge_head_infer", "trx_gat_prologue_infer"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

@@ -39,6 +39,7 @@ class Topology:
     max_graph_edges: int    # CSR positions per graph (self loops included)
     src32: torch.Tensor
     dst32: torch.Tensor
+    pos_src: torch.Tensor   # [Et] int32 per CSR position: input link id, or -(node+1) for a self loop
 
 
 _topo_cache: Dict[Tuple, Optional[Topology]] = {}
@@ -63,7 +64,14 @@ def topology(edge_index: torch.Tensor, batch: torch.Tensor, B: int) -> Optional[
             per = g.rowptr.view(-1)[:: n].diff() if N else g.rowptr
             mx = int(per.max()) if per.numel() else 0
             if 0 < mx <= 256:
-                topo = Topology(B, n, e, g, mx, src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous())
+                perm = g.perm.long()
+                ek = g.dst_kept.numel()
+                link = perm.clamp(max=max(ek - 1, 0))
+                if g.kept_idx is not None and ek:
+                    link = g.kept_idx[link]
+                pos = torch.where(perm < ek, link, -(perm - ek) - 1).to(torch.int32).contiguous()
+                topo = Topology(B, n, e, g, mx, src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous(),
+                                pos)
     if len(_topo_cache) > 64:
         _topo_cache.clear()
     _topo_cache[key] = topo
@@ -72,6 +80,12 @@ def topology(edge_index: torch.Tensor, batch: torch.Tensor, B: int) -> Optional[
 
 def autocast_bf16() -> bool:
     return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+def head_supported(head) -> bool:
+    """trx_edge_head_infer limits: hidden 4..512 in steps of 4, edge_dim <= 8."""
+    hid = head.edge_mlp[0].weight.shape[0]
+    return hid % 4 == 0 and 4 <= hid <= 512 and 1 <= head.edge_in <= 8
 
 
 def encoder_supported(enc: GATEncoder) -> bool:
@@ -94,26 +108,77 @@ def _bf16r(t: torch.Tensor) -> torch.Tensor:
     return t.detach().to(torch.bfloat16).float().contiguous()
 
 
-def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology):
+def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology):
+    """Actor/Critic input LayerNorms + every encoder layer's edge logits in
+    CSR order (trx_gat_prologue_infer: one small kernel for the M rows, one
+    wave per graph for the rest).  Returns (x0, ea, a_all)."""
+    L = _lib.load()
+    layers = list(model.encoder.layers)
+    dev = node_x.device
+    nx, ex = node_x.float().contiguous(), edge_attr.float().contiguous()
+    nd, ed = nx.shape[1], ex.shape[1]
+    A = sum(l.heads for l in layers)
+    x0 = torch.empty(nx.shape[0], nd, device=dev)
+    ea = torch.empty(ex.shape[0], ed, device=dev)
+    a_all = torch.empty(topo.g.col.numel(), A, device=dev)
+    m_work = torch.empty(A, ed, device=dev)
+    keep = [m_work]
+    a = _lib.TrxGatPrologueArgs()
+    a.num_graphs, a.nodes_per_graph, a.edges_per_graph, a.node_dim, a.edge_dim = topo.B, topo.n, topo.e, nd, ed
+    a.node_x, a.edge_x = nx.data_ptr(), ex.data_ptr()
+    for pre, ln in (("node", model.node_norm), ("edge", model.edge_norm)):
+        w, b = ln.weight.detach().float().contiguous(), ln.bias.detach().float().contiguous()
+        keep += [w, b]
+        setattr(a, pre + "_ln_w", w.data_ptr())
+        setattr(a, pre + "_ln_b", b.data_ptr())
+        setattr(a, pre + "_ln_eps", float(ln.eps))
+    a.src, a.dst, a.rowptr, a.pos_src = (topo.src32.data_ptr(), topo.dst32.data_ptr(), topo.g.rowptr.data_ptr(),
+                                         topo.pos_src.data_ptr())
+    a.num_layers = len(layers)
+    for i, l in enumerate(layers):
+        w = l.lin_edge.weight.detach().float().contiguous()
+        at = l.att_edge.detach().float().contiguous()
+        keep += [w, at]
+        a.heads[i], a.channels[i] = l.heads, l.out_channels
+        a.lin_edge_w[i], a.att_edge[i] = w.data_ptr(), at.data_ptr()
+    a.m_work, a.x0, a.ea, a.a_edge = m_work.data_ptr(), x0.data_ptr(), ea.data_ptr(), a_all.data_ptr()
+    _lib.check(L.trx_gat_prologue_infer(a, _lib.stream_ptr(dev)), "trx_gat_prologue_infer")
+    del keep
+    return x0, ea, a_all
+
+
+def prologue_supported(model) -> bool:
+    layers = list(model.encoder.layers)
+    return (len(layers) <= _lib.MAX_GAT_LAYERS and sum(l.heads for l in layers) <= 32
+            and model.node_norm.weight.numel() <= 8 and model.edge_norm.weight.numel() <= 8
+            and model.node_norm.weight is not None and model.edge_norm.weight is not None)
+
+
+def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology,
+                  a_edge: Optional[torch.Tensor] = None):
     """GATEncoder.forward (gat_encoder.py) for a regular batch, no grad, bf16
-    autocast semantics.  Returns (node_emb bf16 [N, out], global ctx fp32
-    [B, 2*out])."""
+    autocast semantics.  `a_edge`: every layer's edge logits in CSR order
+    from `prologue` (else computed here with torch ops).  Returns (node_emb
+    bf16 [N, out], global ctx fp32 [B, 2*out])."""
     L = _lib.load()
     g = topo.g
     dev = x.device
     N = x.shape[0]
     layers = list(enc.layers)
     x = x.float().contiguous()
-    ea = edge_attr if g.kept_idx is None else edge_attr.index_select(0, g.kept_idx)
-    ea = ea.float()
-    full = torch.cat([ea, _LoopMean.apply(ea, g)], 0)
-    Ms = [(l.lin_edge.weight.view(l.heads, l.out_channels, -1).float() * l.att_edge.view(l.heads, l.out_channels, 1)
-           .float()).sum(1) for l in layers]
     offs = [0]
-    for M in Ms:
-        offs.append(offs[-1] + M.shape[0])
-    a_all = (full @ torch.cat(Ms, 0).t())            # bf16 under autocast, like GATConv's a_edge
-    a_all = a_all[g.perm].float().contiguous()        # CSR order
+    for l in layers:
+        offs.append(offs[-1] + l.heads)
+    if a_edge is None:
+        ea = edge_attr if g.kept_idx is None else edge_attr.index_select(0, g.kept_idx)
+        ea = ea.float()
+        full = torch.cat([ea, _LoopMean.apply(ea, g)], 0)
+        Ms = [(l.lin_edge.weight.view(l.heads, l.out_channels, -1).float()
+               * l.att_edge.view(l.heads, l.out_channels, 1).float()).sum(1) for l in layers]
+        a_all = (full @ torch.cat(Ms, 0).t())            # bf16 under autocast, like GATConv's a_edge
+        a_all = a_all[g.perm].float().contiguous()        # CSR order
+    else:
+        a_all = a_edge
     stride = a_all.shape[1]
     stream = _lib.stream_ptr(dev)
     prev_f32, prev_bf16 = None, None
@@ -168,7 +233,7 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
 
 
 def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: torch.Tensor, topo: Topology,
-                    mask: Optional[torch.Tensor] = None):
+                    mask: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None):
     """_EdgeHead.edge_scores (+ the Actor's mask and per-graph softmax when
     `mask` is given).  Returns logits (Critic) or (masked logits, probs)."""
     L = _lib.load()
@@ -189,13 +254,21 @@ def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: 
     m = mask.float().contiguous() if mask is not None else None
     args = _lib.TrxEdgeHeadArgs()
     args.num_graphs, args.edges_per_graph, args.hidden, args.edge_dim = topo.B, topo.e, hid, k
+    args.nodes_per_graph = topo.n
     args.src, args.dst, args.p, args.c = topo.src32.data_ptr(), topo.dst32.data_ptr(), p.data_ptr(), c.data_ptr()
     args.ea, args.we, args.w2, args.b2 = ea.data_ptr(), we.data_ptr(), w2.data_ptr(), b2.data_ptr()
     args.mask = 0 if m is None else m.data_ptr()
     args.softmax = 1 if mask is not None else 0
     args.out = out.data_ptr()
     args.logits = 0 if logits is None else logits.data_ptr()
+    action = None
+    if u is not None:
+        uu = u.float().contiguous()
+        action = torch.empty(topo.B, device=dev, dtype=torch.int64)
+        args.u, args.action = uu.data_ptr(), action.data_ptr()
     _lib.check(L.trx_edge_head_infer(args, _lib.stream_ptr(dev)), "trx_edge_head_infer")
     if mask is None:
         return out
+    if u is not None:
+        return logits, out, action
     return logits, out

@@ -157,11 +157,11 @@ def clip_grad_norm_listwise_(params, max_norm: float):
 FUSED_INFERENCE = True   # module switch (tests compare both paths)
 
 
-def _fused_topology(encoder, node_x, edge_index, batch, B):
+def _fused_topology(encoder, node_x, edge_index, batch, B, head=None):
     """Topology for the fused inference kernels, or None -> general path.
     Taken only without autograd, under bf16 autocast, on the GPU."""
     if (not FUSED_INFERENCE or torch.is_grad_enabled() or not node_x.is_cuda or not fused.autocast_bf16()
-            or not fused.encoder_supported(encoder)):
+            or not fused.encoder_supported(encoder) or (head is not None and not fused.head_supported(head))):
         return None
     return fused.topology(edge_index, batch, B)
 
@@ -173,6 +173,18 @@ class _EdgeHead(nn.Module):
         super().__init__()
         self.embed, self.edge_in = embed, edge_in
         self.edge_mlp = nn.Sequential(nn.Linear(embed * 4 + edge_in, hidden), nn.ReLU(), nn.Linear(hidden, 1))
+
+    def _fused(self, node_x, edge_index, edge_attr, batch, B, mask=None, u=None):
+        """Fused inference (models/fused.py) from the raw features: prologue
+        (input LayerNorms + edge logits), one kernel per GAT layer, edge head
+        (+ masked softmax, + one draw per graph when u is given).  None when
+        the general path must run."""
+        topo = _fused_topology(self.encoder, node_x, edge_index, batch, B, self)
+        if topo is None or not fused.prologue_supported(self):
+            return None
+        x0, ea, a_all = fused.prologue(self, node_x, edge_attr, topo)
+        emb, ctx = fused.encoder_infer(self.encoder, x0, ea, topo, a_edge=a_all)
+        return fused.edge_head_infer(self, emb, ctx, ea, topo, mask=mask, u=u)
 
     def edge_scores(self, node_emb, global_ctx, edge_attr, src, dst, edge_batch, regular=None):
         """regular = (B, src_local, dst_local) for fixed-topology batches: the
@@ -205,14 +217,14 @@ class Actor(_EdgeHead):
 
     def forward(self, node_x, edge_index, edge_attr, action_mask, batch, return_attention: bool = False,
                 num_graphs: Optional[int] = None):
+        B = num_graphs if num_graphs is not None else int(batch.max()) + 1
+        if not return_attention:
+            out = self._fused(node_x, edge_index, edge_attr, batch, B, mask=action_mask)
+            if out is not None:
+                logits, probs = out
+                return logits, probs, None
         node_x = input_layer_norm(self.node_norm, node_x)
         edge_attr = input_layer_norm(self.edge_norm, edge_attr)
-        B = num_graphs if num_graphs is not None else int(batch.max()) + 1
-        topo = _fused_topology(self.encoder, node_x, edge_index, batch, B) if not return_attention else None
-        if topo is not None:
-            emb, ctx = fused.encoder_infer(self.encoder, node_x, edge_attr, topo)
-            logits, probs = fused.edge_head_infer(self, emb, ctx, edge_attr, topo, mask=action_mask)
-            return logits, probs, None
         node_emb, global_ctx, attn = self.encoder(node_x, edge_index, edge_attr, batch,
                                                   return_attention=return_attention, num_graphs=B)
         src, dst = edge_index
@@ -235,13 +247,12 @@ class Critic(_EdgeHead):
                                                                       num_layers=num_layers)
 
     def forward(self, node_x, edge_index, edge_attr, batch, num_graphs: Optional[int] = None):
+        B = num_graphs if num_graphs is not None else int(batch.max()) + 1
+        out = self._fused(node_x, edge_index, edge_attr, batch, B)
+        if out is not None:
+            return out
         node_x = input_layer_norm(self.node_norm, node_x)
         edge_attr = input_layer_norm(self.edge_norm, edge_attr)
-        B = num_graphs if num_graphs is not None else int(batch.max()) + 1
-        topo = _fused_topology(self.encoder, node_x, edge_index, batch, B)
-        if topo is not None:
-            emb, ctx = fused.encoder_infer(self.encoder, node_x, edge_attr, topo)
-            return fused.edge_head_infer(self, emb, ctx, edge_attr, topo)
         node_emb, global_ctx, _ = self.encoder(node_x, edge_index, edge_attr, batch, num_graphs=B)
         src, dst = edge_index
         return self.edge_scores(node_emb, global_ctx, edge_attr, src, dst, batch[src],
@@ -330,6 +341,11 @@ class DiscreteSAC:
         """Batched acting for B graphs with identical link counts (VecRepairEnv):
         one actor forward, one multinomial draw per graph, no host sync."""
         with torch.no_grad(), self._amp():
+            if not deterministic:  # fused path: the draw happens inside the edge-head kernel
+                u = torch.rand(num_graphs, device=node_x.device, generator=generator)
+                out = self.actor._fused(node_x, edge_index, edge_attr, batch, num_graphs, mask=action_mask, u=u)
+                if out is not None:
+                    return out[2]
             _, probs, _ = self.actor(node_x, edge_index, edge_attr, action_mask, batch, num_graphs=num_graphs)
         p = probs.view(num_graphs, -1)
         if deterministic:

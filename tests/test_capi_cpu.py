@@ -35,7 +35,7 @@ def test_exports_every_declared_symbol():
     assert set(syms) == set(_lib.EXPORTS)
     for s in syms:
         assert hasattr(L, s), s
-    assert L.trx_abi_version() == 2
+    assert L.trx_abi_version() == 3
 
 
 def test_struct_layout_matches_header(tmp_path):
@@ -106,7 +106,9 @@ def test_fused_args_layout_matches_header(tmp_path):
     compiler lays them out equals the ctypes mirror in trafficrl/_lib.py."""
     from trafficrl import _lib
     lines = []
-    for cname, cls in (("trx_gat_layer_args", _lib.TrxGatLayerArgs), ("trx_edge_head_args", _lib.TrxEdgeHeadArgs)):
+    structs = (("trx_gat_layer_args", _lib.TrxGatLayerArgs), ("trx_edge_head_args", _lib.TrxEdgeHeadArgs),
+               ("trx_gat_prologue_args", _lib.TrxGatPrologueArgs))
+    for cname, cls in structs:
         lines.append(f'printf("%zu\\n", sizeof({cname}));')
         for f, _ in cls._fields_:
             lines.append(f'printf("%zu\\n", offsetof({cname}, {f}));')
@@ -117,7 +119,7 @@ def test_fused_args_layout_matches_header(tmp_path):
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
     vals = list(map(int, subprocess.check_output([str(exe)]).split()))
     want = []
-    for cls in (_lib.TrxGatLayerArgs, _lib.TrxEdgeHeadArgs):
+    for _, cls in structs:
         want.append(ctypes.sizeof(cls))
         want += [getattr(cls, f).offset for f, _ in cls._fields_]
     assert vals == want
@@ -137,3 +139,13 @@ def test_fused_infer_validation_without_gpu():
     h = _lib.TrxEdgeHeadArgs()
     h.num_graphs, h.edges_per_graph, h.hidden, h.edge_dim = 4, 76, 256, 32
     assert L.trx_edge_head_infer(h, None) == -3
+    pa = _lib.TrxGatPrologueArgs()
+    pa.num_graphs, pa.nodes_per_graph, pa.edges_per_graph, pa.node_dim, pa.edge_dim = 4, 24, 76, 4, 6
+    pa.num_layers = 5
+    assert L.trx_gat_prologue_infer(pa, None) == -3
+    assert b"num_layers" in L.trx_last_error()
+    pa.num_layers, pa.heads[0], pa.channels[0] = 1, 4, 256
+    assert L.trx_gat_prologue_infer(pa, None) == -1    # NULL weights
+    h.edge_dim, h.nodes_per_graph = 6, 200             # p rows of one graph would not fit in LDS
+    assert L.trx_edge_head_infer(h, None) == -3
+    assert b"nodes_per_graph" in L.trx_last_error()

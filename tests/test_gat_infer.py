@@ -116,3 +116,59 @@ def test_irregular_batch_takes_general_path():
     assert torch.isfinite(probs).all()
     sums = torch.zeros(len(sizes), device="cuda").index_add_(0, bv[ei[0]], probs)
     torch.testing.assert_close(sums, torch.ones(len(sizes), device="cuda"), atol=1e-5, rtol=0)
+
+
+def test_prologue_matches_torch_ops():
+    """trx_gat_prologue_infer (input LayerNorms, self-loop means, every
+    layer's a_edge in CSR order) against the same quantities from torch ops:
+    LayerNorm outputs to fp32 rounding, a_edge to one bf16 ulp (the 6-term
+    dot products are summed in another order before the bf16 rounding)."""
+    from trafficrl.models import fused
+    from trafficrl.models.gat_encoder import _LoopMean
+    from trafficrl.rl.sac import Actor, input_layer_norm
+    torch.manual_seed(5)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=3)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        topo = fused.topology(ei, bv, B)
+        x0, ean, a_all = fused.prologue(actor, node_x, ea, topo)
+        x_ref = input_layer_norm(actor.node_norm, node_x)
+        e_ref = input_layer_norm(actor.edge_norm, ea)
+        g = topo.g
+        full = torch.cat([e_ref, _LoopMean.apply(e_ref, g)], 0)
+        Ms = [(l.lin_edge.weight.view(l.heads, l.out_channels, -1) * l.att_edge.view(l.heads, l.out_channels, 1))
+              .sum(1) for l in actor.encoder.layers]
+        a_ref = (full @ torch.cat(Ms, 0).t())[g.perm].float()
+    torch.testing.assert_close(x0, x_ref.float(), atol=2e-6, rtol=2e-6)
+    torch.testing.assert_close(ean, e_ref.float(), atol=2e-6, rtol=2e-6)
+    assert a_all.shape == a_ref.shape
+    torch.testing.assert_close(a_all, a_ref, atol=1e-3, rtol=1.6e-2)
+
+
+def test_fused_draw_is_inverse_cdf_of_probs():
+    """select_actions' in-kernel categorical draw: for each graph and uniform
+    u the action is the first link whose cumulative probability exceeds u
+    (checked in float64, skipping u within 1e-5 of a boundary), masked links
+    are never drawn, and the action frequencies over many draws follow the
+    probabilities."""
+    from trafficrl.models import fused
+    from trafficrl.rl.sac import Actor
+    torch.manual_seed(6)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=5)
+    gen = torch.Generator(device="cuda").manual_seed(2)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        counts = torch.zeros(B, E, device="cuda", dtype=torch.float64)
+        for _ in range(200):
+            u = torch.rand(B, device="cuda", generator=gen)
+            logits, probs, act = actor._fused(node_x, ei, ea, bv, B, mask=mask, u=u)
+            cdf = probs.view(B, E).double().cumsum(1)
+            want = (cdf <= u.double()[:, None]).sum(1).clamp(max=E - 1)
+            near = ((cdf - u.double()[:, None]).abs() < 1e-5).any(1)
+            assert torch.equal(act[~near], want[~near])
+            assert bool((mask.view(B, E).gather(1, act[:, None]) > 0).all())
+            counts[torch.arange(B, device="cuda"), act] += 1
+    freq = counts / 200
+    p = probs.view(B, E).double()
+    # binomial standard error at n=200 is <= 0.036; 5 sigma
+    assert (freq - p).abs().max().item() < 0.18

@@ -15,6 +15,9 @@ sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
 def main():
     from torch.profiler import ProfilerActivity, profile
 
+    if os.environ.get("TRX_LIB"):   # A/B a second build of libtrafficrl.so
+        from trafficrl import _lib
+        _lib.LIB_PATH = os.path.abspath(os.environ["TRX_LIB"])
     from trafficrl.train import Trainer, load_config
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     cfg = load_config(None)
