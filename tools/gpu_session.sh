@@ -33,6 +33,8 @@ for s in "$@"; do
         epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --workload env --steps 44 --warmup 22 --no-cpu; done ;;
         gattests) step gat_tests 400 python -m pytest tests/test_gat_infer.py tests/test_gat.py tests/test_sac.py -x -q ;;
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
+        upd) step upd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/upd -o run --output-format csv -- python3 tools/agent_profile.py 4096 update ;;
+        overlap) step overlap 300 python tools/overlap_probe.py 4096 ;;
         istamps) step istamps 300 python tools/infer_stamps.py 4096 ;;
         abact) TRX_LIB=${TRX_LIB_A:-} step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act
                TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
