@@ -228,7 +228,9 @@ class GATConv(nn.Module):
         if self.att_edge is not None:
             _glorot_(self.att_edge)
 
-    def forward(self, x, edge_index, edge_attr=None, return_attention_weights=None):
+    def forward(self, x, edge_index, edge_attr=None, return_attention_weights=None, a_edge_csr=None):
+        """a_edge_csr: this layer's edge logits [Et, H] already in CSR order
+        (GATEncoder computes every layer's in one product); else computed here."""
         H, C = self.heads, self.out_channels
         N = x.size(0)
         g = build_csr(edge_index, N)
@@ -245,7 +247,9 @@ class GATConv(nn.Module):
         with torch.autocast("cuda", enabled=False):
             a_sd = skinny_linear(xh.float(), A.t())        # [N, 2H]
         a_src, a_dst = a_sd[:, :H], a_sd[:, H:]
-        if self.lin_edge is not None and edge_attr is not None:
+        if a_edge_csr is not None:
+            a_edge = None
+        elif self.lin_edge is not None and edge_attr is not None:
             ea = (edge_attr if g.kept_idx is None else edge_attr.index_select(0, g.kept_idx)).float()
             # fill_value='mean': loop attr = mean of the node's incoming edge attrs
             loop = _LoopMean.apply(ea, g)
@@ -254,8 +258,9 @@ class GATConv(nn.Module):
             a_edge = skinny_linear(full, M)                # [Et, H]
         else:
             a_edge = torch.zeros(g.src_all.numel(), H, device=x.device)
-        out, alpha = gat_aggregate(xh, a_src, a_dst, perm_gather(a_edge, g.perm, g.inv_perm), g, H, C,
-                                   self.negative_slope)
+        if a_edge_csr is None:
+            a_edge_csr = perm_gather(a_edge, g.perm, g.inv_perm)
+        out, alpha = gat_aggregate(xh, a_src, a_dst, a_edge_csr, g, H, C, self.negative_slope)
         if not self.concat:
             out = out.view(N, H, C).mean(1)
         if self.bias is not None:
@@ -324,19 +329,35 @@ class GATEncoder(nn.Module):
         for i in range(self.num_layers):
             self.norms.append(nn.LayerNorm(out_dim if i == self.num_layers - 1 else hidden_dim * heads))
 
+    def edge_logits(self, edge_index, edge_attr, num_nodes: int):
+        """Every layer's a_edge in CSR order, as one product: the self-loop
+        mean attrs, the cast and the skinny GEMM happen once per forward
+        instead of once per layer.  Column block l holds layer l's heads."""
+        g = build_csr(edge_index, num_nodes)
+        ea = (edge_attr if g.kept_idx is None else edge_attr.index_select(0, g.kept_idx)).float()
+        full = torch.cat([ea, _LoopMean.apply(ea, g)], 0)
+        M = torch.cat([(l.lin_edge.weight.view(l.heads, l.out_channels, -1).float()
+                        * l.att_edge.view(l.heads, l.out_channels, 1).float()).sum(1) for l in self.layers], 0)
+        return perm_gather(skinny_linear(full, M), g.perm, g.inv_perm)
+
     def forward(self, x, edge_index, edge_attr, batch, return_attention: bool = False,
                 num_graphs: Optional[int] = None):
         attn = None
+        shared = edge_attr is not None and all(l.lin_edge is not None for l in self.layers)
+        a_all = self.edge_logits(edge_index, edge_attr, x.size(0)) if shared else None
+        off = 0
         for i, layer in enumerate(self.layers):
             last = i == len(self.layers) - 1
+            ae = a_all[:, off:off + layer.heads] if shared else None
+            off += layer.heads
             if last and return_attention:
-                x, attn_info = layer(x, edge_index, edge_attr=edge_attr, return_attention_weights=True)
+                x, attn_info = layer(x, edge_index, edge_attr=edge_attr, return_attention_weights=True, a_edge_csr=ae)
                 attn = attn_info[1]
             elif last:
-                x = layer(x, edge_index, edge_attr=edge_attr)
+                x = layer(x, edge_index, edge_attr=edge_attr, a_edge_csr=ae)
             else:
                 x_in = x
-                x = layer(x, edge_index, edge_attr=edge_attr)
+                x = layer(x, edge_index, edge_attr=edge_attr, a_edge_csr=ae)
                 if i == 0:
                     ip = self.input_proj
                     x_in = (skinny_linear(x_in, ip.weight, ip.bias) if ip.in_features <= _SKINNY_IN

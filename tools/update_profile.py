@@ -30,10 +30,21 @@ def main():
         u, her_u = tr._draw_update_randoms()
         tr._update_once(u, her_u)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    copies = len(sys.argv) > 2 and sys.argv[2] == "copies"
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                 with_stack=copies) as prof:
         u, her_u = tr._draw_update_randoms()
         tr._update_once(u, her_u)
         torch.cuda.synchronize()
+    if copies:  # dtype conversions attributed to the trafficrl source line that issued them
+        ka = prof.key_averages(group_by_input_shape=True, group_by_stack_n=6)
+        evs = [e for e in ka if e.key in ("aten::_to_copy", "aten::copy_") and e.device_time_total > 0]
+        evs.sort(key=lambda e: -e.device_time_total)
+        for e in evs[:rows]:
+            stack = [f for f in (e.stack or []) if "trafficrl" in f][:2]
+            print(f"{e.device_time_total / 1e3:7.3f} ms x{e.count:<3d} {e.key:15s} {str(e.input_shapes)[:60]:60s} "
+                  f"{' <- '.join(x.split('/')[-1] for x in stack)}")
+        return
     ka = prof.key_averages(group_by_input_shape=True)
     evs = [e for e in ka if not e.key.startswith(("autograd::", "Cijk", "void ", "trx::", "Custom_", "__amd"))]
     evs.sort(key=lambda e: -e.device_time_total)
