@@ -32,18 +32,32 @@ constexpr int kGatWaves = 4;         // waves (nodes) per workgroup
 constexpr int kMaxChunks = 8;        // float4 chunks per lane: H*C <= 64*4*8 = 2048
 constexpr int kMaxDegCache = 64;     // in-edges whose alphas are cached in LDS
 
+// Wave reductions on DPP row ops + readlane (no LDS round trips, unlike
+// ds_bpermute shuffles): every lane gets the (uniform) result.
+#define TRX_DPPS(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false))
+#define TRX_DPPM(v, ctrl) \
+    __int_as_float(__builtin_amdgcn_update_dpp((int)0xff800000, __float_as_int(v), ctrl, 0xf, 0xf, false))
+#define TRX_RL(v, l) __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l))
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-    return v;
+    v = fmaxf(v, TRX_DPPM(v, 0xB1));   // quad_perm [1,0,3,2]
+    v = fmaxf(v, TRX_DPPM(v, 0x4E));   // quad_perm [2,3,0,1]
+    v = fmaxf(v, TRX_DPPM(v, 0x141));  // row_half_mirror
+    v = fmaxf(v, TRX_DPPM(v, 0x140));  // row_mirror
+    return fmaxf(fmaxf(TRX_RL(v, 0), TRX_RL(v, 16)), fmaxf(TRX_RL(v, 32), TRX_RL(v, 48)));
 }
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+    v = v + TRX_DPPS(v, 0xB1);
+    v = v + TRX_DPPS(v, 0x4E);
+    v = v + TRX_DPPS(v, 0x141);
+    v = v + TRX_DPPS(v, 0x140);
+    return (TRX_RL(v, 0) + TRX_RL(v, 16)) + (TRX_RL(v, 32) + TRX_RL(v, 48));
 }
+#undef TRX_DPPS
+#undef TRX_DPPM
+#undef TRX_RL
 // sum over aligned groups of `group` lanes (power of two <= 64)
 __device__ __forceinline__ float group_sum(float v, int group) {
+    if (group == kWave) return wave_sum(v);
     for (int o = group >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
     return v;
 }
@@ -85,7 +99,35 @@ __global__ void __launch_bounds__(kWave * kGatWaves)
     const int beg = rowptr[i], deg = rowptr[i + 1] - beg;
     float* sa = s_alpha[w];
 
-    // -------- per-head softmax over the in-edges of i (edges across lanes)
+    // -------- per-head softmax over the in-edges of i
+    if (deg * H <= kWave && H <= 8) {
+        // lanes = (edge, head) pairs: one round of gathers, per-head masked wave reductions
+        const int e = lane / H, h = lane - (lane / H) * H;
+        const bool on = lane < deg * H;
+        const float lg = on ? leaky(a_src[(size_t)src[beg + e] * H + h] + a_dst[(size_t)i * H + h] +
+                                        a_edge[(size_t)(beg + e) * H + h], slope)
+                            : -__builtin_huge_valf();
+        float m = -__builtin_huge_valf();
+#pragma unroll
+        for (int hh = 0; hh < 8; ++hh)
+            if (hh < H) {
+                const float mh = wave_max(on && h == hh ? lg : -__builtin_huge_valf());
+                if (h == hh) m = mh;
+            }
+        const float ex = on ? __expf(lg - m) : 0.0f;
+        float denom = 1.0f;
+#pragma unroll
+        for (int hh = 0; hh < 8; ++hh)
+            if (hh < H) {
+                const float sh = wave_sum(h == hh ? ex : 0.0f);
+                if (h == hh) denom = sh + 1e-16f;
+            }
+        if (on) {
+            const float al = ex / denom;
+            alpha[(size_t)(beg + e) * H + h] = al;
+            sa[lane] = al;  // = sa[e * H + h]
+        }
+    } else
     for (int h = 0; h < H; ++h) {
         const float ad = a_dst[(size_t)i * H + h];
         float m = -__builtin_huge_valf();
@@ -195,11 +237,17 @@ __global__ void __launch_bounds__(kWave * kGatWaves)
             }
             if (k * kWave < nq) {
                 float gsum = group_sum(part, group);
-                // every lane of the group now holds the group sum; lane leader adds it
-                const bool leader = (lane & (group - 1)) == 0;
-                if (leader && q < nq) {
+                if (group == kWave) {  // C >= 256: a chunk lies in one head, the sum is wave-uniform
+                    const int hk = (4 * kWave * k) / C;
 #pragma unroll
-                    for (int hh = 0; hh < 8; ++hh) hs[hh] += (hh == h) ? gsum : 0.0f;
+                    for (int hh = 0; hh < 8; ++hh) hs[hh] += (hh == hk) ? gsum : 0.0f;
+                } else {
+                    // every lane of the group now holds the group sum; lane leader adds it
+                    const bool leader = (lane & (group - 1)) == 0;
+                    if (leader && q < nq) {
+#pragma unroll
+                        for (int hh = 0; hh < 8; ++hh) hs[hh] += (hh == h) ? gsum : 0.0f;
+                    }
                 }
             }
         }
@@ -207,7 +255,7 @@ __global__ void __launch_bounds__(kWave * kGatWaves)
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
             if (h < H) {
-                float v = wave_sum(hs[h]);
+                float v = group == kWave ? hs[h] : wave_sum(hs[h]);
                 if (lane == 0 && e < kMaxDegCache) sda[e * H + h] = v;
                 if (e >= kMaxDegCache && lane == 0) dlogit[(size_t)(beg + e) * H + h] = v;  // temp: dalpha
             }
@@ -215,7 +263,34 @@ __global__ void __launch_bounds__(kWave * kGatWaves)
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // softmax + leaky_relu backward, lanes = edges
+    // softmax + leaky_relu backward
+    if (deg * H <= kWave && deg <= kMaxDegCache && H <= 8) {
+        // lanes = (edge, head) pairs, per-head masked wave reductions
+        const int e = lane / H, h = lane - (lane / H) * H;
+        const bool on = lane < deg * H;
+        float da = 0.0f, al = 0.0f, raw = 0.0f;
+        if (on) {
+            da = sda[lane];  // = sda[e * H + h]
+            al = alpha[(size_t)(beg + e) * H + h];
+            raw = a_src[(size_t)src[beg + e] * H + h] + a_dst[(size_t)i * H + h] + a_edge[(size_t)(beg + e) * H + h];
+        }
+        float t = 0.0f;
+#pragma unroll
+        for (int hh = 0; hh < 8; ++hh)
+            if (hh < H) {
+                const float th = wave_sum(h == hh ? al * da : 0.0f);
+                if (h == hh) t = th;
+            }
+        const float dl = on ? al * (da - t) * (raw > 0.0f ? 1.0f : slope) : 0.0f;
+        if (on) dlogit[(size_t)(beg + e) * H + h] = dl;
+#pragma unroll
+        for (int hh = 0; hh < 8; ++hh)
+            if (hh < H) {
+                const float gd = wave_sum(h == hh ? dl : 0.0f);
+                if (lane == hh) ga_dst[(size_t)i * H + hh] = gd;
+            }
+        return;
+    }
     for (int h = 0; h < H; ++h) {
         const float ad = a_dst[(size_t)i * H + h];
         float t = 0.0f;
