@@ -306,6 +306,25 @@ int trx_per_update(double* tree, int64_t capacity, const int64_t* idx, const dou
 int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
                    double* out_priority, void* stream);
 
+/* ------------------------------------------------ GAT layer tail (training)
+ * The autograd path's post-aggregation tail of a GATEncoder layer
+ * (src/models/gat_encoder.py:43-52): z = out + bias, h = LayerNorm(z; ln_w,
+ * ln_b, eps) (biased variance, like torch), then act 0: y = relu(h + res)
+ * (middle layers; res float32 or bfloat16 per res_dtype) or act 1: y = elu(h)
+ * (last layer).  out, y: float32 [N, F]; stats: float32 [N, 2] (mean, rstd)
+ * saved for the backward.  Backward: grad_out = dL/dz [N, F] float32,
+ * grad_res = dL/dres [N, F] in res_dtype (act 0), grads = [3, F] float32 sums
+ * over rows of dL/dz (bias), dL/dh * xhat (ln_w) and dL/dh (ln_b), reduced
+ * in a fixed order from workspace (trx_layer_tail_workspace_floats).  F <= 1024,
+ * F % 4 == 0.                                                              */
+int trx_layer_tail_forward(int32_t N, int32_t F, int32_t act, int32_t res_dtype, const float* out, const float* bias,
+                           const float* ln_w, const float* ln_b, float eps, const void* res, float* y, float* stats,
+                           void* stream);
+int64_t trx_layer_tail_workspace_floats(int32_t N, int32_t F);
+int trx_layer_tail_backward(int32_t N, int32_t F, int32_t act, int32_t res_dtype, const float* grad_y,
+                            const float* out, const float* bias, const float* ln_w, const float* y, const float* stats,
+                            float* grad_out, void* grad_res, float* grads, float* workspace, void* stream);
+
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
  * (passed as void*) into an equivalent fill-kernel node with the same

@@ -582,6 +582,41 @@ int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream) {
     return TRX_OK;
 }
 
+int trx_layer_tail_forward(int32_t N, int32_t F, int32_t act, int32_t res_dtype, const float* out, const float* bias,
+                           const float* ln_w, const float* ln_b, float eps, const void* res, float* y, float* stats,
+                           void* stream) {
+    if (N < 0 || F < 4 || F > 1024 || F % 4) return fail(TRX_EUNSUP, "layer_tail: F must be 4..1024, multiple of 4");
+    if (act != 0 && act != 1) return fail(TRX_EINVAL, "layer_tail: act must be 0 (relu(h + res)) or 1 (elu(h))");
+    if (res_dtype != 0 && res_dtype != 1) return fail(TRX_EUNSUP, "layer_tail: res dtype 0 (float32) or 1 (bfloat16)");
+    if (!out || !bias || !ln_w || !ln_b || !y || !stats || (act == 0 && !res))
+        return fail(TRX_EINVAL, "layer_tail: NULL buffer");
+    if (N == 0) return TRX_OK;
+    hipError_t e = trx::launch_layer_tail_fwd(N, F, act, res_dtype, out, bias, ln_w, ln_b, eps, res, y, stats,
+                                              static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "layer_tail forward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int64_t trx_layer_tail_workspace_floats(int32_t N, int32_t F) {
+    return N < 0 || F < 0 ? -1 : (int64_t)trx::layer_tail_blocks(N) * 3 * F;
+}
+
+int trx_layer_tail_backward(int32_t N, int32_t F, int32_t act, int32_t res_dtype, const float* grad_y,
+                            const float* out, const float* bias, const float* ln_w, const float* y, const float* stats,
+                            float* grad_out, void* grad_res, float* grads, float* workspace, void* stream) {
+    if (N < 0 || F < 4 || F > 1024 || F % 4) return fail(TRX_EUNSUP, "layer_tail: F must be 4..1024, multiple of 4");
+    if (act != 0 && act != 1) return fail(TRX_EINVAL, "layer_tail: act must be 0 (relu(h + res)) or 1 (elu(h))");
+    if (res_dtype != 0 && res_dtype != 1) return fail(TRX_EUNSUP, "layer_tail: res dtype 0 (float32) or 1 (bfloat16)");
+    if (!grad_y || !out || !bias || !ln_w || !y || !stats || !grad_out || !grads || !workspace ||
+        (act == 0 && !grad_res))
+        return fail(TRX_EINVAL, "layer_tail: NULL buffer");
+    if (N == 0) return TRX_OK;
+    hipError_t e = trx::launch_layer_tail_bwd(N, F, act, res_dtype, grad_y, out, bias, ln_w, y, stats, grad_out,
+                                              grad_res, workspace, grads, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "layer_tail backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
     if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
     int n = 0;

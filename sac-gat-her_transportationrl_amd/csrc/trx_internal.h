@@ -144,6 +144,13 @@ size_t gat_layer_infer_smem(const trx_gat_layer_args& a);
 hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream);
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
 size_t edge_head_infer_smem(const trx_edge_head_args& a);
+int layer_tail_blocks(int N);
+hipError_t launch_layer_tail_fwd(int N, int F, int act, int res_bf16, const float* out, const float* bias,
+                                 const float* w, const float* b, float eps, const void* res, float* y, float* stats,
+                                 hipStream_t stream);
+hipError_t launch_layer_tail_bwd(int N, int F, int act, int res_bf16, const float* gy, const float* out,
+                                 const float* bias, const float* w, const float* y, const float* stats, float* gout,
+                                 void* gres, float* part, float* grads, hipStream_t stream);
 hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t stream);
 size_t gat_prologue_smem(const trx_gat_prologue_args& a);
 hipError_t patch_graph_memsets(hipGraph_t graph, int* n_patched);

@@ -160,6 +160,57 @@ def gat_aggregate(xh, a_src, a_dst, a_edge_csr, g: GraphCSR, heads, channels, sl
     return _GATAggregate.apply(xh, a_src, a_dst, a_edge_csr, g, heads, channels, slope)
 
 
+class _LayerTail(torch.autograd.Function):
+    """GATEncoder's per-layer tail (gat_encoder.py:43-52 of the reference):
+    y = relu(LayerNorm(out + bias) + res) (act 0) or elu(LayerNorm(out +
+    bias)) (act 1), forward and backward as single kernels
+    (csrc/layer_tail.hip); same math as the torch ops it replaces, fp32."""
+
+    @staticmethod
+    def forward(ctx, out, bias, w, b, eps: float, res, act: int):
+        L = _lib.load()
+        out = out.float().contiguous()
+        N, F = out.shape
+        y = torch.empty_like(out)
+        stats = torch.empty(N, 2, device=out.device, dtype=torch.float32)
+        rdt = 0
+        if res is not None:
+            if res.dtype != torch.bfloat16:
+                res = res.float()
+            res = res.contiguous()
+            rdt = 1 if res.dtype == torch.bfloat16 else 0
+        bias_c, w_c, b_c = bias.float().contiguous(), w.float().contiguous(), b.float().contiguous()
+        _lib.check(L.trx_layer_tail_forward(N, F, act, rdt, _lib.ptr(out), _lib.ptr(bias_c), _lib.ptr(w_c),
+                                            _lib.ptr(b_c), float(eps), _lib.ptr(res), _lib.ptr(y), _lib.ptr(stats),
+                                            _lib.stream_ptr(out.device)), "trx_layer_tail_forward")
+        ctx.save_for_backward(out, bias_c, w_c, y, stats)
+        ctx.act, ctx.rdt = act, rdt
+        ctx.res_dtype = None if res is None else res.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        L = _lib.load()
+        out, bias, w, y, stats = ctx.saved_tensors
+        N, F = out.shape
+        gy = gy.float().contiguous()
+        gout = torch.empty_like(out)
+        gres = torch.empty(N, F, device=out.device, dtype=ctx.res_dtype) if ctx.act == 0 else None
+        grads = torch.empty(3, F, device=out.device, dtype=torch.float32)
+        ws = torch.empty(max(1, int(L.trx_layer_tail_workspace_floats(N, F))), device=out.device,
+                         dtype=torch.float32)
+        _lib.check(L.trx_layer_tail_backward(N, F, ctx.act, ctx.rdt, _lib.ptr(gy), _lib.ptr(out), _lib.ptr(bias),
+                                             _lib.ptr(w), _lib.ptr(y), _lib.ptr(stats), _lib.ptr(gout),
+                                             _lib.ptr(gres), _lib.ptr(grads), _lib.ptr(ws),
+                                             _lib.stream_ptr(out.device)), "trx_layer_tail_backward")
+        return gout, grads[0], grads[1], grads[2], None, gres, None
+
+
+def layer_tail(out, bias, norm: nn.LayerNorm, res=None):
+    """relu(norm(out + bias) + res) when res is given, else elu(norm(out + bias))."""
+    return _LayerTail.apply(out, bias, norm.weight, norm.bias, norm.eps, res, 0 if res is not None else 1)
+
+
 class _LoopMean(torch.autograd.Function):
     """PyG add_remaining_self_loops(fill_value='mean'): loop_attr[i] = sum of
     the kept in-edge attrs of i / max(count, 1).  Forward gathers through the
@@ -228,9 +279,12 @@ class GATConv(nn.Module):
         if self.att_edge is not None:
             _glorot_(self.att_edge)
 
-    def forward(self, x, edge_index, edge_attr=None, return_attention_weights=None, a_edge_csr=None):
+    def forward(self, x, edge_index, edge_attr=None, return_attention_weights=None, a_edge_csr=None,
+                skip_bias: bool = False):
         """a_edge_csr: this layer's edge logits [Et, H] already in CSR order
-        (GATEncoder computes every layer's in one product); else computed here."""
+        (GATEncoder computes every layer's in one product); else computed here.
+        skip_bias: return the output before `+ bias` (GATEncoder fuses the add
+        into the layer tail kernel)."""
         H, C = self.heads, self.out_channels
         N = x.size(0)
         g = build_csr(edge_index, N)
@@ -262,8 +316,8 @@ class GATConv(nn.Module):
             a_edge_csr = perm_gather(a_edge, g.perm, g.inv_perm)
         out, alpha = gat_aggregate(xh, a_src, a_dst, a_edge_csr, g, H, C, self.negative_slope)
         if not self.concat:
-            out = out.view(N, H, C).mean(1)
-        if self.bias is not None:
+            out = out.view(N, H, C).mean(1) if H > 1 else out.view(N, C)
+        if self.bias is not None and not skip_bias:
             out = out + self.bias
         if return_attention_weights:
             a_pyg = torch.empty_like(alpha)
@@ -350,22 +404,32 @@ class GATEncoder(nn.Module):
             last = i == len(self.layers) - 1
             ae = a_all[:, off:off + layer.heads] if shared else None
             off += layer.heads
+            norm = self.norms[i]
+            F_out = layer.heads * layer.out_channels if layer.concat else layer.out_channels
+            tail = (x.is_cuda and layer.bias is not None and norm.elementwise_affine and F_out % 4 == 0
+                    and F_out <= 1024 and not (last and return_attention))
             if last and return_attention:
                 x, attn_info = layer(x, edge_index, edge_attr=edge_attr, return_attention_weights=True, a_edge_csr=ae)
                 attn = attn_info[1]
             elif last:
-                x = layer(x, edge_index, edge_attr=edge_attr, a_edge_csr=ae)
+                x = layer(x, edge_index, edge_attr=edge_attr, a_edge_csr=ae, skip_bias=tail)
+                if tail:
+                    x = layer_tail(x, layer.bias, norm)
+                    continue
             else:
                 x_in = x
-                x = layer(x, edge_index, edge_attr=edge_attr, a_edge_csr=ae)
+                x = layer(x, edge_index, edge_attr=edge_attr, a_edge_csr=ae, skip_bias=tail)
                 if i == 0:
                     ip = self.input_proj
                     x_in = (skinny_linear(x_in, ip.weight, ip.bias) if ip.in_features <= _SKINNY_IN
                             else ip(x_in))
-                x = self.norms[i](x)
+                if tail:
+                    x = layer_tail(x, layer.bias, norm, x_in)
+                    continue
+                x = norm(x)
                 x = torch.relu(x + x_in)
                 continue
-            x = self.norms[i](x)
+            x = norm(x)
             x = F.elu(x)
         g_mean = global_mean_pool(x, batch, num_graphs)
         g_max = global_max_pool(x, batch, num_graphs)

@@ -131,3 +131,50 @@ def test_encoder_forward_backward_shapes():
     assert h.shape == (B * N, 256) and ctx.shape == (B, 512) and attn.shape == (B * (E + N), 1)
     (h.sum() + ctx.sum()).backward()
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in enc.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act,res_dtype,F", [(0, torch.float32, 1024), (0, torch.bfloat16, 1024), (1, None, 256),
+                                             (0, torch.float32, 12)])
+def test_layer_tail_matches_torch_ops(act, res_dtype, F):
+    """csrc/layer_tail.hip forward and backward against the torch ops of
+    GATEncoder's layer tail (bias add, LayerNorm, residual, ReLU / ELU):
+    values and all five gradients to fp32 reduction-order tolerance; two
+    backward runs agree bit for bit (fixed-order column sums)."""
+    from trafficrl.models.gat_encoder import layer_tail
+    g = torch.Generator(device="cuda").manual_seed(F + act)
+    N = 6144 if F > 12 else 37
+    out = torch.randn(N, F, device="cuda", generator=g, requires_grad=True)
+    norm = torch.nn.LayerNorm(F).cuda()
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.1 * torch.randn(F, device="cuda", generator=g))
+        norm.bias.copy_(0.1 * torch.randn(F, device="cuda", generator=g))
+    bias = (0.1 * torch.randn(F, device="cuda", generator=g)).requires_grad_()
+    res = None
+    if act == 0:
+        res = torch.randn(N, F, device="cuda", generator=g).to(res_dtype).requires_grad_()
+    gy = torch.randn(N, F, device="cuda", generator=g)
+
+    def run(fused):
+        for t in [out, bias, norm.weight, norm.bias] + ([res] if res is not None else []):
+            t.grad = None
+        if fused:
+            y = layer_tail(out, bias, norm, res)
+        else:
+            h = F_.layer_norm(out + bias, (F,), norm.weight, norm.bias, norm.eps)
+            y = torch.relu(h + res) if res is not None else F_.elu(h)
+        y.backward(gy)
+        grads = [t.grad.clone() for t in [out, bias, norm.weight, norm.bias] + ([res] if res is not None else [])]
+        return y.detach(), grads
+
+    F_ = torch.nn.functional
+    y_ref, g_ref = run(False)
+    y_got, g_got = run(True)
+    _, g_again = run(True)
+    torch.testing.assert_close(y_got, y_ref, atol=2e-5, rtol=2e-5)
+    for a, b in zip(g_got, g_ref):
+        assert a.dtype == b.dtype
+        tol = 2e-2 if a.dtype == torch.bfloat16 else 1e-4 * max(1.0, b.abs().max().item())
+        torch.testing.assert_close(a.float(), b.float(), atol=tol, rtol=1e-3)
+    for a, b in zip(g_got, g_again):
+        assert torch.equal(a, b)
