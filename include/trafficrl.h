@@ -325,6 +325,21 @@ int trx_layer_tail_backward(int32_t N, int32_t F, int32_t act, int32_t res_dtype
                             const float* out, const float* bias, const float* ln_w, const float* y, const float* stats,
                             float* grad_out, void* grad_res, float* grads, float* workspace, void* stream);
 
+/* -------------------------------------------- GAT attention dot products
+ * Training-path a_src[i,h] = <xh[i, h*C:(h+1)*C], att_src[h*C:(h+1)*C]> and
+ * a_dst likewise (PyG GATConv inside src/models/gat_encoder.py), float32
+ * [N, H].  xh [N, H*C] float32 (dtype 0) or bfloat16 (1).  Backward:
+ * grad_xh [N, H*C] in xh's dtype = grad_src[i,h] att_src + grad_dst[i,h]
+ * att_dst; grad_att float32 [2, H*C] (att_src, att_dst) = column sums over
+ * nodes, reduced in a fixed order from workspace
+ * (trx_att_dots_workspace_floats).  H <= 8, C % 4 == 0, H*C <= 1024.        */
+int trx_att_dots_forward(int32_t N, int32_t H, int32_t C, const void* xh, int32_t xh_dtype, const float* att_src,
+                         const float* att_dst, float* a_src, float* a_dst, void* stream);
+int64_t trx_att_dots_workspace_floats(int32_t N, int32_t H, int32_t C);
+int trx_att_dots_backward(int32_t N, int32_t H, int32_t C, const void* xh, int32_t xh_dtype, const float* att_src,
+                          const float* att_dst, const float* grad_src, const float* grad_dst, void* grad_xh,
+                          float* grad_att, float* workspace, void* stream);
+
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
  * (passed as void*) into an equivalent fill-kernel node with the same

@@ -617,6 +617,41 @@ int trx_layer_tail_backward(int32_t N, int32_t F, int32_t act, int32_t res_dtype
     return TRX_OK;
 }
 
+static int att_dots_check(int32_t N, int32_t H, int32_t C, int32_t xh_dtype) {
+    if (N < 0 || H < 1 || H > 8 || C < 4 || C % 4 || H * C > 1024)
+        return fail(TRX_EUNSUP, "att_dots: need 1 <= heads <= 8, channels % 4 == 0, heads*channels <= 1024");
+    if (xh_dtype != 0 && xh_dtype != 1) return fail(TRX_EUNSUP, "att_dots: xh dtype 0 (float32) or 1 (bfloat16)");
+    return TRX_OK;
+}
+
+int trx_att_dots_forward(int32_t N, int32_t H, int32_t C, const void* xh, int32_t xh_dtype, const float* att_src,
+                         const float* att_dst, float* a_src, float* a_dst, void* stream) {
+    if (int rc = att_dots_check(N, H, C, xh_dtype)) return rc;
+    if (!xh || !att_src || !att_dst || !a_src || !a_dst) return fail(TRX_EINVAL, "att_dots: NULL buffer");
+    if (N == 0) return TRX_OK;
+    hipError_t e = trx::launch_att_dots_fwd(N, H, C, xh, xh_dtype, att_src, att_dst, a_src, a_dst,
+                                            static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "att_dots forward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int64_t trx_att_dots_workspace_floats(int32_t N, int32_t H, int32_t C) {
+    return N < 0 || H < 0 || C < 0 ? -1 : (int64_t)trx::att_dots_blocks(N) * 2 * H * C;
+}
+
+int trx_att_dots_backward(int32_t N, int32_t H, int32_t C, const void* xh, int32_t xh_dtype, const float* att_src,
+                          const float* att_dst, const float* grad_src, const float* grad_dst, void* grad_xh,
+                          float* grad_att, float* workspace, void* stream) {
+    if (int rc = att_dots_check(N, H, C, xh_dtype)) return rc;
+    if (!xh || !att_src || !att_dst || !grad_src || !grad_dst || !grad_xh || !grad_att || !workspace)
+        return fail(TRX_EINVAL, "att_dots: NULL buffer");
+    if (N == 0) return TRX_OK;
+    hipError_t e = trx::launch_att_dots_bwd(N, H, C, xh, xh_dtype, att_src, att_dst, grad_src, grad_dst, grad_xh,
+                                            grad_att, workspace, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "att_dots backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
     if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
     int n = 0;

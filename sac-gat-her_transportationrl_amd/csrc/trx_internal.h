@@ -145,6 +145,12 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
 size_t edge_head_infer_smem(const trx_edge_head_args& a);
 int layer_tail_blocks(int N);
+int att_dots_blocks(int N);
+hipError_t launch_att_dots_fwd(int N, int H, int C, const void* xh, int bf16, const float* att_src,
+                               const float* att_dst, float* a_src, float* a_dst, hipStream_t stream);
+hipError_t launch_att_dots_bwd(int N, int H, int C, const void* xh, int bf16, const float* att_src,
+                               const float* att_dst, const float* g_src, const float* g_dst, void* g_xh,
+                               float* g_att, float* part, hipStream_t stream);
 hipError_t launch_layer_tail_fwd(int N, int F, int act, int res_bf16, const float* out, const float* bias,
                                  const float* w, const float* b, float eps, const void* res, float* y, float* stats,
                                  hipStream_t stream);

@@ -160,6 +160,51 @@ def gat_aggregate(xh, a_src, a_dst, a_edge_csr, g: GraphCSR, heads, channels, sl
     return _GATAggregate.apply(xh, a_src, a_dst, a_edge_csr, g, heads, channels, slope)
 
 
+class _AttDots(torch.autograd.Function):
+    """a_src[i,h] = <xh[i,h,:], att_src[h,:]>, a_dst likewise, float32 --
+    GATConv's attention dot products as one kernel each way
+    (csrc/att_dots.hip) instead of a cast + block-diagonal GEMM."""
+
+    @staticmethod
+    def forward(ctx, xh, att_src, att_dst, heads: int, channels: int):
+        L = _lib.load()
+        if xh.dtype not in (torch.float32, torch.bfloat16):
+            xh = xh.float()
+        xh = xh.contiguous()
+        N = xh.shape[0]
+        s_, d_ = att_src.detach().float().reshape(-1).contiguous(), att_dst.detach().float().reshape(-1).contiguous()
+        a_src = torch.empty(N, heads, device=xh.device, dtype=torch.float32)
+        a_dst = torch.empty_like(a_src)
+        dt = 1 if xh.dtype == torch.bfloat16 else 0
+        _lib.check(L.trx_att_dots_forward(N, heads, channels, _lib.ptr(xh), dt, _lib.ptr(s_), _lib.ptr(d_),
+                                          _lib.ptr(a_src), _lib.ptr(a_dst), _lib.stream_ptr(xh.device)),
+                   "trx_att_dots_forward")
+        ctx.save_for_backward(xh, s_, d_)
+        ctx.dims, ctx.dt, ctx.att_shape = (heads, channels), dt, att_src.shape
+        return a_src, a_dst
+
+    @staticmethod
+    def backward(ctx, g_src, g_dst):
+        L = _lib.load()
+        xh, s_, d_ = ctx.saved_tensors
+        H, C = ctx.dims
+        N = xh.shape[0]
+        g_src = torch.zeros(N, H, device=xh.device) if g_src is None else g_src.float().contiguous()
+        g_dst = torch.zeros(N, H, device=xh.device) if g_dst is None else g_dst.float().contiguous()
+        gxh = torch.empty_like(xh)
+        gatt = torch.empty(2, H * C, device=xh.device, dtype=torch.float32)
+        ws = torch.empty(max(1, int(L.trx_att_dots_workspace_floats(N, H, C))), device=xh.device,
+                         dtype=torch.float32)
+        _lib.check(L.trx_att_dots_backward(N, H, C, _lib.ptr(xh), ctx.dt, _lib.ptr(s_), _lib.ptr(d_), _lib.ptr(g_src),
+                                           _lib.ptr(g_dst), _lib.ptr(gxh), _lib.ptr(gatt), _lib.ptr(ws),
+                                           _lib.stream_ptr(xh.device)), "trx_att_dots_backward")
+        return gxh, gatt[0].view(ctx.att_shape), gatt[1].view(ctx.att_shape), None, None
+
+
+def att_dots(xh, att_src, att_dst, heads: int, channels: int):
+    return _AttDots.apply(xh, att_src, att_dst, heads, channels)
+
+
 class _LayerTail(torch.autograd.Function):
     """GATEncoder's per-layer tail (gat_encoder.py:43-52 of the reference):
     y = relu(LayerNorm(out + bias) + res) (act 0) or elu(LayerNorm(out +
@@ -292,15 +337,18 @@ class GATConv(nn.Module):
             xh = skinny_linear(x, self.lin.weight)         # [N, H*C]  (4 input features)
         else:
             xh = self.lin(x)                               # [N, H*C]  (MFMA GEMM)
-        # per-head attention dot products <xh_h, att_h> for src and dst as ONE
-        # float32 product with a block-diagonal [H*C, 2H] matrix (skinny:
-        # split-K weight gradient); same fp32 values as (xh3 * att).sum(-1)
-        eye = torch.eye(H, device=xh.device, dtype=torch.float32)
-        A = torch.cat([(self.att_src.view(H, C, 1).float() * eye.view(H, 1, H)).reshape(H * C, H),
-                       (self.att_dst.view(H, C, 1).float() * eye.view(H, 1, H)).reshape(H * C, H)], 1)
-        with torch.autocast("cuda", enabled=False):
-            a_sd = skinny_linear(xh.float(), A.t())        # [N, 2H]
-        a_src, a_dst = a_sd[:, :H], a_sd[:, H:]
+        # per-head attention dot products <xh_h, att_h> for src and dst: one
+        # kernel each way on the GPU; elsewhere ONE float32 product with a
+        # block-diagonal [H*C, 2H] matrix; same fp32 values as (xh3 * att).sum(-1)
+        if xh.is_cuda and H <= 8 and C % 4 == 0 and H * C <= 1024:
+            a_src, a_dst = att_dots(xh, self.att_src, self.att_dst, H, C)   # csrc/att_dots.hip
+        else:
+            eye = torch.eye(H, device=xh.device, dtype=torch.float32)
+            A = torch.cat([(self.att_src.view(H, C, 1).float() * eye.view(H, 1, H)).reshape(H * C, H),
+                           (self.att_dst.view(H, C, 1).float() * eye.view(H, 1, H)).reshape(H * C, H)], 1)
+            with torch.autocast("cuda", enabled=False):
+                a_sd = skinny_linear(xh.float(), A.t())        # [N, 2H]
+            a_src, a_dst = a_sd[:, :H], a_sd[:, H:]
         if a_edge_csr is not None:
             a_edge = None
         elif self.lin_edge is not None and edge_attr is not None:

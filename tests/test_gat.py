@@ -178,3 +178,43 @@ def test_layer_tail_matches_torch_ops(act, res_dtype, F):
         torch.testing.assert_close(a.float(), b.float(), atol=tol, rtol=1e-3)
     for a, b in zip(g_got, g_again):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,C,dt", [(4, 256, torch.bfloat16), (1, 256, torch.bfloat16), (4, 64, torch.float32),
+                                    (3, 12, torch.float32)])
+def test_att_dots_matches_torch_ops(H, C, dt):
+    """csrc/att_dots.hip against (xh.view(N,H,C).float() * att).sum(-1) and
+    its autograd gradients (xh in its own dtype, att float32); backward runs
+    agree bit for bit (fixed-order column sums)."""
+    from trafficrl.models.gat_encoder import att_dots
+    g = torch.Generator(device="cuda").manual_seed(H * C)
+    N = 6144 if C >= 64 else 50
+    xh = torch.randn(N, H * C, device="cuda", generator=g).to(dt).requires_grad_()
+    a_s = torch.randn(1, H, C, device="cuda", generator=g).requires_grad_()
+    a_d = torch.randn(1, H, C, device="cuda", generator=g).requires_grad_()
+    gs, gd = torch.randn(N, H, device="cuda", generator=g), torch.randn(N, H, device="cuda", generator=g)
+
+    def run(fused):
+        for t in (xh, a_s, a_d):
+            t.grad = None
+        if fused:
+            s, d = att_dots(xh, a_s, a_d, H, C)
+        else:
+            x3 = xh.float().view(N, H, C)
+            s, d = (x3 * a_s).sum(-1), (x3 * a_d).sum(-1)
+        (s * gs + d * gd).sum().backward()
+        return s.detach(), d.detach(), xh.grad.clone(), a_s.grad.clone(), a_d.grad.clone()
+
+    ref = run(False)
+    got = run(True)
+    again = run(True)
+    torch.testing.assert_close(got[0], ref[0], atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(got[1], ref[1], atol=1e-4, rtol=1e-4)
+    assert got[2].dtype == dt
+    torch.testing.assert_close(got[2].float(), ref[2].float(), atol=1e-2 if dt == torch.bfloat16 else 1e-5,
+                               rtol=1e-2 if dt == torch.bfloat16 else 1e-5)
+    for k in (3, 4):
+        torch.testing.assert_close(got[k], ref[k], atol=2e-3 * N ** 0.5 / 10, rtol=1e-4)
+    for a, b in zip(got[2:], again[2:]):
+        assert torch.equal(a, b)
