@@ -18,7 +18,7 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kAdWaves = 4;
-constexpr int kAdRows = 64;    // rows per workgroup in the backward
+constexpr int kAdRows = 16;    // rows per workgroup in the backward (>= 384 workgroups at N = 6144)
 constexpr int kAdChunks = 4;   // H*C <= 1024
 constexpr int kAdHeads = 8;
 

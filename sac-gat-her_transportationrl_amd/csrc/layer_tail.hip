@@ -22,7 +22,7 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kTailWaves = 4;
-constexpr int kTailRows = 64;      // rows per workgroup in the backward (16 per wave)
+constexpr int kTailRows = 16;      // rows per workgroup in the backward (4 per wave): >= 384 workgroups at N = 6144
 constexpr int kTailChunks = 4;     // F <= 64 * 4 * 4 = 1024
 
 #define TRX_DPPS(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false))
