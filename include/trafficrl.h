@@ -173,11 +173,12 @@ int trx_gat_forward(int32_t num_nodes, int32_t heads, int32_t channels, const in
 /* Backward of trx_gat_forward (without bias).  (sptr, spos, sdst) is the same
  * graph in CSR by SOURCE: for node j, entries sptr[j]..sptr[j+1] give the
  * dst-CSR position and destination of each out-edge (fixed order =>
- * deterministic, no float atomics).  grad_xh [N,heads*channels] float32. */
+ * deterministic, no float atomics).  grad_xh [N,heads*channels] in xh's dtype
+ * (float32, or bfloat16 rounded to nearest even when xh_bf16). */
 int trx_gat_backward(int32_t num_nodes, int32_t heads, int32_t channels, const int32_t* rowptr, const int32_t* src,
                      const int32_t* sptr, const int32_t* spos, const int32_t* sdst, const void* xh, int32_t xh_bf16,
                      const float* a_src, const float* a_dst, const float* a_edge, float negative_slope,
-                     const float* alpha, const float* grad_out, float* grad_xh, float* grad_a_src, float* grad_a_dst,
+                     const float* alpha, const float* grad_out, void* grad_xh, float* grad_a_src, float* grad_a_dst,
                      float* grad_a_edge, void* stream);
 
 /* ------------------------------------------------ fused GAT inference

@@ -470,7 +470,7 @@ int trx_gat_forward(int32_t num_nodes, int32_t heads, int32_t channels, const in
 int trx_gat_backward(int32_t num_nodes, int32_t heads, int32_t channels, const int32_t* rowptr, const int32_t* src,
                      const int32_t* sptr, const int32_t* spos, const int32_t* sdst, const void* xh, int32_t xh_bf16,
                      const float* a_src, const float* a_dst, const float* a_edge, float negative_slope,
-                     const float* alpha, const float* grad_out, float* grad_xh, float* grad_a_src, float* grad_a_dst,
+                     const float* alpha, const float* grad_out, void* grad_xh, float* grad_a_src, float* grad_a_dst,
                      float* grad_a_edge, void* stream) {
     if (num_nodes < 0 || heads <= 0 || heads > 8 || channels <= 0 || channels % 4 != 0 || heads * channels > 2048)
         return fail(TRX_EUNSUP, "gat: unsupported heads/channels");

@@ -79,6 +79,20 @@ __device__ __forceinline__ float4 load4<__hip_bfloat16>(const __hip_bfloat16* p)
     return f;
 }
 
+template <typename T>
+__device__ __forceinline__ void store4(T* p, float4 v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, float4 v) {
+    *reinterpret_cast<float4*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void store4<__hip_bfloat16>(__hip_bfloat16* p, float4 v) {
+    uint2 u;
+    u.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v.x) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v.y) << 16);
+    u.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v.z) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v.w) << 16);
+    *reinterpret_cast<uint2*>(p) = u;
+}
+
 __device__ __forceinline__ float leaky(float x, float slope) { return x > 0.0f ? x : x * slope; }
 
 }  // namespace
@@ -321,10 +335,11 @@ __global__ void __launch_bounds__(kWave * kGatWaves)
 
 // ------------------------------------------------------- backward (src)
 // CSR by source: sptr[j]..sptr[j+1] lists dst-CSR positions p of j's out-edges.
+template <typename T>
 __global__ void __launch_bounds__(kWave * kGatWaves)
     gat_bwd_src_kernel(int Nt, int H, int C, const int32_t* __restrict__ sptr, const int32_t* __restrict__ spos,
                        const int32_t* __restrict__ sdst, const float* __restrict__ alpha,
-                       const float* __restrict__ dlogit, const float* __restrict__ gout, float* __restrict__ gxh,
+                       const float* __restrict__ dlogit, const float* __restrict__ gout, T* __restrict__ gxh,
                        float* __restrict__ ga_src) {
     const int lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
@@ -356,7 +371,7 @@ __global__ void __launch_bounds__(kWave * kGatWaves)
 #pragma unroll
     for (int k = 0; k < kMaxChunks; ++k) {
         const int q = lane + kWave * k;
-        if (q < nq) *reinterpret_cast<float4*>(gxh + (size_t)j * HC + 4 * q) = acc[k];
+        if (q < nq) store4<T>(gxh + (size_t)j * HC + 4 * q, acc[k]);  // grad in xh's dtype (RNE to bf16)
     }
     for (int h = lane; h < H; h += kWave) {
         float s = 0.0f;
@@ -381,7 +396,7 @@ hipError_t launch_gat_forward(int Nt, int H, int C, const int32_t* rowptr, const
 hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, const int32_t* src, const int32_t* sptr,
                                const int32_t* spos, const int32_t* sdst, const void* xh, int bf16, const float* a_src,
                                const float* a_dst, const float* a_edge, float slope, const float* alpha,
-                               const float* gout, float* gxh, float* ga_src, float* ga_dst, float* ga_edge,
+                               const float* gout, void* gxh, float* ga_src, float* ga_dst, float* ga_edge,
                                hipStream_t stream) {
     dim3 grid((Nt + kGatWaves - 1) / kGatWaves), block(kWave * kGatWaves);
     if (bf16)
@@ -393,8 +408,12 @@ hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, cons
                            static_cast<const float*>(xh), a_src, a_dst, a_edge, slope, alpha, gout, ga_edge, ga_dst);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gat_bwd_src_kernel, grid, block, 0, stream, Nt, H, C, sptr, spos, sdst, alpha, ga_edge, gout,
-                       gxh, ga_src);
+    if (bf16)
+        hipLaunchKernelGGL(gat_bwd_src_kernel<__hip_bfloat16>, grid, block, 0, stream, Nt, H, C, sptr, spos, sdst,
+                           alpha, ga_edge, gout, static_cast<__hip_bfloat16*>(gxh), ga_src);
+    else
+        hipLaunchKernelGGL(gat_bwd_src_kernel<float>, grid, block, 0, stream, Nt, H, C, sptr, spos, sdst, alpha,
+                           ga_edge, gout, static_cast<float*>(gxh), ga_src);
     return hipGetLastError();
 }
 

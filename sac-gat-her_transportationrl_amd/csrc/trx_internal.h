@@ -137,7 +137,7 @@ hipError_t launch_gat_forward(int Nt, int H, int C, const int32_t* rowptr, const
 hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, const int32_t* src, const int32_t* sptr,
                                const int32_t* spos, const int32_t* sdst, const void* xh, int bf16, const float* a_src,
                                const float* a_dst, const float* a_edge, float slope, const float* alpha,
-                               const float* gout, float* gxh, float* ga_src, float* ga_dst, float* ga_edge,
+                               const float* gout, void* gxh, float* ga_src, float* ga_dst, float* ga_edge,
                                hipStream_t stream);
 
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a);

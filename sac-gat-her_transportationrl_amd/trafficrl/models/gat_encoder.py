@@ -143,7 +143,7 @@ class _GATAggregate(torch.autograd.Function):
         g = ctx.g
         N = g.num_nodes
         gout = gout.float().contiguous()
-        gxh = torch.empty(N, ctx.heads * ctx.channels, device=gout.device, dtype=torch.float32)
+        gxh = torch.empty(N, ctx.heads * ctx.channels, device=gout.device, dtype=xh.dtype)  # written in xh's dtype
         ga_src = torch.empty_like(a_src)
         ga_dst = torch.empty_like(a_dst)
         ga_edge = torch.empty_like(a_edge)
@@ -153,7 +153,7 @@ class _GATAggregate(torch.autograd.Function):
                                       _lib.ptr(alpha), _lib.ptr(gout), _lib.ptr(gxh), _lib.ptr(ga_src),
                                       _lib.ptr(ga_dst), _lib.ptr(ga_edge), _lib.stream_ptr(gout.device)),
                    "trx_gat_backward")
-        return gxh.to(ctx.xh_dtype), ga_src, ga_dst, ga_edge, None, None, None, None
+        return gxh.to(ctx.xh_dtype), ga_src, ga_dst, ga_edge, None, None, None, None  # no-op cast unless xh was promoted
 
 
 def gat_aggregate(xh, a_src, a_dst, a_edge_csr, g: GraphCSR, heads, channels, slope=0.2):
