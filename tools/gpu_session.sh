@@ -35,6 +35,8 @@ for s in "$@"; do
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         upd) step upd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/upd -o run --output-format csv -- python3 tools/agent_profile.py 4096 update ;;
         overlap) step overlap 300 python tools/overlap_probe.py 4096 ;;
+        walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
+        uprof) step uprof 300 python tools/update_profile.py 70 ;;
         copies) step copies 300 python tools/update_profile.py 60 copies ;;
         istamps) step istamps 300 python tools/infer_stamps.py 4096 ;;
         abact) TRX_LIB=${TRX_LIB_A:-} step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act
