@@ -341,6 +341,19 @@ int trx_att_dots_backward(int32_t N, int32_t H, int32_t C, const void* xh, int32
                           const float* att_dst, const float* grad_src, const float* grad_dst, void* grad_xh,
                           float* grad_att, float* workspace, void* stream);
 
+/* ------------------------------------------------- narrow-row LayerNorm
+ * Training-path LayerNorm of the 4-/6-wide raw node / link features
+ * (src/rl/sac.py:38-39): y = (x - mean) * rsqrt(var + eps) * w + b per row
+ * (biased variance), x, y float32 [N, d], d <= 8; stats [N, 2] (mean,
+ * rstd) for the backward.  Backward: grad_x [N, d]; grad_wb float32 [2, d]
+ * = column sums of grad_y * xhat and grad_y, reduced in a fixed order from
+ * workspace (trx_small_ln_workspace_floats).                              */
+int trx_small_ln_forward(int32_t N, int32_t d, const float* x, const float* w, const float* b, float eps, float* y,
+                         float* stats, void* stream);
+int64_t trx_small_ln_workspace_floats(int32_t N, int32_t d);
+int trx_small_ln_backward(int32_t N, int32_t d, const float* grad_y, const float* x, const float* w,
+                          const float* stats, float* grad_x, float* grad_wb, float* workspace, void* stream);
+
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
  * (passed as void*) into an equivalent fill-kernel node with the same

@@ -652,6 +652,32 @@ int trx_att_dots_backward(int32_t N, int32_t H, int32_t C, const void* xh, int32
     return TRX_OK;
 }
 
+int trx_small_ln_forward(int32_t N, int32_t d, const float* x, const float* w, const float* b, float eps, float* y,
+                         float* stats, void* stream) {
+    if (N < 0 || d < 1 || d > 8) return fail(TRX_EUNSUP, "small_ln: row width must be 1..8 (got %d)", d);
+    if (!x || !w || !b || !y || !stats) return fail(TRX_EINVAL, "small_ln: NULL buffer");
+    if (N == 0) return TRX_OK;
+    hipError_t e = trx::launch_small_ln_fwd(N, d, x, w, b, eps, y, stats, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "small_ln forward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int64_t trx_small_ln_workspace_floats(int32_t N, int32_t d) {
+    return N < 0 || d < 0 ? -1 : (int64_t)trx::small_ln_blocks(N) * 2 * d;
+}
+
+int trx_small_ln_backward(int32_t N, int32_t d, const float* grad_y, const float* x, const float* w,
+                          const float* stats, float* grad_x, float* grad_wb, float* workspace, void* stream) {
+    if (N < 0 || d < 1 || d > 8) return fail(TRX_EUNSUP, "small_ln: row width must be 1..8 (got %d)", d);
+    if (!grad_y || !x || !w || !stats || !grad_x || !grad_wb || !workspace)
+        return fail(TRX_EINVAL, "small_ln: NULL buffer");
+    if (N == 0) return TRX_OK;
+    hipError_t e = trx::launch_small_ln_bwd(N, d, grad_y, x, w, stats, grad_x, grad_wb, workspace,
+                                            static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "small_ln backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
     if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
     int n = 0;

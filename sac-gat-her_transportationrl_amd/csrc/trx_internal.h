@@ -146,6 +146,11 @@ hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t strea
 size_t edge_head_infer_smem(const trx_edge_head_args& a);
 int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
+int small_ln_blocks(int N);
+hipError_t launch_small_ln_fwd(int N, int d, const float* x, const float* w, const float* b, float eps, float* y,
+                               float* stats, hipStream_t stream);
+hipError_t launch_small_ln_bwd(int N, int d, const float* gy, const float* x, const float* w, const float* stats,
+                               float* gx, float* gwb, float* part, hipStream_t stream);
 hipError_t launch_att_dots_fwd(int N, int H, int C, const void* xh, int bf16, const float* att_src,
                                const float* att_dst, float* a_src, float* a_dst, hipStream_t stream);
 hipError_t launch_att_dots_bwd(int N, int H, int C, const void* xh, int bf16, const float* att_src,

@@ -25,6 +25,7 @@ EXPORTS = (
     "trx_gat_backward", "trx_per_update", "trx_per_sample", "trx_graph_patch_memsets", "trx_gat_layer_infer",
     "trx_edge_head_infer", "trx_gat_prologue_infer", "trx_layer_tail_forward", "trx_layer_tail_workspace_floats",
     "trx_layer_tail_backward", "trx_att_dots_forward", "trx_att_dots_workspace_floats", "trx_att_dots_backward",
+    "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward",
 )
 
 
@@ -156,6 +157,10 @@ def load():
     L.trx_att_dots_workspace_floats.argtypes = [_i32, _i32, _i32]
     L.trx_att_dots_workspace_floats.restype = ctypes.c_int64
     L.trx_att_dots_backward.argtypes = [_i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.trx_small_ln_forward.argtypes = [_i32, _i32, _vp, _vp, _vp, _f32, _vp, _vp, _vp]
+    L.trx_small_ln_workspace_floats.argtypes = [_i32, _i32]
+    L.trx_small_ln_workspace_floats.restype = ctypes.c_int64
+    L.trx_small_ln_backward.argtypes = [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_layer_tail_workspace_floats.argtypes = [_i32, _i32]
     L.trx_layer_tail_workspace_floats.restype = ctypes.c_int64
     L.trx_layer_tail_backward.argtypes = [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -164,7 +169,7 @@ def load():
                  "trx_observe", "trx_gat_forward", "trx_gat_backward", "trx_per_update", "trx_per_sample",
                  "trx_graph_patch_memsets", "trx_gat_layer_infer", "trx_edge_head_infer", "trx_gat_prologue_infer",
                  "trx_layer_tail_forward", "trx_layer_tail_backward", "trx_att_dots_forward",
-                 "trx_att_dots_backward"):
+                 "trx_att_dots_backward", "trx_small_ln_forward", "trx_small_ln_backward"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

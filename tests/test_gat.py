@@ -218,3 +218,34 @@ def test_att_dots_matches_torch_ops(H, C, dt):
         torch.testing.assert_close(got[k], ref[k], atol=2e-3 * N ** 0.5 / 10, rtol=1e-4)
     for a, b in zip(got[2:], again[2:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,d", [(19456, 6), (6144, 4), (300, 8)])
+def test_small_layer_norm_matches_torch(N, d):
+    """csrc/small_ln.hip (input_layer_norm on the GPU) against
+    torch.nn.functional.layer_norm: output and the x / weight / bias
+    gradients to fp32 reduction-order tolerance; deterministic backward."""
+    from trafficrl.rl.sac import input_layer_norm
+    g = torch.Generator(device="cuda").manual_seed(N + d)
+    x = (3 * torch.randn(N, d, device="cuda", generator=g) + 1).requires_grad_()
+    ln = torch.nn.LayerNorm(d).cuda()
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.2 * torch.randn(d, device="cuda", generator=g))
+        ln.bias.copy_(0.2 * torch.randn(d, device="cuda", generator=g))
+    gy = torch.randn(N, d, device="cuda", generator=g)
+
+    def run(fused):
+        for t in (x, ln.weight, ln.bias):
+            t.grad = None
+        y = input_layer_norm(ln, x) if fused else F.layer_norm(x, (d,), ln.weight, ln.bias, ln.eps)
+        y.backward(gy)
+        return y.detach(), x.grad.clone(), ln.weight.grad.clone(), ln.bias.grad.clone()
+
+    ref, got, again = run(False), run(True), run(True)
+    torch.testing.assert_close(got[0], ref[0], atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(got[1], ref[1], atol=1e-4, rtol=1e-4)
+    for k in (2, 3):
+        torch.testing.assert_close(got[k], ref[k], atol=1e-3 * N ** 0.5 / 10, rtol=1e-4)
+    for a, b in zip(got, again):
+        assert torch.equal(a, b)

@@ -125,15 +125,16 @@ def test_prologue_matches_torch_ops():
     dot products are summed in another order before the bf16 rounding)."""
     from trafficrl.models import fused
     from trafficrl.models.gat_encoder import _LoopMean
-    from trafficrl.rl.sac import Actor, input_layer_norm
+    from trafficrl.rl.sac import Actor
     torch.manual_seed(5)
     actor = Actor(4, 6, 256, 256, 3).cuda()
     node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=3)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         topo = fused.topology(ei, bv, B)
         x0, ean, a_all = fused.prologue(actor, node_x, ea, topo)
-        x_ref = input_layer_norm(actor.node_norm, node_x)
-        e_ref = input_layer_norm(actor.edge_norm, ea)
+        lnf = torch.nn.functional.layer_norm
+        x_ref = lnf(node_x.float(), (4,), actor.node_norm.weight, actor.node_norm.bias, actor.node_norm.eps)
+        e_ref = lnf(ea.float(), (6,), actor.edge_norm.weight, actor.edge_norm.bias, actor.edge_norm.eps)
         g = topo.g
         full = torch.cat([e_ref, _LoopMean.apply(e_ref, g)], 0)
         Ms = [(l.lin_edge.weight.view(l.heads, l.out_channels, -1) * l.att_edge.view(l.heads, l.out_channels, 1))
