@@ -253,6 +253,15 @@ typedef struct trx_edge_head_args {
     int64_t* action;            /* [B] drawn graph-local link (u != NULL) */
 } trx_edge_head_args;
 int trx_edge_head_infer(const trx_edge_head_args* a, void* stream);
+/* Backward of the edge scorer's logits (softmax = 0) for training, one
+ * workgroup per graph (hidden <= 256): from grad_logits [B*E] float32 and the
+ * same args (p, c, ea, we, w2, src, dst, nodes_per_graph) it writes grad_p
+ * [N, 2H] bf16, grad_c [B, H] float32, grad_z [B*E, H] bf16 (the gradient at
+ * the bf16 link pre-activation: the link-feature weight and input gradients
+ * are GEMMs of it) and grad_w2_part [B, H] float32 (per-graph partial sums of
+ * the 256->1 weight gradient).  bf16 roundings follow the autocast torch path. */
+int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
+                           void* grad_z, float* grad_w2_part, void* stream);
 
 /* Input stage of Actor/Critic (src/rl/sac.py:38-41) plus every layer's edge
  * attention logits (src/models/gat_encoder.py:36-52: PyG GATConv with

@@ -752,6 +752,105 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
     return hipErrorInvalidValue;
 }
 
+// ------------------------------------------------ edge scorer, backward
+// Training-path backward of the edge scorer (the logits of edge_head_infer
+// with softmax = 0), one workgroup per graph, thread k = hidden unit k
+// (hidden <= 256).  The forward is recomputed from the LDS-staged p rows; the
+// bf16 roundings are those of the autocast torch path: the incoming logit
+// gradient and d relu = bf16(g * w2) are bf16, relu backward on the fp32 z,
+// the gradient reaching the bf16 sum of the gathers and the link term is
+// rounded to bf16 (grad_z), p gradients are fp32 sums over the graph's links
+// (thread k owns LDS column k: no atomics) rounded to bf16 at the end.
+// Outputs: grad_p [N, 2H] bf16, grad_c [B, H], grad_z [E_total, H] bf16 (for
+// the link-feature weight / input gradients, GEMMs on the host side) and
+// grad_w2_part [B, H] (per-graph sums of bf16(g) * bf16(relu(z))).
+__global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
+                                                                      uint16_t* grad_p, float* grad_c,
+                                                                      uint16_t* grad_z, float* grad_w2_part) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int ED = kEdgeED;
+    const int g = blockIdx.x, k = threadIdx.x;
+    const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
+    uint16_t* pr = reinterpret_cast<uint16_t*>(smem);                 // [n][2*Hd] bf16
+    float* gps = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);   // [n][Hd] grad of p[:, :Hd]
+    float* gpd = gps + (size_t)n * Hd;                                 // [n][Hd] grad of p[:, Hd:]
+    float* eal = gpd + (size_t)n * Hd;                                 // [E][ED] bf16-rounded link features
+    float* gl = eal + (size_t)E * ED;                                  // [E] bf16(grad logit)
+    int* sl = reinterpret_cast<int*>(gl + E);                          // [E]
+    int* dl = sl + E;                                                  // [E]
+    const int64_t node0 = (int64_t)g * n;
+    {
+        const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.p) + node0 * 2 * Hd);
+        trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
+        for (int v = k; v < n * 2 * Hd / 8; v += kInferThreads) dst4[v] = src4[v];
+    }
+    for (int v = k; v < n * Hd; v += kInferThreads) gps[v] = gpd[v] = 0.0f;
+    for (int e = k; e < E; e += kInferThreads) {
+        const int64_t eg = (int64_t)g * E + e;
+        int s = (int)(a.src[eg] - node0), d = (int)(a.dst[eg] - node0);
+        s = s < 0 ? 0 : (s >= n ? n - 1 : s);  // out-of-block links are refused on the host (topology check)
+        d = d < 0 ? 0 : (d >= n ? n - 1 : d);
+        sl[e] = s;
+        dl[e] = d;
+        gl[e] = bf16r(grad_logits[eg]);
+    }
+    for (int v = k; v < E * ED; v += kInferThreads) {
+        const int e = v / ED, j = v - (v / ED) * ED;
+        eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
+    }
+    const bool on = k < Hd;
+    float we[ED];
+#pragma unroll
+    for (int j = 0; j < ED; ++j) we[j] = (on && j < D) ? a.we[k * D + j] : 0.0f;
+    const float w2 = on ? a.w2[k] : 0.0f, ck = on ? a.c[(int64_t)g * Hd + k] : 0.0f;
+    __syncthreads();
+    float gc = 0.0f, gw2 = 0.0f;
+    if (on) {
+        for (int e = 0; e < E; ++e) {
+            const int s = sl[e], d = dl[e];
+            float ew = 0.0f;
+#pragma unroll
+            for (int j = 0; j < ED; ++j)
+                if (j < D) ew += eal[e * ED + j] * we[j];
+            const float z1 = bf16r(bf2f(pr[s * 2 * Hd + k]) + bf2f(pr[d * 2 * Hd + Hd + k]));
+            const float z2 = bf16r(z1 + bf16r(ew));
+            const float z3 = z2 + ck;
+            const float gb = gl[e];
+            gw2 += gb * bf16r(fmaxf(z3, 0.0f));
+            const float dz = z3 > 0.0f ? bf16r(gb * w2) : 0.0f;
+            gc += dz;
+            const float dzz = bf16r(dz);
+            grad_z[((int64_t)g * E + e) * Hd + k] = f2bf(dzz);
+            gps[s * Hd + k] += dzz;
+            gpd[d * Hd + k] += dzz;
+        }
+        grad_c[(int64_t)g * Hd + k] = gc;
+        grad_w2_part[(int64_t)g * Hd + k] = gw2;
+        for (int i = 0; i < n; ++i) {
+            grad_p[(node0 + i) * 2 * Hd + k] = f2bf(gps[i * Hd + k]);
+            grad_p[(node0 + i) * 2 * Hd + Hd + k] = f2bf(gpd[i * Hd + k]);
+        }
+    }
+}
+
+size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
+    return (size_t)a.nodes_per_graph * 2 * a.hidden * 2 + (size_t)a.nodes_per_graph * 2 * a.hidden * 4 +
+           (size_t)a.edges_per_graph * (kEdgeED * 4 + 4 + 8);
+}
+
+hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
+                                void* grad_z, float* grad_w2_part, hipStream_t stream) {
+    const size_t smem = edge_head_bwd_smem(a);
+    if (smem > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(edge_head_bwd_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(edge_head_bwd_kernel, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a, grad_logits,
+                       static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
+    return hipGetLastError();
+}
+
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream) {
     const size_t smem = edge_head_infer_smem(a);
     const void* fn = a.hidden <= 256 ? reinterpret_cast<const void*>(edge_head_infer_kernel<1>)

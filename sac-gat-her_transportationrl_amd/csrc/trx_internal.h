@@ -144,6 +144,9 @@ size_t gat_layer_infer_smem(const trx_gat_layer_args& a);
 hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream);
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
 size_t edge_head_infer_smem(const trx_edge_head_args& a);
+size_t edge_head_bwd_smem(const trx_edge_head_args& a);
+hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
+                                void* grad_z, float* grad_w2_part, hipStream_t stream);
 int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
 int small_ln_blocks(int N);

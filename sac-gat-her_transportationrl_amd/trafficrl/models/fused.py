@@ -272,3 +272,77 @@ def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: 
     if u is not None:
         return logits, out, action
     return logits, out
+
+
+_idx32_cache: Dict[Tuple, torch.Tensor] = {}
+
+
+def _idx32(t: torch.Tensor) -> torch.Tensor:
+    key = (t.data_ptr(), t._version, t.numel(), t.device)
+    r = _idx32_cache.get(key)
+    if r is None:
+        r = t.to(torch.int32).contiguous()
+        if len(_idx32_cache) > 64:
+            _idx32_cache.clear()
+        _idx32_cache[key] = r
+    return r
+
+
+def _edge_args(p, c, ea, we, w2, b2, src32, dst32, B: int, n: int, E: int):
+    a = _lib.TrxEdgeHeadArgs()
+    a.num_graphs, a.edges_per_graph, a.hidden, a.edge_dim = B, E, we.shape[0], we.shape[1]
+    a.nodes_per_graph = n
+    a.src, a.dst, a.p, a.c = src32.data_ptr(), dst32.data_ptr(), p.data_ptr(), c.data_ptr()
+    a.ea, a.we, a.w2, a.b2 = ea.data_ptr(), we.data_ptr(), w2.data_ptr(), b2.data_ptr()
+    a.softmax = 0
+    return a
+
+
+class _EdgeScores(torch.autograd.Function):
+    """Training-path edge scorer logits (the factored edge MLP of
+    _EdgeHead.edge_scores for a regular batch): forward = the inference
+    kernel with softmax off, backward = trx_edge_head_backward plus two
+    products for the link-feature block.  Same bf16 rounding points as the
+    autocast torch path."""
+
+    @staticmethod
+    def forward(ctx, p, c, ea, W1e, W2, b2, src, dst, B: int, n: int):
+        L = _lib.load()
+        E = ea.shape[0] // B
+        p = p.to(torch.bfloat16).contiguous()
+        c = c.float().contiguous()
+        eaf = ea.float().contiguous()
+        we, w2, b2r = _bf16r(W1e), _bf16r(W2.reshape(-1)), _bf16r(b2.reshape(-1))
+        src32, dst32 = _idx32(src), _idx32(dst)
+        out = torch.empty(B * E, device=p.device, dtype=torch.float32)
+        a = _edge_args(p, c, eaf, we, w2, b2r, src32, dst32, B, n, E)
+        a.out = out.data_ptr()
+        _lib.check(L.trx_edge_head_infer(a, _lib.stream_ptr(p.device)), "trx_edge_head_infer")
+        ctx.save_for_backward(p, c, eaf, we, w2, b2r, src32, dst32)
+        ctx.dims = (B, n, E)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        L = _lib.load()
+        p, c, ea, we, w2, b2r, src32, dst32 = ctx.saved_tensors
+        B, n, E = ctx.dims
+        H = we.shape[0]
+        g = g.float().contiguous()
+        grad_p = torch.empty_like(p)
+        grad_c = torch.empty(B, H, device=p.device, dtype=torch.float32)
+        grad_z = torch.empty(B * E, H, device=p.device, dtype=torch.bfloat16)
+        gw2 = torch.empty(B, H, device=p.device, dtype=torch.float32)
+        a = _edge_args(p, c, ea, we, w2, b2r, src32, dst32, B, n, E)
+        _lib.check(L.trx_edge_head_backward(a, _lib.ptr(g), _lib.ptr(grad_p), _lib.ptr(grad_c), _lib.ptr(grad_z),
+                                            _lib.ptr(gw2), _lib.stream_ptr(p.device)), "trx_edge_head_backward")
+        from .skinny import _splitk_wgrad
+        g_ea = (grad_z @ we.to(torch.bfloat16)).float()                     # skinny_linear's dx (bf16 GEMM)
+        g_we = _splitk_wgrad(grad_z, ea.to(torch.bfloat16))                  # and its split-K fp32 dW
+        g_w2 = gw2.sum(0).view(1, H)
+        g_b2 = g.to(torch.bfloat16).sum(0, dtype=torch.float32).view(1)
+        return grad_p, grad_c, g_ea, g_we, g_w2, g_b2, None, None, None, None
+
+
+def edge_scores_train(p, c, ea, W1e, W2, b2, src, dst, B: int, n: int):
+    return _EdgeScores.apply(p, c, ea, W1e, W2, b2, src, dst, B, n)

@@ -192,6 +192,7 @@ def clip_grad_norm_listwise_(params, max_norm: float):
 
 
 FUSED_INFERENCE = True   # module switch (tests compare both paths)
+FUSED_EDGE_TRAIN = True  # training-path edge scorer kernels (tests compare both paths)
 
 
 def _fused_topology(encoder, node_x, edge_index, batch, B, head=None):
@@ -232,6 +233,14 @@ class _EdgeHead(nn.Module):
         p = node_emb @ w_nodes.t()                                    # per-node projections
         hdim = W1.shape[0]
         c = global_ctx @ W1[:, 2 * d + k:].t() + b1                   # [B, H] per-graph context
+        W2, b2 = self.edge_mlp[2].weight, self.edge_mlp[2].bias
+        if (FUSED_EDGE_TRAIN and regular is not None and p.is_cuda and fused.autocast_bf16() and hdim % 4 == 0
+                and hdim <= 256
+                and k <= 8 and node_emb.shape[0] % regular[0] == 0 and node_emb.shape[0] // regular[0] <= 64):
+            # one kernel each way for the gathers, link term, context, ReLU and 256->1 product
+            B = regular[0]
+            return fused.edge_scores_train(p, c, edge_attr, W1[:, 2 * d:2 * d + k], W2, b2, src, dst, B,
+                                           node_emb.shape[0] // B)
         if regular is not None:
             B, src_l, dst_l = regular
             z = regular_gather(p[:, :hdim], src_l, B) + regular_gather(p[:, hdim:], dst_l, B)
@@ -241,7 +250,6 @@ class _EdgeHead(nn.Module):
             z = p[src, :hdim] + p[dst, hdim:]
             z = z + skinny_linear(edge_attr, W1[:, 2 * d:2 * d + k])
             z = z + c[edge_batch]
-        W2, b2 = self.edge_mlp[2].weight, self.edge_mlp[2].bias
         return skinny_linear(torch.relu(z), W2, b2).squeeze(-1)
 
 

@@ -173,3 +173,46 @@ def test_fused_draw_is_inverse_cdf_of_probs():
     p = probs.view(B, E).double()
     # binomial standard error at n=200 is <= 0.036; 5 sigma
     assert (freq - p).abs().max().item() < 0.18
+
+
+def test_edge_scores_training_kernels_match_torch_ops():
+    """Training-path edge scorer (trx_edge_head_infer forward + trx_edge_head_
+    backward) against the autograd torch ops of _EdgeHead.edge_scores under
+    bf16 autocast: logits and the gradients of node embeddings, context,
+    link features and the edge-MLP weights to bf16 precision."""
+    from trafficrl.rl import sac
+    from trafficrl.rl.sac import Critic, regular_layout
+    torch.manual_seed(7)
+    critic = Critic(4, 6, 256, 256, 3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(B=32, seed=9)
+    N = node_x.shape[0]
+    g = torch.Generator(device="cuda").manual_seed(3)
+    emb = torch.randn(N, 256, device="cuda", generator=g).requires_grad_()
+    ctx = torch.randn(B, 512, device="cuda", generator=g).requires_grad_()
+    eat = torch.randn(B * E, 6, device="cuda", generator=g).requires_grad_()
+    gl = torch.randn(B * E, device="cuda", generator=g)
+    src, dst = ei
+    reg = regular_layout(ei, bv, B)
+
+    def run(flag):
+        sac.FUSED_EDGE_TRAIN = flag
+        for t in [emb, ctx, eat] + list(critic.edge_mlp.parameters()):
+            t.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            lg = critic.edge_scores(emb, ctx, eat, src, dst, bv[src], reg).float()
+        lg.backward(gl)
+        grads = [t.grad.float().clone() for t in [emb, ctx, eat] + list(critic.edge_mlp.parameters())]
+        return lg.detach(), grads
+
+    try:
+        ref_l, ref_g = run(False)
+        got_l, got_g = run(True)
+    finally:
+        sac.FUSED_EDGE_TRAIN = True
+    span = (ref_l.max() - ref_l.min()).item()
+    assert (got_l - ref_l).abs().max().item() <= 0.01 * span + 1e-3
+    names = ["emb", "ctx", "edge_attr", "W1", "b1", "W2", "b2"]
+    for name, a, b in zip(names, got_g, ref_g):
+        scale = b.abs().max().item() + 1e-6
+        err = (a - b).abs().max().item()
+        assert err <= 0.03 * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
