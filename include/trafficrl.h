@@ -363,6 +363,16 @@ int64_t trx_small_ln_workspace_floats(int32_t N, int32_t d);
 int trx_small_ln_backward(int32_t N, int32_t d, const float* grad_y, const float* x, const float* w,
                           const float* stats, float* grad_x, float* grad_wb, float* workspace, void* stream);
 
+/* --------------------------------------------------- global graph pooling
+ * GATEncoder's readout (src/models/gat_encoder.py:53) for a regular batch:
+ * out [B, 2F] = mean over the graph's n nodes | max over them, x [B*n, F]
+ * float32; ties [B, F] = how many nodes reach the max (saved for the
+ * backward, which spreads the max gradient evenly over ties like torch's
+ * amax).  grad_x [B*n, F] = grad_mean / n + (x == max) * grad_max / ties.   */
+int trx_graph_pool_forward(int32_t B, int32_t n, int32_t F, const float* x, float* out, float* ties, void* stream);
+int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, const float* out, const float* ties,
+                            const float* grad_out, float* grad_x, void* stream);
+
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
  * (passed as void*) into an equivalent fill-kernel node with the same

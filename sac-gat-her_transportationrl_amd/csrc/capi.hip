@@ -697,6 +697,25 @@ int trx_small_ln_backward(int32_t N, int32_t d, const float* grad_y, const float
     return TRX_OK;
 }
 
+int trx_graph_pool_forward(int32_t B, int32_t n, int32_t F, const float* x, float* out, float* ties, void* stream) {
+    if (B < 0 || n < 1 || F < 1) return fail(TRX_EINVAL, "graph_pool: B >= 0, n >= 1, F >= 1");
+    if (!x || !out || !ties) return fail(TRX_EINVAL, "graph_pool: NULL buffer");
+    if (B == 0) return TRX_OK;
+    hipError_t e = trx::launch_graph_pool_fwd(B, n, F, x, out, ties, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "graph_pool forward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, const float* out, const float* ties,
+                            const float* grad_out, float* grad_x, void* stream) {
+    if (B < 0 || n < 1 || F < 1) return fail(TRX_EINVAL, "graph_pool: B >= 0, n >= 1, F >= 1");
+    if (!x || !out || !ties || !grad_out || !grad_x) return fail(TRX_EINVAL, "graph_pool: NULL buffer");
+    if (B == 0) return TRX_OK;
+    hipError_t e = trx::launch_graph_pool_bwd(B, n, F, x, out, ties, grad_out, grad_x, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "graph_pool backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
     if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
     int n = 0;

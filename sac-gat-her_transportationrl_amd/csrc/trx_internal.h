@@ -150,6 +150,9 @@ hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_l
 int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
 int small_ln_blocks(int N);
+hipError_t launch_graph_pool_fwd(int B, int n, int F, const float* x, float* out, float* ties, hipStream_t stream);
+hipError_t launch_graph_pool_bwd(int B, int n, int F, const float* x, const float* out, const float* ties,
+                                 const float* g, float* gx, hipStream_t stream);
 hipError_t launch_small_ln_fwd(int N, int d, const float* x, const float* w, const float* b, float eps, float* y,
                                float* stats, hipStream_t stream);
 hipError_t launch_small_ln_bwd(int N, int d, const float* gy, const float* x, const float* w, const float* stats,

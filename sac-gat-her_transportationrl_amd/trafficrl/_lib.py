@@ -26,6 +26,7 @@ EXPORTS = (
     "trx_edge_head_infer", "trx_gat_prologue_infer", "trx_layer_tail_forward", "trx_layer_tail_workspace_floats",
     "trx_layer_tail_backward", "trx_att_dots_forward", "trx_att_dots_workspace_floats", "trx_att_dots_backward",
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
+    "trx_graph_pool_forward", "trx_graph_pool_backward",
 )
 
 
@@ -153,6 +154,8 @@ def load():
     L.trx_edge_head_infer.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp]
     L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
     L.trx_edge_head_backward.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp, _vp, _vp, _vp, _vp, _vp]
+    L.trx_graph_pool_forward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp]
+    L.trx_graph_pool_backward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_layer_tail_forward.argtypes = [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]
     L.trx_att_dots_forward.argtypes = [_i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]
     L.trx_att_dots_workspace_floats.argtypes = [_i32, _i32, _i32]
@@ -171,7 +174,7 @@ def load():
                  "trx_graph_patch_memsets", "trx_gat_layer_infer", "trx_edge_head_infer", "trx_gat_prologue_infer",
                  "trx_layer_tail_forward", "trx_layer_tail_backward", "trx_att_dots_forward",
                  "trx_att_dots_backward", "trx_small_ln_forward", "trx_small_ln_backward",
-                 "trx_edge_head_backward"):
+                 "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

@@ -256,6 +256,35 @@ def layer_tail(out, bias, norm: nn.LayerNorm, res=None):
     return _LayerTail.apply(out, bias, norm.weight, norm.bias, norm.eps, res, 0 if res is not None else 1)
 
 
+class _GraphPool(torch.autograd.Function):
+    """cat([global_mean_pool, global_max_pool], 1) for a regular batch as one
+    kernel each way (csrc/graph_pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, B: int):
+        L = _lib.load()
+        x = x.float().contiguous()
+        N, F_ = x.shape
+        out = torch.empty(B, 2 * F_, device=x.device, dtype=torch.float32)
+        ties = torch.empty(B, F_, device=x.device, dtype=torch.float32)
+        _lib.check(L.trx_graph_pool_forward(B, N // B, F_, _lib.ptr(x), _lib.ptr(out), _lib.ptr(ties),
+                                            _lib.stream_ptr(x.device)), "trx_graph_pool_forward")
+        ctx.save_for_backward(x, out, ties)
+        ctx.B = B
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        L = _lib.load()
+        x, out, ties = ctx.saved_tensors
+        N, F_ = x.shape
+        gx = torch.empty_like(x)
+        _lib.check(L.trx_graph_pool_backward(ctx.B, N // ctx.B, F_, _lib.ptr(x), _lib.ptr(out), _lib.ptr(ties),
+                                             _lib.ptr(g.float().contiguous()), _lib.ptr(gx),
+                                             _lib.stream_ptr(x.device)), "trx_graph_pool_backward")
+        return gx, None
+
+
 class _LoopMean(torch.autograd.Function):
     """PyG add_remaining_self_loops(fill_value='mean'): loop_attr[i] = sum of
     the kept in-edge attrs of i / max(count, 1).  Forward gathers through the
@@ -479,6 +508,9 @@ class GATEncoder(nn.Module):
                 continue
             x = norm(x)
             x = F.elu(x)
+        B = int(batch.max()) + 1 if num_graphs is None else num_graphs
+        if x.is_cuda and x.dtype == torch.float32 and B > 0 and is_regular_batch(batch, B):
+            return x, _GraphPool.apply(x, B), attn                       # csrc/graph_pool.hip
         g_mean = global_mean_pool(x, batch, num_graphs)
         g_max = global_max_pool(x, batch, num_graphs)
         return x, torch.cat([g_mean, g_max], dim=1), attn

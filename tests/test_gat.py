@@ -249,3 +249,25 @@ def test_small_layer_norm_matches_torch(N, d):
         torch.testing.assert_close(got[k], ref[k], atol=1e-3 * N ** 0.5 / 10, rtol=1e-4)
     for a, b in zip(got, again):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_graph_pool_matches_torch_ops():
+    """csrc/graph_pool.hip: mean | max readout and its gradient against
+    view().mean / amax (ties included: ReLU outputs are often exactly 0, and
+    amax's backward spreads the gradient over ties)."""
+    from trafficrl.models.gat_encoder import _GraphPool
+    g = torch.Generator(device="cuda").manual_seed(11)
+    B, n, F_ = 256, 24, 256
+    x = torch.relu(torch.randn(B * n, F_, device="cuda", generator=g)).requires_grad_()
+    x.data[:n, :8] = 0.0                      # an all-zero column block: n-way ties
+    gy = torch.randn(B, 2 * F_, device="cuda", generator=g)
+    out = _GraphPool.apply(x, B)
+    out.backward(gy)
+    gx = x.grad.clone()
+    x.grad = None
+    xv = x.view(B, n, F_)
+    ref = torch.cat([xv.mean(1), xv.amax(1)], 1)
+    ref.backward(gy)
+    torch.testing.assert_close(out, ref, atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(gx, x.grad, atol=1e-6, rtol=1e-6)
