@@ -108,6 +108,36 @@ def _bf16r(t: torch.Tensor) -> torch.Tensor:
     return t.detach().to(torch.bfloat16).float().contiguous()
 
 
+# Prepared (bf16 / bf16-rounded) weight copies for the no-grad passes, reused
+# until the weights change.  The SAC update is replayed from a HIP graph, which
+# updates parameters without bumping their version counters, so the trainer
+# and DiscreteSAC.apply_gradients advance an epoch after every update; the key
+# also holds each parameter's (address, version) for in-place edits from Python
+# (load_state_dict, eager optimizer steps).  Never used while a graph is being
+# captured (the captured update must recompute them on every replay).
+_PREP_EPOCH = [0]
+_prep_cache: Dict[Tuple, Tuple] = {}
+
+
+def weights_changed():
+    _PREP_EPOCH[0] += 1
+
+
+def _prepared(owner, name: str, params, make):
+    if torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing():
+        return make()
+    key = (_PREP_EPOCH[0],) + tuple((p.data_ptr(), p._version) for p in params)
+    slot = (id(owner), name)
+    hit = _prep_cache.get(slot)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    val = make()
+    if len(_prep_cache) > 256:
+        _prep_cache.clear()
+    _prep_cache[slot] = (key, val)
+    return val
+
+
 def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology):
     """Actor/Critic input LayerNorms + every encoder layer's edge logits in
     CSR order (trx_gat_prologue_infer: one small kernel for the M rows, one
@@ -191,13 +221,15 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
         args.concat, args.max_graph_edges = int(l.concat), topo.max_graph_edges
         keep = []
         if i == 0:
-            w0 = _bf16r(l.lin.weight)
-            wp, bp = _bf16r(enc.input_proj.weight), _bf16r(enc.input_proj.bias)
+            ip = enc.input_proj
+            w0, wp, bp = _prepared(l, "l0", (l.lin.weight, ip.weight, ip.bias),
+                                   lambda: (_bf16r(l.lin.weight), _bf16r(ip.weight), _bf16r(ip.bias)))
             keep += [w0, wp, bp]
             args.in_dim, args.x0, args.w0 = x.shape[1], x.data_ptr(), w0.data_ptr()
             args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
         else:
-            xh = torch.mm(prev_bf16, l.lin.weight.detach().to(torch.bfloat16).t())
+            wl = _prepared(l, "lin", (l.lin.weight,), lambda: l.lin.weight.detach().to(torch.bfloat16))
+            xh = torch.mm(prev_bf16, wl.t())
             keep.append(xh)
             args.in_dim, args.xh = 0, xh.data_ptr()
             if last:
@@ -241,12 +273,13 @@ def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: 
     W1, b1 = head.edge_mlp[0].weight, head.edge_mlp[0].bias
     d, k = head.embed, head.edge_in
     hid = W1.shape[0]
-    w_nodes = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0).detach().to(torch.bfloat16)
+    w_nodes, wc, we, w2, b2 = _prepared(head, "edge", (W1, b1, head.edge_mlp[2].weight, head.edge_mlp[2].bias), lambda: (
+        torch.cat([W1[:, :d], W1[:, d:2 * d]], 0).detach().to(torch.bfloat16),
+        W1[:, 2 * d + k:].detach().to(torch.bfloat16).t(),
+        _bf16r(W1[:, 2 * d:2 * d + k]), _bf16r(head.edge_mlp[2].weight.reshape(-1)),
+        _bf16r(head.edge_mlp[2].bias.reshape(-1))))
     p = torch.mm(emb_bf16, w_nodes.t()).contiguous()                      # bf16 [N, 2*hid]
-    c = (ctx @ W1[:, 2 * d + k:].t() + b1).float().contiguous()           # autocast: bf16 GEMM + fp32 bias
-    we = _bf16r(W1[:, 2 * d:2 * d + k])
-    w2 = _bf16r(head.edge_mlp[2].weight.reshape(-1))
-    b2 = _bf16r(head.edge_mlp[2].bias.reshape(-1))                     # stays on the device (graph capture)
+    c = (torch.mm(ctx.to(torch.bfloat16), wc) + b1).float().contiguous()  # autocast's bf16 GEMM + fp32 bias
     ea = edge_attr.float().contiguous()
     BE = topo.B * topo.e
     out = torch.empty(BE, device=dev, dtype=torch.float32)

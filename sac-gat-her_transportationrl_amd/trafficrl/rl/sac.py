@@ -502,6 +502,7 @@ class DiscreteSAC:
         if clip:
             clip_grad_norm_listwise_([self.log_alpha], self.grad_clip)
         self.alpha_opt.step()
+        fused.weights_changed()   # prepared inference weights are stale now
         with torch.no_grad():
             if alpha_max is not None:
                 self.log_alpha.clamp_(max=float(np.log(alpha_max)))

@@ -35,6 +35,7 @@ import numpy as np
 import torch
 
 from .data.tntp_parser import load_graph_data, sioux_falls
+from .models import fused
 from .env.vec_env import VecRepairEnv
 from .rl.replay import DeviceReplay, her_relabel
 from . import _lib
@@ -286,6 +287,7 @@ class Trainer:
             out = self._graphed()
         else:
             out = self._update_once(*self._draw_update_randoms())
+        fused.weights_changed()   # a graph replay changes parameters without bumping their versions
         self.last_losses = out
         return out
 

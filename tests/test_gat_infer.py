@@ -216,3 +216,32 @@ def test_edge_scores_training_kernels_match_torch_ops():
         scale = b.abs().max().item() + 1e-6
         err = (a - b).abs().max().item()
         assert err <= 0.03 * scale, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def test_prepared_weights_follow_updates():
+    """The fused no-grad path reuses prepared bf16 weight copies between
+    updates.  A parameter change the version counter does not see (what a
+    HIP-graph replay of the SAC update does; emulated with .data) must reach
+    the kernels once fused.weights_changed() is called -- Trainer.update and
+    DiscreteSAC.apply_gradients call it after every update."""
+    from trafficrl.models import fused
+    from trafficrl.rl.sac import Actor
+    torch.manual_seed(8)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(B=16, seed=2)
+
+    def logits():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            return actor._fused(node_x, ei, ea, bv, B, mask=mask)[0].clone()
+
+    before = logits()
+    torch.testing.assert_close(logits(), before, atol=0, rtol=0)      # cached copies reproduce the result
+    actor.edge_mlp[0].weight.data.mul_(-1.0)                           # invisible to the version counter
+    actor.encoder.layers[1].lin.weight.data.mul_(0.5)
+    fused.weights_changed()
+    after = logits()
+    (ref, _, _), _ = _both(lambda: actor(node_x, ei, ea, mask, bv, num_graphs=B))
+    valid = mask > 0
+    assert not torch.allclose(after[valid], before[valid])
+    # to bf16 precision of the logits' magnitude (the span can be tiny here)
+    assert (after[valid] - ref[valid]).abs().max().item() <= 1e-2 * ref[valid].abs().max().item() + 1e-3
