@@ -263,7 +263,7 @@ int trx_edge_head_infer(const trx_edge_head_args* a, void* stream);
 int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
                            void* grad_z, float* grad_w2_part, void* stream);
 
-/* Input stage of Actor/Critic (src/rl/sac.py:38-41) plus every layer's edge
+/* Input stage of Actor/Critic (src/rl/sac.py:36-37) plus every layer's edge
  * attention logits (src/models/gat_encoder.py:36-52: PyG GATConv with
  * edge_dim and add_self_loops fill_value='mean') for regular batches:
  *   x0 = LayerNorm(node_x), ea = LayerNorm(edge_x)                  (fp32)
@@ -318,7 +318,7 @@ int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_
 
 /* ------------------------------------------------ GAT layer tail (training)
  * The autograd path's post-aggregation tail of a GATEncoder layer
- * (src/models/gat_encoder.py:43-52): z = out + bias, h = LayerNorm(z; ln_w,
+ * (src/models/gat_encoder.py:40-49): z = out + bias, h = LayerNorm(z; ln_w,
  * ln_b, eps) (biased variance, like torch), then act 0: y = relu(h + res)
  * (middle layers; res float32 or bfloat16 per res_dtype) or act 1: y = elu(h)
  * (last layer).  out, y: float32 [N, F]; stats: float32 [N, 2] (mean, rstd)
@@ -352,7 +352,7 @@ int trx_att_dots_backward(int32_t N, int32_t H, int32_t C, const void* xh, int32
 
 /* ------------------------------------------------- narrow-row LayerNorm
  * Training-path LayerNorm of the 4-/6-wide raw node / link features
- * (src/rl/sac.py:38-39): y = (x - mean) * rsqrt(var + eps) * w + b per row
+ * (src/rl/sac.py:27-28, 36-37): y = (x - mean) * rsqrt(var + eps) * w + b per row
  * (biased variance), x, y float32 [N, d], d <= 8; stats [N, 2] (mean,
  * rstd) for the backward.  Backward: grad_x [N, d]; grad_wb float32 [2, d]
  * = column sums of grad_y * xhat and grad_y, reduced in a fixed order from
@@ -364,7 +364,7 @@ int trx_small_ln_backward(int32_t N, int32_t d, const float* grad_y, const float
                           const float* stats, float* grad_x, float* grad_wb, float* workspace, void* stream);
 
 /* --------------------------------------------------- global graph pooling
- * GATEncoder's readout (src/models/gat_encoder.py:53) for a regular batch:
+ * GATEncoder's readout (src/models/gat_encoder.py:50-52) for a regular batch:
  * out [B, 2F] = mean over the graph's n nodes | max over them, x [B*n, F]
  * float32; ties [B, F] = how many nodes reach the max (saved for the
  * backward, which spreads the max gradient evenly over ties like torch's

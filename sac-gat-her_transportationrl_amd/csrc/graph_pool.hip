@@ -1,5 +1,5 @@
 // graph_pool.hip -- global mean | max pooling of GATEncoder (src/models/
-// gat_encoder.py:53, PyG global_mean_pool / global_max_pool + cat) for a
+// gat_encoder.py:50-52, PyG global_mean_pool / global_max_pool + cat) for a
 // regular batch (graph b owns nodes [b*n, (b+1)*n)), training path.
 // Forward: one thread per (graph, feature) -> out [B, 2F] = mean | max, the
 // max and its tie count kept for the backward.  Backward: one thread per

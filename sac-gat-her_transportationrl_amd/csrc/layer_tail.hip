@@ -1,7 +1,7 @@
 // layer_tail.hip -- the post-aggregation tail of a GATEncoder layer in the
 // training (autograd) path, forward and backward as single kernels.
 //
-// GATEncoder (src/models/gat_encoder.py:36-52) after each GATConv:
+// GATEncoder (src/models/gat_encoder.py:40-49) after each GATConv:
 //     z = out + bias;  h = LayerNorm(z; w, b)
 //     middle layers: y = relu(h + res)     last layer: y = elu(h)
 // Through torch ops that is 4 kernels forward (bias add, LayerNorm, residual

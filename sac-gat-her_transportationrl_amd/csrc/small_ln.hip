@@ -1,5 +1,5 @@
 // small_ln.hip -- LayerNorm over the 4-/6-wide raw node / link features of
-// Actor and Critic (src/rl/sac.py:38-39, nn.LayerNorm(node_in / edge_in)) in
+// Actor and Critic (src/rl/sac.py:27-28, 36-37: nn.LayerNorm(node_in / edge_in)) in
 // the training (autograd) path.  torch runs such narrow rows either with one
 // workgroup per row (nn.LayerNorm) or as ~8 elementwise/reduction launches
 // forward and ~12 backward (the vectorised form in rl/sac.py); here one

@@ -206,7 +206,7 @@ def att_dots(xh, att_src, att_dst, heads: int, channels: int):
 
 
 class _LayerTail(torch.autograd.Function):
-    """GATEncoder's per-layer tail (gat_encoder.py:43-52 of the reference):
+    """GATEncoder's per-layer tail (gat_encoder.py:40-49 of the reference):
     y = relu(LayerNorm(out + bias) + res) (act 0) or elu(LayerNorm(out +
     bias)) (act 1), forward and backward as single kernels
     (csrc/layer_tail.hip); same math as the torch ops it replaces, fp32."""

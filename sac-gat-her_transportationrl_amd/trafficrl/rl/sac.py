@@ -83,7 +83,7 @@ class _SmallLN(torch.autograd.Function):
 
 
 def input_layer_norm(ln: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
-    """nn.LayerNorm over the 4-/6-wide raw node/edge features (sac.py:38-39).
+    """nn.LayerNorm over the 4-/6-wide raw node/edge features (sac.py:27-28, 36-37).
     torch's generic row kernel spends one workgroup per row there (~0.9 ms per
     acting call at 4096 graphs); on the GPU one thread per row (_SmallLN),
     elsewhere the same math as a handful of vectorised ops.  Wide rows keep
