@@ -191,11 +191,34 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
         S.act[tid] = active;
     }
     for (int i = tid; i < NP * NP; i += L) S.eid[i] = g.eid_of[i];
+    // the cost-table region doubles as the [E] i16 scratch of link positions below
+    int16_t* wpos_tmp = reinterpret_cast<int16_t*>(S.w);
+    for (int i = tid; i < E; i += L) wpos_tmp[i] = -1;
     for (int i = tid; i < Z * N; i += L) S.dem[i] = g.dem[i];
     for (int i = tid; i <= N; i += L) S.inptr[i] = (int16_t)g.in_ptr[i];
     for (int i = tid; i < E; i += L) S.insrc[i] = (uint8_t)g.in_src[i];
     for (int i = tid; i < E; i += L) S.t0[i] = g.t0[i];
     __syncthreads();
+    // cost tables in quad layout: entries without a link stay +inf for the whole
+    // launch; only the link entries are rewritten per MSA iteration.  Thread i
+    // (< EPW*E <= L) keeps the table position of env-link i in a register.
+    for (int i = tid; i < NP * NP; i += L) {
+        const int e = S.eid[i];
+        if (e >= 0) {
+            const int u = i / NP, v = i - u * NP;
+            wpos_tmp[e] = (int16_t)(u * NP + (v & (kQuad - 1)) * NPL + (v >> 2));
+        }
+    }
+    __syncthreads();
+    const bool wpos_reg = EL <= L;
+    int my_wpos = -1;
+    if (wpos_reg && tid < EL) {
+        const int el = tid / E, e = tid - el * E;
+        const int pos = wpos_tmp[e];
+        my_wpos = pos >= 0 ? el * NP * NP + pos : -1;
+    }
+    __syncthreads();
+    for (int x = tid; x < EPW * NP * NP; x += L) S.w[x] = kInfF;
 
     // ------------------------------------------------------- load state
     for (int i = tid; i < EL; i += L) {
@@ -240,13 +263,18 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
     float unassigned_lane = 0.0f;
 
     for (int it = 0; it < p.iters; ++it) {
-        // ---------------- per-env cost rows in quad layout (LDS)
-        for (int x = tid; x < EPW * NP * NP; x += L) {
-            int el = x / (NP * NP), r = x - el * NP * NP;
-            int u = r / NP, c = r - u * NP;  // c = jj * NPL + ii  ->  v = 4*ii + jj
-            int v = kQuad * (c % NPL) + c / NPL;
-            int e = S.eid[u * NP + v];
-            S.w[x] = e >= 0 ? S.t[el * E + e] : kInfF;
+        // ---------------- per-env cost rows in quad layout (LDS): the link entries
+        //                  (u -> v = 4*ii + jj at column c = jj * NPL + ii of row u)
+        if (wpos_reg) {
+            if (my_wpos >= 0) S.w[my_wpos] = S.t[tid];
+        } else {
+            for (int x = tid; x < EPW * NP * NP; x += L) {
+                int el = x / (NP * NP), r = x - el * NP * NP;
+                int u = r / NP, c = r - u * NP;  // c = jj * NPL + ii  ->  v = 4*ii + jj
+                int v = kQuad * (c % NPL) + c / NPL;
+                int e = S.eid[u * NP + v];
+                S.w[x] = e >= 0 ? S.t[el * E + e] : kInfF;
+            }
         }
         __syncthreads();
         TRX_STAMP(1);
