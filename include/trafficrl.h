@@ -373,6 +373,21 @@ int trx_graph_pool_forward(int32_t B, int32_t n, int32_t F, const float* x, floa
 int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, const float* out, const float* ties,
                             const float* grad_out, float* grad_x, void* stream);
 
+/* ------------------------------------------------ multi-tensor bf16 round
+ * dst[k] = bf16(src[k]) for up to TRX_MAX_ROUND row-major blocks in one launch
+ * (src rows x cols float32 with row stride src_stride; dst contiguous, bf16
+ * bits when out_bf16[k], else the bf16-rounded value as float32).  Used to
+ * prepare the small weight blocks of the fused inference passes.           */
+#define TRX_MAX_ROUND 16
+typedef struct trx_round_list {
+    int32_t count;
+    int32_t out_bf16[TRX_MAX_ROUND];
+    int64_t rows[TRX_MAX_ROUND], cols[TRX_MAX_ROUND], src_stride[TRX_MAX_ROUND];
+    const float* src[TRX_MAX_ROUND];
+    void* dst[TRX_MAX_ROUND];
+} trx_round_list;
+int trx_bf16_round(const trx_round_list* l, void* stream);
+
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
  * (passed as void*) into an equivalent fill-kernel node with the same

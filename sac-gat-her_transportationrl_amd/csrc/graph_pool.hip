@@ -6,6 +6,8 @@
 // (node, feature): g_mean / n + (x == max ? g_max / ties : 0) -- torch's
 // amax backward spreads the gradient evenly over ties.  Replaces ~3 forward
 // and ~7 backward torch launches per encoder.
+// Also here: trx_bf16_round, the multi-tensor bf16 rounding of the small
+// weight blocks the fused inference passes read (one launch per pass).
 #include <hip/hip_runtime.h>
 
 #include "trx_internal.h"
@@ -60,4 +62,35 @@ hipError_t launch_graph_pool_bwd(int B, int n, int F, const float* x, const floa
     return hipGetLastError();
 }
 
+}  // namespace trx
+
+// ------------------------------------------------------------------------
+// Multi-tensor bf16 rounding (trx_bf16_round): the fused inference passes
+// need bf16 copies (or bf16-rounded float32 copies) of ~10 small weight
+// blocks per pass; one launch for all of them instead of one or two each.
+namespace trx {
+namespace {
+__global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
+    const int k = blockIdx.y;
+    if (k >= l.count) return;
+    const int64_t rows = l.rows[k], cols = l.cols[k], n = rows * cols;
+    const float* src = l.src[k];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / cols, c = i - r * cols;
+        const __bf16 h = (__bf16)src[r * l.src_stride[k] + c];
+        if (l.out_bf16[k])
+            static_cast<uint16_t*>(l.dst[k])[i] = __builtin_bit_cast(uint16_t, h);
+        else
+            static_cast<float*>(l.dst[k])[i] = (float)h;
+    }
+}
+}  // namespace
+
+hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream) {
+    int64_t mx = 1;
+    for (int k = 0; k < l.count; ++k) mx = l.rows[k] * l.cols[k] > mx ? l.rows[k] * l.cols[k] : mx;
+    const unsigned bx = (unsigned)((mx + 255) / 256 < 64 ? (mx + 255) / 256 : 64);
+    hipLaunchKernelGGL(bf16_round_kernel, dim3(bx, l.count), dim3(256), 0, stream, l);
+    return hipGetLastError();
+}
 }  // namespace trx

@@ -150,6 +150,7 @@ hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_l
 int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
 int small_ln_blocks(int N);
+hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream);
 hipError_t launch_graph_pool_fwd(int B, int n, int F, const float* x, float* out, float* ties, hipStream_t stream);
 hipError_t launch_graph_pool_bwd(int B, int n, int F, const float* x, const float* out, const float* ties,
                                  const float* g, float* gx, hipStream_t stream);

@@ -26,7 +26,7 @@ EXPORTS = (
     "trx_edge_head_infer", "trx_gat_prologue_infer", "trx_layer_tail_forward", "trx_layer_tail_workspace_floats",
     "trx_layer_tail_backward", "trx_att_dots_forward", "trx_att_dots_workspace_floats", "trx_att_dots_backward",
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
-    "trx_graph_pool_forward", "trx_graph_pool_backward",
+    "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round",
 )
 
 
@@ -112,6 +112,18 @@ class TrxGatPrologueArgs(ctypes.Structure):
     ]
 
 
+MAX_ROUND = 16
+
+
+class TrxRoundList(ctypes.Structure):
+    """trx_round_list (include/trafficrl.h)."""
+    _fields_ = [
+        ("count", _i32), ("out_bf16", _i32 * MAX_ROUND), ("rows", ctypes.c_int64 * MAX_ROUND),
+        ("cols", ctypes.c_int64 * MAX_ROUND), ("src_stride", ctypes.c_int64 * MAX_ROUND),
+        ("src", _vp * MAX_ROUND), ("dst", _vp * MAX_ROUND),
+    ]
+
+
 class TrafficRLError(RuntimeError):
     pass
 
@@ -155,6 +167,7 @@ def load():
     L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
     L.trx_edge_head_backward.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_graph_pool_forward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp]
+    L.trx_bf16_round.argtypes = [ctypes.POINTER(TrxRoundList), _vp]
     L.trx_graph_pool_backward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_layer_tail_forward.argtypes = [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]
     L.trx_att_dots_forward.argtypes = [_i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]
@@ -174,7 +187,8 @@ def load():
                  "trx_graph_patch_memsets", "trx_gat_layer_infer", "trx_edge_head_infer", "trx_gat_prologue_infer",
                  "trx_layer_tail_forward", "trx_layer_tail_backward", "trx_att_dots_forward",
                  "trx_att_dots_backward", "trx_small_ln_forward", "trx_small_ln_backward",
-                 "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward"):
+                 "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward",
+                 "trx_bf16_round"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

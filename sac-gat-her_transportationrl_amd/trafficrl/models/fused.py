@@ -119,6 +119,26 @@ _PREP_EPOCH = [0]
 _prep_cache: Dict[Tuple, Tuple] = {}
 
 
+def _round_into(pairs):
+    """One trx_bf16_round launch: for each (src float32 2-D/1-D view with unit
+    column stride, dst contiguous float32 or bfloat16 tensor of the same
+    shape) write bf16(src) (as bf16 bits, or rounded float32)."""
+    L = _lib.load()
+    lst = _lib.TrxRoundList()
+    lst.count = len(pairs)
+    dev = None
+    for k, (src, dst) in enumerate(pairs):
+        src = src.detach()
+        src2 = src.reshape(1, -1) if src.dim() == 1 else src
+        assert src2.dtype == torch.float32 and src2.stride(1) == 1 and dst.is_contiguous()
+        lst.out_bf16[k] = int(dst.dtype == torch.bfloat16)
+        lst.rows[k], lst.cols[k] = src2.shape
+        lst.src_stride[k] = src2.stride(0)
+        lst.src[k], lst.dst[k] = src2.data_ptr(), dst.data_ptr()
+        dev = src.device
+    _lib.check(L.trx_bf16_round(lst, _lib.stream_ptr(dev)), "trx_bf16_round")
+
+
 def weights_changed():
     _PREP_EPOCH[0] += 1
 
@@ -136,6 +156,38 @@ def _prepared(owner, name: str, params, make):
         _prep_cache.clear()
     _prep_cache[slot] = (key, val)
     return val
+
+
+def _encoder_weights(enc, layers):
+    """bf16-rounded float32 (w0, wp, bp) of layer 0, bf16 lin weights of the
+    later layers: one trx_bf16_round launch."""
+    l0, ip = layers[0], enc.input_proj
+    w0, wp, bp = (torch.empty_like(l0.lin.weight), torch.empty_like(ip.weight), torch.empty_like(ip.bias))
+    pairs = [(l0.lin.weight, w0), (ip.weight, wp), (ip.bias, bp)]
+    out = [(w0, wp, bp)]
+    for l in layers[1:]:
+        w = torch.empty(l.lin.weight.shape, device=w0.device, dtype=torch.bfloat16)
+        pairs.append((l.lin.weight, w))
+        out.append(w)
+    _round_into(pairs)
+    return out
+
+
+def _head_weights(head):
+    """(w_nodes bf16 [2H, d], W_ctx^T bf16 view, we, w2, b2 bf16-rounded float32): one launch."""
+    W1, b1 = head.edge_mlp[0].weight, head.edge_mlp[0].bias
+    d, k = head.embed, head.edge_in
+    hid = W1.shape[0]
+    dev = W1.device
+    wn = torch.empty(2 * hid, d, device=dev, dtype=torch.bfloat16)
+    wc = torch.empty(hid, W1.shape[1] - 2 * d - k, device=dev, dtype=torch.bfloat16)
+    we = torch.empty(hid, k, device=dev, dtype=torch.float32)
+    w2 = torch.empty(hid, device=dev, dtype=torch.float32)
+    b2 = torch.empty(1, device=dev, dtype=torch.float32)
+    _round_into([(W1[:, :d], wn[:hid]), (W1[:, d:2 * d], wn[hid:]), (W1[:, 2 * d + k:], wc),
+                 (W1[:, 2 * d:2 * d + k], we), (head.edge_mlp[2].weight.reshape(-1), w2),
+                 (head.edge_mlp[2].bias.reshape(-1), b2)])
+    return wn, wc.t(), we, w2, b2
 
 
 def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology):
@@ -211,6 +263,9 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
         a_all = a_edge
     stride = a_all.shape[1]
     stream = _lib.stream_ptr(dev)
+    wts = _prepared(enc, "enc", [p for l in layers for p in (l.lin.weight,)] + [enc.input_proj.weight,
+                                                                                enc.input_proj.bias],
+                    lambda: _encoder_weights(enc, layers))
     prev_f32, prev_bf16 = None, None
     emb = ctx = None
     for i, l in enumerate(layers):
@@ -221,15 +276,12 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
         args.concat, args.max_graph_edges = int(l.concat), topo.max_graph_edges
         keep = []
         if i == 0:
-            ip = enc.input_proj
-            w0, wp, bp = _prepared(l, "l0", (l.lin.weight, ip.weight, ip.bias),
-                                   lambda: (_bf16r(l.lin.weight), _bf16r(ip.weight), _bf16r(ip.bias)))
+            w0, wp, bp = wts[0]
             keep += [w0, wp, bp]
             args.in_dim, args.x0, args.w0 = x.shape[1], x.data_ptr(), w0.data_ptr()
             args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
         else:
-            wl = _prepared(l, "lin", (l.lin.weight,), lambda: l.lin.weight.detach().to(torch.bfloat16))
-            xh = torch.mm(prev_bf16, wl.t())
+            xh = torch.mm(prev_bf16, wts[i].t())
             keep.append(xh)
             args.in_dim, args.xh = 0, xh.data_ptr()
             if last:
@@ -273,11 +325,8 @@ def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: 
     W1, b1 = head.edge_mlp[0].weight, head.edge_mlp[0].bias
     d, k = head.embed, head.edge_in
     hid = W1.shape[0]
-    w_nodes, wc, we, w2, b2 = _prepared(head, "edge", (W1, b1, head.edge_mlp[2].weight, head.edge_mlp[2].bias), lambda: (
-        torch.cat([W1[:, :d], W1[:, d:2 * d]], 0).detach().to(torch.bfloat16),
-        W1[:, 2 * d + k:].detach().to(torch.bfloat16).t(),
-        _bf16r(W1[:, 2 * d:2 * d + k]), _bf16r(head.edge_mlp[2].weight.reshape(-1)),
-        _bf16r(head.edge_mlp[2].bias.reshape(-1))))
+    w_nodes, wc, we, w2, b2 = _prepared(head, "edge", (W1, b1, head.edge_mlp[2].weight, head.edge_mlp[2].bias),
+                                        lambda: _head_weights(head))
     p = torch.mm(emb_bf16, w_nodes.t()).contiguous()                      # bf16 [N, 2*hid]
     c = (torch.mm(ctx.to(torch.bfloat16), wc) + b1).float().contiguous()  # autocast's bf16 GEMM + fp32 bias
     ea = edge_attr.float().contiguous()

@@ -476,11 +476,11 @@ class GATEncoder(nn.Module):
         attn = None
         shared = edge_attr is not None and all(l.lin_edge is not None for l in self.layers)
         a_all = self.edge_logits(edge_index, edge_attr, x.size(0)) if shared else None
-        off = 0
+        # torch.split: one cat in the backward instead of a zero-fill + copy per slice
+        a_layers = torch.split(a_all, [l.heads for l in self.layers], dim=1) if shared else None
         for i, layer in enumerate(self.layers):
             last = i == len(self.layers) - 1
-            ae = a_all[:, off:off + layer.heads] if shared else None
-            off += layer.heads
+            ae = a_layers[i] if shared else None
             norm = self.norms[i]
             F_out = layer.heads * layer.out_channels if layer.concat else layer.out_channels
             tail = (x.is_cuda and layer.bias is not None and norm.elementwise_affine and F_out % 4 == 0

@@ -19,7 +19,7 @@ LIB = os.path.join(PKG_DIR, "trafficrl", "libtrafficrl.so")
 def declared_symbols():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(trx_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(trx_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_exists_and_targets_gfx950():
