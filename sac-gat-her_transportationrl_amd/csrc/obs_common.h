@@ -38,21 +38,21 @@ __device__ float pairwise_any(const float* a, int n) {
 
 // One thread per env: bw [N] = normalised-by-networkx betweenness (float32,
 // before division by its max); prod = scratch of >= E floats.
-__device__ void obs_env_features(const DevGraph& g, const trx_state& s, int gb, const float* bw, float* prod,
-                                 float* __restrict__ node_x) {
+// goal / dmg / flow: the env's [E] rows (global memory, or LDS copies staged by the caller).
+__device__ void obs_env_features(const DevGraph& g, const trx_state& s, int gb, const float* goal, const float* dmg,
+                                 const float* flow, const float* bw, float* prod, float* __restrict__ node_x) {
     const int N = g.N, E = g.E;
-    const size_t eb = (size_t)gb * E;
     float bmax = 0.0f;
     for (int v = 0; v < N; ++v) bmax = fmaxf(bmax, bw[v]);
     // remaining goal ratio, avg undamaged flow (np.mean), log10 tstt (772-785)
-    for (int e = 0; e < E; ++e) prod[e] = __fmul_rn(s.goal[eb + e], s.damaged[eb + e]);
+    for (int e = 0; e < E; ++e) prod[e] = __fmul_rn(goal[e], dmg[e]);
     float rem = pairwise_any(prod, E);
-    for (int e = 0; e < E; ++e) prod[e] = s.goal[eb + e];
+    for (int e = 0; e < E; ++e) prod[e] = goal[e];
     float gtot = pairwise_any(prod, E);
     double remaining_ratio = (double)rem / ((double)gtot > 1.0 ? (double)gtot : 1.0);
     int nund = 0;
     for (int e = 0; e < E; ++e)
-        if (s.damaged[eb + e] == 0.0f) prod[nund++] = s.flow[eb + e];
+        if (dmg[e] == 0.0f) prod[nund++] = flow[e];
     double avg_flow = 0.0;
     if (nund > 0) {
         float sm = pairwise_any(prod, nund);

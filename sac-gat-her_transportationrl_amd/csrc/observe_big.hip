@@ -280,7 +280,9 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
         bw[v] = (float)b;
     }
     __syncthreads();
-    if (tid == 0) obs_env_features(g, s, gb, bw, reinterpret_cast<float*>(sigma_all), node_x);
+    if (tid == 0)
+        obs_env_features(g, s, gb, s.goal + (size_t)gb * g.E, s.damaged + (size_t)gb * g.E, s.flow + (size_t)gb * g.E, bw,
+                         reinterpret_cast<float*>(sigma_all), node_x);
     for (int e = tid; e < E; e += L) obs_edge_features(g, s, gb, e, edge_x, mask);
 }
 

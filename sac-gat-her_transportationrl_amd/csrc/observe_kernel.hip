@@ -37,10 +37,15 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     float* dmg = reinterpret_cast<float*>(queue + (((size_t)N * L + 15) & ~size_t(15)));
     uint8_t* insub = reinterpret_cast<uint8_t*>(dmg + (size_t)EPW * E);
     int* nsub = reinterpret_cast<int*>(insub + (((size_t)EPW * N + 15) & ~size_t(15)));
+    float* goal_l = reinterpret_cast<float*>(nsub + 16);  // [EPW][E] staged for the per-env features
+    float* flow_l = goal_l + (size_t)EPW * E;             // [EPW][E]
 
     for (int i = tid; i < EPW * E; i += L) {
         int el = i / E, gb = env0 + el;
-        dmg[i] = gb < B ? s.damaged[(size_t)gb * E + (i - el * E)] : 1.0f;
+        const size_t gi = (size_t)gb * E + (i - el * E);
+        dmg[i] = gb < B ? s.damaged[gi] : 1.0f;
+        goal_l[i] = gb < B ? s.goal[gi] : 0.0f;
+        flow_l[i] = gb < B ? s.flow[gi] : 0.0f;
     }
     __syncthreads();
     for (int i = tid; i < EPW * N; i += L) {
@@ -139,7 +144,8 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
 
     if (tid < EPW && env0 + tid < B) {
         // feature scratch reuses delta (>= E + 8 floats per env, checked at launch)
-        obs_env_features(g, s, env0 + tid, bwv + tid * N, reinterpret_cast<float*>(delta) + tid * (E + 8), node_x);
+        obs_env_features(g, s, env0 + tid, goal_l + tid * E, dmg + tid * E, flow_l + tid * E, bwv + tid * N,
+                         reinterpret_cast<float*>(delta) + tid * (E + 8), node_x);
     }
     for (int i = tid; i < EPW * E; i += L) {
         int el = i / E, e = i - el * E, gb = env0 + el;
@@ -152,6 +158,7 @@ static size_t observe_smem(const DevGraph& g, int epw) {
     size_t b = n * 8 * 2 + n * 2 + ((n + 15) & ~size_t(15));
     b += (size_t)epw * g.E * 4;
     b += (((size_t)epw * g.N + 15) & ~size_t(15)) + 16 * 4;
+    b += (size_t)epw * g.E * 4 * 2;  // goal / flow staged for the per-env features
     // the feature scratch reuses delta: needs epw*(E+8) floats <= N*L doubles
     return b;
 }
