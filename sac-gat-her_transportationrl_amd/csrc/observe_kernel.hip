@@ -39,6 +39,25 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     int* nsub = reinterpret_cast<int*>(insub + (((size_t)EPW * N + 15) & ~size_t(15)));
     float* goal_l = reinterpret_cast<float*>(nsub + 16);  // [EPW][E] staged for the per-env features
     float* flow_l = goal_l + (size_t)EPW * E;             // [EPW][E]
+    // the graph's adjacency (read in every BFS step) staged as int16
+    int16_t* gop = reinterpret_cast<int16_t*>(flow_l + (size_t)EPW * E);  // out_ptr [N+1]
+    int16_t* gip = gop + (N + 1);                                          // in_ptr  [N+1]
+    int16_t* goe = gip + (N + 1);                                          // out_eid [E]
+    int16_t* god = goe + E;                                                // out_dst [E]
+    int16_t* gie = god + E;                                                // in_eid  [E]
+    int16_t* gis = gie + E;                                                // in_src  [E]
+    int16_t* gnx = gis + E;                                                // nx_order [N]
+    for (int i = tid; i <= N; i += L) {
+        gop[i] = (int16_t)g.out_ptr[i];
+        gip[i] = (int16_t)g.in_ptr[i];
+    }
+    for (int i = tid; i < E; i += L) {
+        goe[i] = (int16_t)g.out_eid[i];
+        god[i] = (int16_t)g.out_dst[i];
+        gie[i] = (int16_t)g.in_eid[i];
+        gis[i] = (int16_t)g.in_src[i];
+    }
+    for (int i = tid; i < N; i += L) gnx[i] = (int16_t)g.nx_order[i];
 
     for (int i = tid; i < EPW * E; i += L) {
         int el = i / E, gb = env0 + el;
@@ -51,8 +70,8 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     for (int i = tid; i < EPW * N; i += L) {
         int el = i / N, v = i - el * N;
         int in = 0;
-        for (int j = g.out_ptr[v]; j < g.out_ptr[v + 1] && !in; ++j) in = dmg[el * E + g.out_eid[j]] == 0.0f;
-        for (int j = g.in_ptr[v]; j < g.in_ptr[v + 1] && !in; ++j) in = dmg[el * E + g.in_eid[j]] == 0.0f;
+        for (int j = gop[v]; j < gop[v + 1] && !in; ++j) in = dmg[el * E + goe[j]] == 0.0f;
+        for (int j = gip[v]; j < gip[v + 1] && !in; ++j) in = dmg[el * E + gie[j]] == 0.0f;
         insub[i] = (uint8_t)in;
     }
     __syncthreads();
@@ -65,7 +84,7 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     // ---------------- Brandes from source = nx_order[j] for lane (env, j)
     const int lenv = tid / N, j = tid - lenv * N;
     const bool on = lenv < EPW && env0 + lenv < B;
-    const int src = on ? g.nx_order[j] : 0;
+    const int src = on ? gnx[j] : 0;
     const bool active_src = on && insub[lenv * N + src];
     if (on) {
         for (int v = 0; v < N; ++v) {
@@ -84,9 +103,9 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
             int v = queue[qh++ * L + tid];
             int dv = dist[v * L + tid];
             double sv = sigma[v * L + tid];
-            for (int k = g.out_ptr[v]; k < g.out_ptr[v + 1]; ++k) {
-                if (dm[g.out_eid[k]] != 0.0f) continue;  // only active edges are in the subgraph
-                int w = g.out_dst[k];
+            for (int k = gop[v]; k < gop[v + 1]; ++k) {
+                if (dm[goe[k]] != 0.0f) continue;  // only active edges are in the subgraph
+                int w = god[k];
                 int dw = dist[w * L + tid];
                 if (dw < 0) {
                     queue[qt++ * L + tid] = (uint8_t)w;
@@ -101,9 +120,9 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
             int w = queue[q * L + tid];
             double coeff = (1.0 + delta[w * L + tid]) / sigma[w * L + tid];
             int dw = dist[w * L + tid];
-            for (int k = g.in_ptr[w]; k < g.in_ptr[w + 1]; ++k) {
-                if (dm[g.in_eid[k]] != 0.0f) continue;
-                int v = g.in_src[k];
+            for (int k = gip[w]; k < gip[w + 1]; ++k) {
+                if (dm[gie[k]] != 0.0f) continue;
+                int v = gis[k];
                 if (dist[v * L + tid] >= 0 && dist[v * L + tid] == dw - 1)
                     delta[v * L + tid] += sigma[v * L + tid] * coeff;
             }
@@ -121,7 +140,7 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
         double bc = 0.0;
         if (env0 + el < B && insub[i]) {
             for (int jj = 0; jj < N; ++jj) {
-                int s_ = g.nx_order[jj];
+                int s_ = gnx[jj];
                 int lane = el * N + jj;
                 if (s_ == w || !insub[el * N + s_]) continue;
                 if (dist[w * L + lane] < 0) continue;
@@ -159,6 +178,7 @@ static size_t observe_smem(const DevGraph& g, int epw) {
     b += (size_t)epw * g.E * 4;
     b += (((size_t)epw * g.N + 15) & ~size_t(15)) + 16 * 4;
     b += (size_t)epw * g.E * 4 * 2;  // goal / flow staged for the per-env features
+    b += ((size_t)2 * (g.N + 1) + 4 * (size_t)g.E + g.N) * 2 + 16;  // int16 adjacency
     // the feature scratch reuses delta: needs epw*(E+8) floats <= N*L doubles
     return b;
 }
