@@ -93,9 +93,12 @@ class DeviceReplay:
         self.size = 0
         self.size_t = torch.zeros((), dtype=torch.float64, device=dev)  # device copy for graph-captured sampling
 
-    def _set(self, idx: torch.Tensor, leaf: torch.Tensor):
+    def _set(self, idx: torch.Tensor, leaf: torch.Tensor, distinct: bool = False):
+        """distinct: the caller guarantees no repeated index (ring-buffer adds of
+        at most `capacity` entries), so no last-wins resolution is needed."""
         idx = idx.contiguous()
-        leaf = _last_wins(idx, leaf.to(torch.float64)).contiguous()
+        leaf = leaf.to(torch.float64)
+        leaf = (leaf if distinct else _last_wins(idx, leaf)).contiguous()
         L = _lib.load()
         _lib.check(L.trx_per_update(_lib.ptr(self.tree), self.capacity, _lib.ptr(idx), _lib.ptr(leaf), idx.numel(),
                                     _lib.stream_ptr(self.device)), "trx_per_update")
@@ -108,20 +111,21 @@ class DeviceReplay:
                   prev_tstt, next_tstt, init_tstt):
         B = action.shape[0]
         idx = (self.ptr + torch.arange(B, device=self.device)) % self.capacity
-        for dst, src in ((self.node_x, node_x), (self.edge_x, edge_x), (self.mask, mask),
-                         (self.next_node_x, next_node_x), (self.next_edge_x, next_edge_x),
-                         (self.next_mask, next_mask), (self.goal, goal)):
-            dst.index_copy_(0, idx, src.to(dst.dtype))
-        self.action.index_copy_(0, idx, action.to(torch.int64))
-        self.reward.index_copy_(0, idx, reward.to(torch.float32))
-        self.done.index_copy_(0, idx, done.to(torch.float32))
-        self.prev_tstt.index_copy_(0, idx, prev_tstt.to(torch.float64))
-        self.next_tstt.index_copy_(0, idx, next_tstt.to(torch.float64))
-        self.init_tstt.index_copy_(0, idx, init_tstt.to(torch.float64))
+        pairs = ((self.node_x, node_x), (self.edge_x, edge_x), (self.mask, mask), (self.next_node_x, next_node_x),
+                 (self.next_edge_x, next_edge_x), (self.next_mask, next_mask), (self.goal, goal),
+                 (self.action, action), (self.reward, reward), (self.done, done), (self.prev_tstt, prev_tstt),
+                 (self.next_tstt, next_tstt), (self.init_tstt, init_tstt))
+        if self.ptr + B <= self.capacity:
+            # contiguous slots: one multi-tensor copy instead of an index_copy per field
+            torch._foreach_copy_([dst[self.ptr:self.ptr + B] for dst, _ in pairs],
+                                 [src.reshape(dst[self.ptr:self.ptr + B].shape).to(dst.dtype) for dst, src in pairs])
+        else:
+            for dst, src in pairs:
+                dst.index_copy_(0, idx, src.reshape((B,) + dst.shape[1:]).to(dst.dtype))
         # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
         pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
         self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
-        self._set(idx, pr ** self.alpha)
+        self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)
         self.ptr = (self.ptr + B) % self.capacity
         self.size = min(self.size + B, self.capacity)
         self.size_t.fill_(float(self.size))
