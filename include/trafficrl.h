@@ -388,6 +388,19 @@ typedef struct trx_round_list {
 } trx_round_list;
 int trx_bf16_round(const trx_round_list* l, void* stream);
 
+/* ------------------------------------------------------ multi-buffer copy
+ * dst[k][0:bytes[k]) = src[k][0:bytes[k]) for up to TRX_MAX_COPY device
+ * buffers in one launch (non-overlapping).  The trainer's replay-ring writes
+ * (src/train.py:27-58 ReplayBuffer.add, vectorised over the envs).         */
+#define TRX_MAX_COPY 16
+typedef struct trx_copy_list {
+    int32_t count, _pad;
+    int64_t bytes[TRX_MAX_COPY];
+    const void* src[TRX_MAX_COPY];
+    void* dst[TRX_MAX_COPY];
+} trx_copy_list;
+int trx_multi_copy(const trx_copy_list* l, void* stream);
+
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
  * (passed as void*) into an equivalent fill-kernel node with the same

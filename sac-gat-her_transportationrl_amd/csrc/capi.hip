@@ -727,6 +727,16 @@ int trx_bf16_round(const trx_round_list* l, void* stream) {
     return TRX_OK;
 }
 
+int trx_multi_copy(const trx_copy_list* l, void* stream) {
+    if (!l || l->count < 0 || l->count > TRX_MAX_COPY) return fail(TRX_EINVAL, "multi_copy: count must be 0..16");
+    for (int k = 0; k < l->count; ++k)
+        if (!l->src[k] || !l->dst[k] || l->bytes[k] < 0) return fail(TRX_EINVAL, "multi_copy: bad entry %d", k);
+    if (l->count == 0) return TRX_OK;
+    hipError_t e = trx::launch_multi_copy(*l, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "multi_copy launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
     if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
     int n = 0;

@@ -94,3 +94,36 @@ hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream) {
     return hipGetLastError();
 }
 }  // namespace trx
+
+// ------------------------------------------------------------------------
+// Multi-buffer device copy (trx_multi_copy): the trainer writes ~13 fields of
+// every step's transitions into the replay ring; one launch instead of one
+// memcpy / index_copy each.
+namespace trx {
+namespace {
+__global__ void __launch_bounds__(256) multi_copy_kernel(trx_copy_list l) {
+    const int k = blockIdx.y;
+    if (k >= l.count) return;
+    const char* src = static_cast<const char*>(l.src[k]);
+    char* dst = static_cast<char*>(l.dst[k]);
+    const int64_t nb = l.bytes[k];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    if ((((uintptr_t)src | (uintptr_t)dst | (uintptr_t)nb) & 15) == 0) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src);
+        uint4* d4 = reinterpret_cast<uint4*>(dst);
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb / 16; i += stride) d4[i] = s4[i];
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
+    }
+}
+}  // namespace
+
+hipError_t launch_multi_copy(const trx_copy_list& l, hipStream_t stream) {
+    int64_t mx = 16;
+    for (int k = 0; k < l.count; ++k) mx = l.bytes[k] > mx ? l.bytes[k] : mx;
+    const int64_t blocks = (mx / 16 + 255) / 256;
+    const unsigned bx = (unsigned)(blocks < 512 ? (blocks > 0 ? blocks : 1) : 512);
+    hipLaunchKernelGGL(multi_copy_kernel, dim3(bx, l.count), dim3(256), 0, stream, l);
+    return hipGetLastError();
+}
+}  // namespace trx

@@ -26,7 +26,7 @@ EXPORTS = (
     "trx_edge_head_infer", "trx_gat_prologue_infer", "trx_layer_tail_forward", "trx_layer_tail_workspace_floats",
     "trx_layer_tail_backward", "trx_att_dots_forward", "trx_att_dots_workspace_floats", "trx_att_dots_backward",
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
-    "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round",
+    "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
 )
 
 
@@ -124,6 +124,27 @@ class TrxRoundList(ctypes.Structure):
     ]
 
 
+MAX_COPY = 16
+
+
+class TrxCopyList(ctypes.Structure):
+    """trx_copy_list (include/trafficrl.h)."""
+    _fields_ = [("count", _i32), ("_pad", _i32), ("bytes", ctypes.c_int64 * MAX_COPY), ("src", _vp * MAX_COPY),
+                ("dst", _vp * MAX_COPY)]
+
+
+def multi_copy(pairs, device):
+    """One trx_multi_copy launch for [(dst, src), ...] (contiguous, same dtype and size)."""
+    L = load()
+    lst = TrxCopyList()
+    lst.count = len(pairs)
+    for k, (dst, src) in enumerate(pairs):
+        assert dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype and dst.numel() == src.numel()
+        lst.bytes[k] = dst.numel() * dst.element_size()
+        lst.src[k], lst.dst[k] = src.data_ptr(), dst.data_ptr()
+    check(L.trx_multi_copy(lst, stream_ptr(device)), "trx_multi_copy")
+
+
 class TrafficRLError(RuntimeError):
     pass
 
@@ -168,6 +189,7 @@ def load():
     L.trx_edge_head_backward.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_graph_pool_forward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp]
     L.trx_bf16_round.argtypes = [ctypes.POINTER(TrxRoundList), _vp]
+    L.trx_multi_copy.argtypes = [ctypes.POINTER(TrxCopyList), _vp]
     L.trx_graph_pool_backward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_layer_tail_forward.argtypes = [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]
     L.trx_att_dots_forward.argtypes = [_i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]
@@ -188,7 +210,7 @@ def load():
                  "trx_layer_tail_forward", "trx_layer_tail_backward", "trx_att_dots_forward",
                  "trx_att_dots_backward", "trx_small_ln_forward", "trx_small_ln_backward",
                  "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward",
-                 "trx_bf16_round"):
+                 "trx_bf16_round", "trx_multi_copy"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

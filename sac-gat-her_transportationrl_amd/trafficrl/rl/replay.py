@@ -103,6 +103,49 @@ class DeviceReplay:
         _lib.check(L.trx_per_update(_lib.ptr(self.tree), self.capacity, _lib.ptr(idx), _lib.ptr(leaf), idx.numel(),
                                     _lib.stream_ptr(self.device)), "trx_per_update")
 
+    def _write(self, idx, pairs, B: int):
+        """Rows [ptr, ptr + B) of each (buffer, values) pair: one trx_multi_copy
+        launch when the slots are contiguous, index_copy otherwise."""
+        if self.ptr + B <= self.capacity and self.device.type == "cuda":
+            _lib.multi_copy([(dst[self.ptr:self.ptr + B],
+                              src.reshape((B,) + dst.shape[1:]).to(dst.dtype).contiguous()) for dst, src in pairs],
+                            self.device)
+        else:
+            for dst, src in pairs:
+                dst.index_copy_(0, idx, src.reshape((B,) + dst.shape[1:]).to(dst.dtype))
+
+    def stage_prev(self, node_x, edge_x, mask, goal, prev_tstt) -> bool:
+        """Write the pre-step fields of the next B transitions into their ring
+        slots now -- before env.step overwrites the observation buffers, so no
+        clones are needed.  add_staged() completes them; False (nothing
+        written) when the slots would wrap: use add_batch then."""
+        B = node_x.shape[0]
+        if self.ptr + B > self.capacity or self.device.type != "cuda":
+            return False
+        self._write(None, ((self.node_x, node_x), (self.edge_x, edge_x), (self.mask, mask), (self.goal, goal),
+                           (self.prev_tstt, prev_tstt)), B)
+        self._staged = B
+        return True
+
+    def add_staged(self, action, reward, next_node_x, next_edge_x, next_mask, done, next_tstt, init_tstt):
+        B = action.shape[0]
+        assert getattr(self, "_staged", None) == B, "stage_prev() first"
+        self._staged = None
+        idx = (self.ptr + torch.arange(B, device=self.device)) % self.capacity
+        self._write(idx, ((self.action, action), (self.reward, reward), (self.next_node_x, next_node_x),
+                          (self.next_edge_x, next_edge_x), (self.next_mask, next_mask), (self.done, done),
+                          (self.next_tstt, next_tstt), (self.init_tstt, init_tstt)), B)
+        self._priorities_for_new(idx, B)
+
+    def _priorities_for_new(self, idx, B: int):
+        # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
+        pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
+        self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
+        self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)
+        self.ptr = (self.ptr + B) % self.capacity
+        self.size = min(self.size + B, self.capacity)
+        self.size_t.fill_(float(self.size))
+
     @property
     def total(self) -> torch.Tensor:
         return self.tree[1]
@@ -115,20 +158,8 @@ class DeviceReplay:
                  (self.next_edge_x, next_edge_x), (self.next_mask, next_mask), (self.goal, goal),
                  (self.action, action), (self.reward, reward), (self.done, done), (self.prev_tstt, prev_tstt),
                  (self.next_tstt, next_tstt), (self.init_tstt, init_tstt))
-        if self.ptr + B <= self.capacity:
-            # contiguous slots: one multi-tensor copy instead of an index_copy per field
-            torch._foreach_copy_([dst[self.ptr:self.ptr + B] for dst, _ in pairs],
-                                 [src.reshape(dst[self.ptr:self.ptr + B].shape).to(dst.dtype) for dst, src in pairs])
-        else:
-            for dst, src in pairs:
-                dst.index_copy_(0, idx, src.reshape((B,) + dst.shape[1:]).to(dst.dtype))
-        # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
-        pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
-        self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
-        self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)
-        self.ptr = (self.ptr + B) % self.capacity
-        self.size = min(self.size + B, self.capacity)
-        self.size_t.fill_(float(self.size))
+        self._write(idx, pairs, B)
+        self._priorities_for_new(idx, B)
 
     def sample(self, batch_size: int, generator: Optional[torch.Generator] = None,
                u: Optional[torch.Tensor] = None) -> Sample:

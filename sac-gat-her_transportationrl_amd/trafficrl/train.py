@@ -326,16 +326,23 @@ class Trainer:
     def iteration(self, obs, it: int):
         cfg, env = self.cfg, self.env
         actions = self.act(obs)
-        prev_obs = (obs.node_x.clone(), obs.edge_x.clone(), obs.action_mask.clone())
-        goal = env.goal.clone()
-        prev_tstt = env.tstt.clone()
+        # pre-step fields go straight into the replay ring (no clones) unless the slots wrap
+        staged = self.replay.stage_prev(obs.node_x, obs.edge_x, obs.action_mask, env.goal, env.tstt)
+        if not staged:
+            prev_obs = (obs.node_x.clone(), obs.edge_x.clone(), obs.action_mask.clone())
+            goal = env.goal.clone()
+            prev_tstt = env.tstt.clone()
         next_obs, reward, done, info = env.step(actions.to(torch.int32), check=False)
         scaled = reward * cfg["reward_scale"]
         self.ep_len += 1
         trunc = (self.ep_len >= int(cfg["max_steps"])) if cfg["max_steps"] > 0 else torch.zeros_like(done)
-        self.replay.add_batch(prev_obs[0], prev_obs[1], prev_obs[2], actions, scaled, next_obs.node_x,
-                              next_obs.edge_x, next_obs.action_mask, done.float(), goal, prev_tstt, env.tstt,
-                              env.initial_tstt)
+        if staged:
+            self.replay.add_staged(actions, scaled, next_obs.node_x, next_obs.edge_x, next_obs.action_mask,
+                                   done.float(), env.tstt, env.initial_tstt)
+        else:
+            self.replay.add_batch(prev_obs[0], prev_obs[1], prev_obs[2], actions, scaled, next_obs.node_x,
+                                  next_obs.edge_x, next_obs.action_mask, done.float(), goal, prev_tstt, env.tstt,
+                                  env.initial_tstt)
         self.ep_reward += scaled
         self.ep_tstt_sum += env.tstt
         self.ep_auc += 0.5 * (self.ep_prev_tstt + env.tstt) * (self.ep_len > 1)

@@ -71,6 +71,32 @@ def test_add_priorities_and_last_wins():
     assert bool((s.idx < B).all())
 
 
+def test_staged_add_equals_add_batch():
+    """Trainer path: stage_prev() before the env step + add_staged() after it
+    (one multi-copy launch each, no clones) leaves the same ring contents and
+    sum tree as add_batch(), including the wrap-around fallback."""
+    from trafficrl.rl.replay import DeviceReplay
+    g = torch.Generator(device="cuda").manual_seed(5)
+    r = lambda *s: torch.rand(*s, device="cuda", generator=g)  # noqa: E731
+    a, b = DeviceReplay(24, 24, 76, device="cuda"), DeviceReplay(24, 24, 76, device="cuda")
+    for B in (10, 10, 10):          # the third add wraps (ptr 20 + 10 > 24)
+        f = dict(node_x=r(B, 24, 4), edge_x=r(B, 76, 6), mask=r(B, 76), goal=r(B, 76),
+                 prev=r(B).double(), action=torch.randint(0, 76, (B,), device="cuda", dtype=torch.int32),
+                 reward=r(B).double(), nnx=r(B, 24, 4), nex=r(B, 76, 6), nm=r(B, 76), done=(r(B) > 0.5),
+                 nt=r(B).double(), it=r(B).double())
+        a.add_batch(f["node_x"], f["edge_x"], f["mask"], f["action"], f["reward"], f["nnx"], f["nex"], f["nm"],
+                    f["done"].float(), f["goal"], f["prev"], f["nt"], f["it"])
+        if b.stage_prev(f["node_x"], f["edge_x"], f["mask"], f["goal"], f["prev"]):
+            b.add_staged(f["action"], f["reward"], f["nnx"], f["nex"], f["nm"], f["done"].float(), f["nt"], f["it"])
+        else:
+            b.add_batch(f["node_x"], f["edge_x"], f["mask"], f["action"], f["reward"], f["nnx"], f["nex"], f["nm"],
+                        f["done"].float(), f["goal"], f["prev"], f["nt"], f["it"])
+    for name in ("node_x", "edge_x", "mask", "next_node_x", "next_edge_x", "next_mask", "goal", "action", "reward",
+                 "done", "prev_tstt", "next_tstt", "init_tstt", "tree", "max_priority"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert (a.ptr, a.size) == (b.ptr, b.size)
+
+
 def test_her_relabel_quirks():
     from trafficrl.rl.replay import DeviceReplay, her_relabel
     rb = DeviceReplay(8, 24, 76, device="cuda")
