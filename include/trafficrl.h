@@ -315,6 +315,11 @@ int trx_per_update(double* tree, int64_t capacity, const int64_t* idx, const dou
                    void* stream);
 int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
                    double* out_priority, void* stream);
+/* trx_per_update for the contiguous leaves lo .. lo+n-1 (lo + n <= capacity):
+ * the ring-buffer add of n new transitions; same tree values as trx_per_update
+ * with idx = lo + k, each touched ancestor recomputed once per level.      */
+int trx_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* priority, int32_t n,
+                         void* stream);
 
 /* ------------------------------------------------ GAT layer tail (training)
  * The autograd path's post-aggregation tail of a GATEncoder layer

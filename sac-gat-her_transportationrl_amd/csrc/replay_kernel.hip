@@ -43,6 +43,33 @@ __global__ void __launch_bounds__(1024) per_update_kernel(double* __restrict__ t
     }
 }
 
+// Contiguous leaf range [lo, lo + n) (ring-buffer adds): the ancestors touched at
+// level l are exactly the contiguous range ((capacity + lo) >> l, (capacity + lo + n
+// - 1) >> l), so each level recomputes its distinct nodes once -- the same node
+// updates, in the same level order, as per_update_kernel, without its per-leaf
+// redundancy (n / 2^l nodes at level l instead of n).
+__global__ void __launch_bounds__(1024) per_update_range_kernel(double* __restrict__ tree, int64_t capacity,
+                                                                int64_t lo, const double* __restrict__ pri, int n) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) tree[capacity + lo + k] = pri[k];
+    __syncthreads();
+    int64_t top = 2 * capacity - 1;
+    int levels = 0;
+    while ((top >> levels) > 1) ++levels;
+    for (int l = 1; l <= levels; ++l) {
+        const int64_t a = (capacity + lo) >> l, b = (capacity + lo + n - 1) >> l;
+        for (int64_t node = a + threadIdx.x; node <= b; node += blockDim.x) {
+            if (node >= 1) {
+                const int64_t c0 = 2 * node, c1 = 2 * node + 1;
+                const double va = c0 < 2 * capacity ? tree[c0] : 0.0;
+                const double vb = c1 < 2 * capacity ? tree[c1] : 0.0;
+                tree[node] = va + vb;
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+    }
+}
+
 __global__ void per_sample_kernel(const double* __restrict__ tree, int64_t capacity, const double* __restrict__ u,
                                   int n, int64_t* __restrict__ out_idx, double* __restrict__ out_pri) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -67,6 +94,13 @@ hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx,
                              hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(per_update_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, idx, pri, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* pri, int n,
+                                   hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(per_update_range_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, lo, pri, n);
     return hipGetLastError();
 }
 

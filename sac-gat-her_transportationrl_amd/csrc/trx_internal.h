@@ -175,6 +175,8 @@ size_t gat_prologue_smem(const trx_gat_prologue_args& a);
 hipError_t patch_graph_memsets(hipGraph_t graph, int* n_patched);
 hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* pri, int n,
                              hipStream_t stream);
+hipError_t launch_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* pri, int n,
+                                   hipStream_t stream);
 hipError_t launch_per_sample(const double* tree, int64_t capacity, const double* u, int n, int64_t* out_idx,
                              double* out_pri, hipStream_t stream);
 

@@ -141,7 +141,13 @@ class DeviceReplay:
         # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
         pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
         self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
-        self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)
+        if self.ptr + B <= self.capacity and self.device.type == "cuda":
+            leaf = (pr ** self.alpha).contiguous()
+            L = _lib.load()
+            _lib.check(L.trx_per_update_range(_lib.ptr(self.tree), self.capacity, self.ptr, _lib.ptr(leaf), B,
+                                              _lib.stream_ptr(self.device)), "trx_per_update_range")
+        else:
+            self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)
         self.ptr = (self.ptr + B) % self.capacity
         self.size = min(self.size + B, self.capacity)
         self.size_t.fill_(float(self.size))

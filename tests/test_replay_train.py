@@ -71,6 +71,25 @@ def test_add_priorities_and_last_wins():
     assert bool((s.idx < B).all())
 
 
+@pytest.mark.parametrize("cap,lo,n", [(1000, 0, 1000), (1000, 377, 500), (65536, 61440, 4096), (24, 20, 4),
+                                      (1_000_000, 995_904, 4096)])
+def test_per_update_range_equals_general(cap, lo, n):
+    """trx_per_update_range (ring adds) leaves the same float64 tree, bit for
+    bit, as trx_per_update with idx = lo..lo+n-1 -- also for capacities that
+    are not powers of two (leaves at two depths)."""
+    from trafficrl import _lib
+    L = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(cap + lo)
+    base = torch.rand(2 * cap, device="cuda", dtype=torch.float64, generator=g)
+    t1, t2 = base.clone(), base.clone()
+    pri = torch.rand(n, device="cuda", dtype=torch.float64, generator=g) + 0.5
+    idx = torch.arange(lo, lo + n, device="cuda", dtype=torch.int64)
+    _lib.check(L.trx_per_update(_lib.ptr(t1), cap, _lib.ptr(idx), _lib.ptr(pri), n, None), "general")
+    _lib.check(L.trx_per_update_range(_lib.ptr(t2), cap, lo, _lib.ptr(pri), n, None), "range")
+    torch.cuda.synchronize()
+    assert torch.equal(t1, t2)
+
+
 def test_staged_add_equals_add_batch():
     """Trainer path: stage_prev() before the env step + add_staged() after it
     (one multi-copy launch each, no clones) leaves the same ring contents and
