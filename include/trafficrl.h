@@ -320,6 +320,12 @@ int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_
  * with idx = lo + k, each touched ancestor recomputed once per level.      */
 int trx_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* priority, int32_t n,
                          void* stream);
+/* The ring add of n new transitions at leaves lo .. lo+n-1 (lo + n <= capacity)
+ * as n sequential reference adds (src/train.py:50-58): leaf k = (max_p + eps *
+ * (k+1)) ** alpha with max_p = *max_priority on entry; *max_priority becomes
+ * max_p + eps * n.  One launch (the ancestors as in trx_per_update_range).  */
+int trx_per_add_range(double* tree, int64_t capacity, int64_t lo, int32_t n, double* max_priority, double eps,
+                      double alpha, void* stream);
 
 /* ------------------------------------------------ GAT layer tail (training)
  * The autograd path's post-aggregation tail of a GATEncoder layer

@@ -505,6 +505,16 @@ int trx_per_update_range(double* tree, int64_t capacity, int64_t lo, const doubl
     return TRX_OK;
 }
 
+int trx_per_add_range(double* tree, int64_t capacity, int64_t lo, int32_t n, double* max_priority, double eps,
+                      double alpha, void* stream) {
+    if (!tree || !max_priority || capacity < 1 || n < 0 || lo < 0 || lo + n > capacity)
+        return fail(TRX_EINVAL, "per_add_range: need 0 <= lo, lo + n <= capacity");
+    hipError_t e = trx::launch_per_add_range(tree, capacity, lo, n, max_priority, eps, alpha,
+                                             static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "per_add_range launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
                    double* out_priority, void* stream) {
     if (!tree || capacity <= 0 || n < 0 || (n > 0 && (!u || !out_idx || !out_priority)))

@@ -48,9 +48,20 @@ __global__ void __launch_bounds__(1024) per_update_kernel(double* __restrict__ t
 // - 1) >> l), so each level recomputes its distinct nodes once -- the same node
 // updates, in the same level order, as per_update_kernel, without its per-leaf
 // redundancy (n / 2^l nodes at level l instead of n).
+// max_priority != NULL: the ring add itself (src/train.py:50-58 applied n times):
+// leaf k = (max_p + eps * (k + 1)) ** alpha, then max_p += ... (written last).
 __global__ void __launch_bounds__(1024) per_update_range_kernel(double* __restrict__ tree, int64_t capacity,
-                                                                int64_t lo, const double* __restrict__ pri, int n) {
-    for (int k = threadIdx.x; k < n; k += blockDim.x) tree[capacity + lo + k] = pri[k];
+                                                                int64_t lo, const double* __restrict__ pri, int n,
+                                                                double* __restrict__ max_priority, double eps,
+                                                                double alpha) {
+    if (max_priority) {
+        const double mp = *max_priority;
+        for (int k = threadIdx.x; k < n; k += blockDim.x) tree[capacity + lo + k] = pow(mp + eps * (double)(k + 1), alpha);
+        __syncthreads();
+        if (threadIdx.x == 0) *max_priority = mp + eps * (double)n;
+    } else {
+        for (int k = threadIdx.x; k < n; k += blockDim.x) tree[capacity + lo + k] = pri[k];
+    }
     __syncthreads();
     int64_t top = 2 * capacity - 1;
     int levels = 0;
@@ -100,7 +111,16 @@ hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx,
 hipError_t launch_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* pri, int n,
                                    hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(per_update_range_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, lo, pri, n);
+    hipLaunchKernelGGL(per_update_range_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, lo, pri, n,
+                       static_cast<double*>(nullptr), 0.0, 0.0);
+    return hipGetLastError();
+}
+
+hipError_t launch_per_add_range(double* tree, int64_t capacity, int64_t lo, int n, double* max_priority, double eps,
+                                double alpha, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(per_update_range_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, lo,
+                       static_cast<const double*>(nullptr), n, max_priority, eps, alpha);
     return hipGetLastError();
 }
 

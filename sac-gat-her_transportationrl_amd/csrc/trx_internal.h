@@ -177,6 +177,8 @@ hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx,
                              hipStream_t stream);
 hipError_t launch_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* pri, int n,
                                    hipStream_t stream);
+hipError_t launch_per_add_range(double* tree, int64_t capacity, int64_t lo, int n, double* max_priority, double eps,
+                                double alpha, hipStream_t stream);
 hipError_t launch_per_sample(const double* tree, int64_t capacity, const double* u, int n, int64_t* out_idx,
                              double* out_pri, hipStream_t stream);
 

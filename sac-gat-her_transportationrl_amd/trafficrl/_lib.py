@@ -27,7 +27,7 @@ EXPORTS = (
     "trx_layer_tail_backward", "trx_att_dots_forward", "trx_att_dots_workspace_floats", "trx_att_dots_backward",
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
-    "trx_per_update_range",
+    "trx_per_update_range", "trx_per_add_range",
 )
 
 
@@ -192,6 +192,8 @@ def load():
     L.trx_bf16_round.argtypes = [ctypes.POINTER(TrxRoundList), _vp]
     L.trx_multi_copy.argtypes = [ctypes.POINTER(TrxCopyList), _vp]
     L.trx_per_update_range.argtypes = [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _i32, _vp]
+    L.trx_per_add_range.argtypes = [_vp, ctypes.c_int64, ctypes.c_int64, _i32, _vp, ctypes.c_double, ctypes.c_double,
+                                    _vp]
     L.trx_graph_pool_backward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_layer_tail_forward.argtypes = [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]
     L.trx_att_dots_forward.argtypes = [_i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]
@@ -213,7 +215,7 @@ def load():
                  "trx_att_dots_backward", "trx_small_ln_forward", "trx_small_ln_backward",
                  "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward",
                  "trx_bf16_round", "trx_multi_copy",
-                 "trx_per_update_range"):
+                 "trx_per_update_range", "trx_per_add_range"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

@@ -139,14 +139,14 @@ class DeviceReplay:
 
     def _priorities_for_new(self, idx, B: int):
         # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
-        pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
-        self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
         if self.ptr + B <= self.capacity and self.device.type == "cuda":
-            leaf = (pr ** self.alpha).contiguous()
-            L = _lib.load()
-            _lib.check(L.trx_per_update_range(_lib.ptr(self.tree), self.capacity, self.ptr, _lib.ptr(leaf), B,
-                                              _lib.stream_ptr(self.device)), "trx_per_update_range")
+            L = _lib.load()     # one launch: leaves, ancestors and max_priority (updated in place)
+            _lib.check(L.trx_per_add_range(_lib.ptr(self.tree), self.capacity, self.ptr, B, _lib.ptr(self.max_priority),
+                                           float(self.eps), float(self.alpha), _lib.stream_ptr(self.device)),
+                       "trx_per_add_range")
         else:
+            pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
+            self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
             self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)
         self.ptr = (self.ptr + B) % self.capacity
         self.size = min(self.size + B, self.capacity)

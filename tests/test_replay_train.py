@@ -90,6 +90,30 @@ def test_per_update_range_equals_general(cap, lo, n):
     assert torch.equal(t1, t2)
 
 
+@pytest.mark.parametrize("cap,lo,n", [(24, 20, 4), (1000, 377, 500), (1_000_000, 995_904, 4096)])
+def test_per_add_range_equals_sequential_adds(cap, lo, n):
+    """trx_per_add_range (one launch: leaves, ancestors, max_priority) ==
+    n sequential reference adds (src/train.py:50-58): leaf k = (max_p +
+    (k+1)*eps)**alpha, max_p -> max_p + n*eps; tree sums consistent."""
+    from trafficrl import _lib
+    L = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(cap + n)
+    base = torch.rand(2 * cap, device="cuda", dtype=torch.float64, generator=g)
+    t1, t2 = base.clone(), base.clone()
+    mp = torch.tensor([1.75], device="cuda", dtype=torch.float64)
+    eps, alpha = 1e-6, 0.6
+    pri = (mp + eps * torch.arange(1, n + 1, device="cuda", dtype=torch.float64)) ** alpha
+    _lib.check(L.trx_per_update_range(_lib.ptr(t1), cap, lo, _lib.ptr(pri), n, None), "range")
+    mp2 = mp.clone()
+    _lib.check(L.trx_per_add_range(_lib.ptr(t2), cap, lo, n, _lib.ptr(mp2), eps, alpha, None), "add_range")
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(t2.cpu().numpy(), t1.cpu().numpy(), rtol=1e-14, atol=0)
+    assert mp2.item() == 1.75 + eps * n
+    leaves = t2[cap + lo:cap + lo + n].cpu().numpy()
+    expect = [(1.75 + (k + 1) * eps) ** alpha for k in range(n)]
+    np.testing.assert_allclose(leaves, expect, rtol=1e-14)
+
+
 def test_staged_add_equals_add_batch():
     """Trainer path: stage_prev() before the env step + add_staged() after it
     (one multi-copy launch each, no clones) leaves the same ring contents and
