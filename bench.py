@@ -72,10 +72,37 @@ def fixed_damage_mask(gd, seed=42, ratio=0.3):
     return DamageSampler(_G, 0, fixed_damage=True, fixed_damage_seed=seed).sample(ratio)
 
 
-def cpu_baseline(network, method, iters, seconds=12.0):
-    """Time the oracle's C restatement (same algorithm: scipy-order Dijkstra,
-    predecessor path walk, fp32 MSA/FW) on the host cores, warm-started
-    steps of the fixed-damage env (one assignment each)."""
+def host_cores():
+    """(cores this job may use, CPUs visible).  Usable = the CPU affinity set,
+    capped by the cgroup CPU quota and by OMP_NUM_THREADS when the launcher
+    sets it: a GPU box hands each 1-GPU job a 16-core share of a larger host
+    (nproc shows the whole host there), and the baseline uses all of that share."""
+    try:
+        vis = len(os.sched_getaffinity(0))
+    except AttributeError:
+        vis = os.cpu_count() or 1
+    n = vis
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n), vis
+
+
+def cpu_baseline(network, method, iters, seconds=12.0, sp="scipy"):
+    """Time the oracle's C restatement (same algorithm as the reference:
+    scipy-order Dijkstra or the torch rule's Floyd-Warshall, predecessor /
+    next-hop path walk, fp32 MSA/FW, then get_state with networkx-order
+    Brandes betweenness) on all host cores available to this process
+    (OpenMP over envs): warm-started env steps of the fixed-damage env, one
+    assignment + one observation each -- the same per-step env work as the
+    GPU env kernel + observe kernel.  The assignment-only rate is reported
+    beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # test/baseline infrastructure only
 
@@ -85,27 +112,73 @@ def cpu_baseline(network, method, iters, seconds=12.0):
     E = og.E
     dmg = fixed_damage_mask(load_network(network))
     cap = np.where(dmg > 0, np.float32(1e-3), gr["cap0"]).astype(np.float32)
-    f0, _, _, _ = og.assign(cap, dmg, np.zeros(E, np.float32), method=method, iters=iters)
-    threads = max(1, min(16, os.cpu_count() or 1, O.max_threads()))
+    f0, _, _, _ = og.assign(cap, dmg, np.zeros(E, np.float32), method=method, iters=iters, sp=sp)
+    threads, visible = host_cores()
     # repair one random damaged link per row, warm start from the reset flow
     rng = np.random.default_rng(7)
     B = (64 if network == "sf" else 4) * threads
     cand = np.where(dmg > 0)[0]
     C = np.repeat(cap[None], B, 0)
     D = np.repeat(dmg[None], B, 0)
+    G = D.copy()
     a = rng.choice(cand, B)
     C[np.arange(B), a] = gr["cap0"][a]
     D[np.arange(B), a] = 0.0
     F = np.repeat(f0[None], B, 0)
     done = 0
+    t_assign = t_obs = 0.0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        og.assign(C, D, F, method=method, iters=iters, nthreads=threads)
+        ta = time.perf_counter()
+        fo, _, ts, _ = og.assign(C, D, F, method=method, iters=iters, nthreads=threads, sp=sp)
+        tb = time.perf_counter()
+        og.observe(C, D, G, fo, ts, nthreads=threads)
+        t_obs += time.perf_counter() - tb
+        t_assign += tb - ta
         done += B
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "env steps/s", "cores": threads, "kind": "port",
-            "sample": f"{done} warm-started {method.upper()}-{iters} steps ({network}, fixed damage seed 42, one repaired "
-                      f"link each) in {dt:.1f}s on {threads} host threads; oracle/trx_oracle.c"}
+            "assign_only": done / t_assign, "host_cpus_visible": visible,
+            "sample": f"{done} warm-started {method.upper()}-{iters} env steps ({network}, {sp} shortest-path rule, "
+                      f"fixed damage seed 42, one repaired link each): assignment + get_state, in {dt:.1f}s on "
+                      f"{threads} host threads (all cores available to the process); assignment alone "
+                      f"{t_assign:.1f}s, get_state {t_obs:.1f}s; oracle/trx_oracle.c"}
+
+
+MFMA_PEAK_BF16 = 2.5e15  # MI355X_MICROARCH.md: dense bf16 MFMA peak (no sparsity)
+
+
+def gemm_mfma(rows, graphs, hidden=256, heads=4, embed=256, reps=20):
+    """MFMA utilisation of the acting pass's dense GEMMs:
+    the same bf16 torch.mm shapes trafficrl/models/fused.py issues per 4096-graph
+    forward -- layer-1 lin [rows, H*C] x [H*C, H*C]^T, layer-2 lin
+    [rows, H*C] x [embed, H*C]^T, the edge head's per-node projection
+    [rows, embed] x [2*hidden, embed]^T and the context product
+    [graphs, 2*embed] x [2*embed, hidden] -- timed with HIP events on the
+    current stream; FLOPs (2mnk) / time vs the dense bf16 MFMA peak."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    bf = dict(dtype=torch.bfloat16, device=dev)
+    hc = heads * hidden
+    shapes = [(rows, hc, hc), (rows, hc, embed), (rows, embed, 2 * hidden), (graphs, 2 * embed, hidden)]
+    ops = []
+    for m, k, n in shapes:
+        a, w = torch.randn(m, k, **bf), torch.randn(n, k, **bf)
+        ops.append((a, w, 2.0 * m * n * k))
+    for a, w, _ in ops:
+        torch.mm(a, w.t())
+    torch.cuda.synchronize()
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_.record()
+    for _ in range(reps):
+        for a, w, _ in ops:
+            torch.mm(a, w.t())
+    e_.record()
+    torch.cuda.synchronize()
+    sec = s_.elapsed_time(e_) / 1e3 / reps
+    flops = sum(f for _, _, f in ops)
+    return {"gemms": "act-pass lin GEMMs, bf16 hipBLASLt: " + ", ".join(f"{m}x{k}x{n}" for m, k, n in shapes),
+            "flops_per_pass": flops, "ms_per_pass": sec * 1e3, "achieved": flops / sec / 1e12,
+            "peak": MFMA_PEAK_BF16 / 1e12, "unit": "TFLOP/s", "frac": flops / sec / MFMA_PEAK_BF16}
 
 
 def measured_traffic(network):
@@ -133,6 +206,9 @@ def main():
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default 4096 sf / 1024 anaheim)")
     ap.add_argument("--method", default=None, choices=["msa", "fw", "cfw"], help="default msa (sf) / fw (anaheim)")
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--sp", default="scipy", choices=["scipy", "torch"],
+                    help="shortest-path rule: scipy = the reference's CPU Dijkstra (default; the bit-exact pinned "
+                         "path), torch = its sp_backend='torch' Floyd-Warshall")
     ap.add_argument("--no-observe", action="store_true", help="skip get_state (assignment-only steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -182,10 +258,11 @@ def main():
         return out
 
     if args.workload == "train":
-        from trafficrl.train import Trainer, load_config
-        cfg = load_config(None)
-        cfg.update(num_envs=B, assignment_iters=args.iters, assignment_method=args.method, batch_start=256,
-                   batch_size=256, update_every=4, updates_per_step=1, eval_every=0, episodes=10 ** 9,
+        from trafficrl.train import Trainer, sf_config
+        cfg = sf_config()
+        cfg.update(num_envs=B, assignment_iters=args.iters, assignment_method=args.method, sp_backend=args.sp,
+                   batch_start=256,
+                   batch_size=256, update_every=4, updates_per_step=1, update_unit="iterations", eval_every=0, episodes=10 ** 9,
                    output_dir=os.path.join("/tmp", f"trx_bench_{os.getpid()}"), amp="bf16")
         tr = Trainer(cfg, device=dev, rank=rank, world=world, log=False)
         env = tr.env
@@ -222,7 +299,8 @@ def main():
     else:
         env = VecRepairEnv(gd, B, device=dev, assignment_method=args.method, assignment_iters=args.iters,
                            reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0, reward_gamma=0.0,
-                           reward_clip=2.0, capacity_damage=1e-3, unassigned_penalty=1e4, reset=False)
+                           reward_clip=2.0, capacity_damage=1e-3, unassigned_penalty=1e4, reset=False,
+                           sp_backend=args.sp)
         E, N = env.num_edges, env.num_nodes
         dmg0 = torch.from_numpy(fixed_damage_mask(gd)).to(dev)
         dmg_all = dmg0[None].expand(B, E).contiguous()
@@ -248,6 +326,12 @@ def main():
         reset()
     for _ in range(args.warmup):
         one_step()
+    if args.workload == "train":
+        # steady state whatever --warmup is: the eager warm-up updates and the
+        # HIP-graph capture of the SAC update happen here, never in the timed loop
+        while tr.replay.size <= int(cfg["batch_start"]):
+            one_step()
+        tr.prime_update()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -283,10 +367,11 @@ def main():
     traffic, traffic_src = measured_traffic(args.network)
     if (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")):
         traffic, traffic_src = None, None  # the committed PMC passes are for the default workloads
+    mfma = gemm_mfma(B * N, B) if (args.workload == "train" and rank == 0) else None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(args.network, args.method, args.iters, args.cpu_seconds)
+            cpu = cpu_baseline(args.network, args.method, args.iters, args.cpu_seconds, args.sp)
         out = {
             "metric": METRIC,
             "value": value,
@@ -304,9 +389,11 @@ def main():
                      "fixed_damage_seed=42, " + ("random-init GAT-SAC (hidden 256, 4 heads, embed 256)"
                                                  if args.workload == "train" else "uniform random valid repair actions")),
             "config": {
-                "workload": (f"{'SF' if not big else 'AnaheimSynth'} {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment + get_state per"
-                             " step" + (", GAT-SAC bf16 acting every step + 1 PER update (batch 256) every 4 steps"
-                                        if args.workload == "train" else ", uniform random valid actions")),
+                "workload": (f"{'SF' if not big else 'AnaheimSynth'} {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment"
+                             f" ({args.sp} shortest-path rule) + get_state per step"
+                             + (f", GAT-SAC bf16 acting every step + 1 PER update (batch 256) every 4 steps (update-to-data "
+                                f"ratio 1/{4 * B} per transition)" if args.workload == "train" else ", uniform random valid actions")),
+                "sp_backend": args.sp,
                 "workload_kind": args.workload,
                 "envs_per_gpu": B, "global_envs": B * world, "network": NETWORKS[args.network][2],
                 "method": args.method, "assignment_iters": args.iters, "episode_len": ep_len,
@@ -319,6 +406,7 @@ def main():
                                  "(raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic else None,
                 "kernel": "trx::env_kernel_big" if big else "trx::env_kernel_q<24>", "kernel_mean_ms": mean_kernel_s * 1e3,
                 "bytes_per_assign": bpa, "assigns_per_launch": B,
+                "mfma": mfma,
             },
             "cpu_baseline": cpu,
             "breakdown_ms_per_step": dict(breakdown, env_kernel=mean_kernel_s * 1e3 * len(kern_ms) / args.steps),

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 3
+#define TRX_ABI_VERSION 4
 
 /* error codes */
 #define TRX_OK 0
@@ -51,6 +51,16 @@ extern "C" {
 #define TRX_REWARD_MINIMIZE_TSTT 3
 #define TRX_REWARD_REL_IMPROVE 4
 
+/* shortest-path rule of the all-or-nothing step: RepairEnv(sp_backend=...)
+ * repair_env.py:34, 111-161, 421-573.  SCIPY: scipy.sparse.csgraph.dijkstra
+ * (float64 labels, scipy heap order on ties; what sp_backend="auto"/"scipy"
+ * resolves to without cupy/cugraph).  TORCH: _all_or_nothing_torch, float32
+ * Floyd-Warshall (k ascending, strict <) + next_hop walk (sp_backend="torch"
+ * on a GPU device: configs/sioux_falls.yaml, run_greedy.py).  TORCH needs
+ * N <= 32; GP assignment always uses SCIPY (as _shortest_paths_from_origin). */
+#define TRX_SP_SCIPY 0
+#define TRX_SP_TORCH 1
+
 typedef struct trx_graph trx_graph;
 
 /* Env constants of RepairEnv.__init__ (repair_env.py:23-50). */
@@ -63,7 +73,7 @@ typedef struct trx_params {
     float _pad0;
     double unassigned_penalty;  /* 2e7 (yaml: 1e4)                   unassigned_penalty  */
     int32_t reward_mode;        /* TRX_REWARD_*                      reward_mode         */
-    int32_t _pad1;
+    int32_t sp_rule;            /* TRX_SP_*                          sp_backend          */
     double reward_alpha, reward_beta, reward_gamma, reward_clip;
     double gp_step;             /* 1.0; <= 0 means 1/(it+1)          gp_step (GP only)   */
     int32_t gp_keep_paths;      /* 3 (yaml: 2); 1..3 supported       gp_keep_paths       */

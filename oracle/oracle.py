@@ -21,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 METHODS = {"msa": 0, "fw": 1, "cfw": 2}
+SP_RULES = {"scipy": 0, "torch": 1}   # _all_or_nothing scipy branch / _all_or_nothing_torch
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -58,8 +59,13 @@ def lib():
         L.orc_graph_build.restype = ctypes.c_int
         L.orc_assign_batch.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_float, ctypes.c_float, ctypes.c_double, _f32p, _f32p, _f32p,
-                                       _f32p, _f64p, _f64p, _u8p, ctypes.c_int]
+                                       _f32p, _f64p, _f64p, _u8p, ctypes.c_int, ctypes.c_int]
         L.orc_assign_batch.restype = ctypes.c_int
+        L.orc_aon_fw.argtypes = [ctypes.POINTER(_Graph), _f32p, _f32p, _i32p]
+        L.orc_aon_fw.restype = ctypes.c_double
+        L.orc_observe_batch.argtypes = [ctypes.POINTER(_Graph), ctypes.c_int, _f32p, _f32p, _f32p, _f32p, _f64p,
+                                        _f32p, _f32p, _f32p, ctypes.c_int]
+        L.orc_observe_batch.restype = ctypes.c_int
         L.orc_all_pairs.argtypes = [ctypes.POINTER(_Graph), _f32p, _f64p, _i32p]
         L.orc_aon.argtypes = [ctypes.POINTER(_Graph), _f32p, _f32p]
         L.orc_aon.restype = ctypes.c_double
@@ -117,11 +123,43 @@ class OracleGraph:
                       alpha, beta, _p(t, _f32p))
         return t
 
-    def aon(self, t):
+    def aon(self, t, sp="scipy"):
+        """_all_or_nothing (scipy branch, repair_env.py:481-503) or, sp="torch",
+        _all_or_nothing_torch (520-573).  Returns (aux, unassigned)."""
         t = np.ascontiguousarray(t, np.float32)
         aux = np.empty(self.E, np.float32)
-        un = lib().orc_aon(ctypes.byref(self._g), _p(t, _f32p), _p(aux, _f32p))
+        if sp == "torch":
+            un = lib().orc_aon_fw(ctypes.byref(self._g), _p(t, _f32p), _p(aux, _f32p), None)
+        else:
+            un = lib().orc_aon(ctypes.byref(self._g), _p(t, _f32p), _p(aux, _f32p))
         return aux, un
+
+    def next_hop(self, t):
+        """The torch backend's float32 Floyd-Warshall next_hop matrix [N,N]."""
+        t = np.ascontiguousarray(t, np.float32)
+        aux = np.empty(self.E, np.float32)
+        nh = np.empty((self.N, self.N), np.int32)
+        lib().orc_aon_fw(ctypes.byref(self._g), _p(t, _f32p), _p(aux, _f32p), _p(nh, _i32p))
+        return nh
+
+    def observe(self, cap, damaged, goal, flow, tstt, nthreads=1):
+        """Batched get_state (repair_env.py:751-819) in C: (node_x [B,N,4],
+        edge_x [B,E,6], mask [B,E])."""
+        cap = np.ascontiguousarray(np.atleast_2d(cap), np.float32)
+        damaged = np.ascontiguousarray(np.atleast_2d(damaged), np.float32)
+        goal = np.ascontiguousarray(np.atleast_2d(goal), np.float32)
+        flow = np.ascontiguousarray(np.atleast_2d(flow), np.float32)
+        tstt = np.ascontiguousarray(np.atleast_1d(tstt), np.float64)
+        B = flow.shape[0]
+        nx_ = np.empty((B, self.N, 4), np.float32)
+        ex = np.empty((B, self.E, 6), np.float32)
+        m = np.empty((B, self.E), np.float32)
+        rc = lib().orc_observe_batch(ctypes.byref(self._g), B, _p(cap, _f32p), _p(damaged, _f32p), _p(goal, _f32p),
+                                     _p(flow, _f32p), _p(tstt, _f64p), _p(nx_, _f32p), _p(ex, _f32p), _p(m, _f32p),
+                                     int(nthreads))
+        if rc != 0:
+            raise RuntimeError("oracle observe failed")
+        return nx_, ex, m
 
     def all_pairs(self, t):
         t = np.ascontiguousarray(t, np.float32)
@@ -131,8 +169,10 @@ class OracleGraph:
         return d, p
 
     def assign(self, cap, damaged, flow, method="msa", iters=30, alpha=0.15, beta=4.0, penalty=1e4,
-               env_mask=None, nthreads=1):
+               env_mask=None, nthreads=1, sp="scipy"):
         """Batched compute_flow_assignment.  cap/damaged/flow: [B,E] (or [E]).
+        sp: "scipy" (Dijkstra, the default backend here) or "torch" (the
+        reference's sp_backend="torch" Floyd-Warshall).
         Returns (flow_out, t_out, tstt[B], unassigned[B])."""
         single = np.ndim(flow) == 1
         cap = np.ascontiguousarray(np.atleast_2d(cap), np.float32)
@@ -146,7 +186,7 @@ class OracleGraph:
         rc = lib().orc_assign_batch(ctypes.byref(self._g), B, METHODS[method], int(iters), alpha, beta, penalty,
                                     _p(cap, _f32p), _p(damaged, _f32p), _p(flow, _f32p), _p(t, _f32p),
                                     _p(tstt, _f64p), _p(un, _f64p), None if mask is None else _p(mask, _u8p),
-                                    int(nthreads))
+                                    int(nthreads), SP_RULES[sp])
         if rc != 0:
             raise RuntimeError("oracle assign failed")
         if single:

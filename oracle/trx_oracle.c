@@ -12,6 +12,9 @@
  *   compute_flow_assignment (MSA/FW/CFW) 299-345
  *   compute_tstt                      724-735
  *   compute_reward_with_goal          244-291, is_goal_complete 293-294
+ *   _all_or_nothing_torch (sp_backend="torch": float32 Floyd-Warshall, strict <,
+ *     k ascending, next_hop walk)     520-573
+ *   get_state (betweenness + features) 751-819, networkx 3.4 Brandes order
  * and scipy 1.15.3 scipy.sparse.csgraph.dijkstra (Fibonacci heap, float64
  * labels, strict-improvement predecessors, CSR rows sorted by column as
  * csr_matrix((w,(row,col))) produces them).  The heap is restated from
@@ -339,6 +342,9 @@ typedef struct {
     float* aux;      /* [E] */
     float* t;        /* [E] */
     float* scratch;  /* [E] */
+    float* fw_dist;  /* [N*N] torch-backend Floyd-Warshall */
+    int32_t* fw_nh;  /* [N*N] */
+    int sp;          /* ORC_SP_* */
 } orc_ws;
 
 static int ws_alloc(orc_ws* ws, int N, int E) {
@@ -354,12 +360,16 @@ static int ws_alloc(orc_ws* ws, int N, int E) {
     ws->aux = (float*)malloc(sizeof(float) * EE);
     ws->t = (float*)malloc(sizeof(float) * EE);
     ws->scratch = (float*)malloc(sizeof(float) * EE);
+    ws->fw_dist = (float*)malloc(sizeof(float) * N * N);
+    ws->fw_nh = (int32_t*)malloc(sizeof(int32_t) * N * N);
+    ws->sp = 0;
     return (ws->w && ws->dist && ws->pred && ws->path && ws->nodes && ws->d_fw && ws->d_prev && ws->dir &&
-            ws->aux && ws->t && ws->scratch) ? 0 : -1;
+            ws->aux && ws->t && ws->scratch && ws->fw_dist && ws->fw_nh) ? 0 : -1;
 }
 static void ws_free(orc_ws* ws) {
     free(ws->w); free(ws->dist); free(ws->pred); free(ws->path); free(ws->nodes);
     free(ws->d_fw); free(ws->d_prev); free(ws->dir); free(ws->aux); free(ws->t); free(ws->scratch);
+    free(ws->fw_dist); free(ws->fw_nh);
 }
 
 /* repair_env.py:481-503 (+ 707-722): returns unassigned demand */
@@ -399,7 +409,70 @@ double orc_aon(const orc_graph* g, const float* t, float* aux) {
     return u;
 }
 
+/* repair_env.py:520-573 (_all_or_nothing_torch): float32 all-pairs
+ * Floyd-Warshall, dist init 1e12 with a zero diagonal, then dist[u][v] =
+ * t[e] and next_hop[u][v] = v per link in file order; for k ascending
+ * alt = dist[i][k] + dist[k][j] (float32), strict `alt < dist` takes alt and
+ * next_hop[i][k].  Each OD pair (dict order, origin != dest) walks next_hop
+ * from the origin for at most N hops; a pair that does not reach its
+ * destination is unassigned (its partial path is dropped).  Returns
+ * unassigned demand.  dist/nh: [N*N] scratch. */
+static double aon_fw(const orc_graph* g, const float* t, float* aux, float* dist, int32_t* nh, int32_t* path) {
+    int N = g->N, E = g->E;
+    double unassigned = 0.0;
+    for (int e = 0; e < E; e++) aux[e] = 0.0f;
+    for (int i = 0; i < N * N; i++) { dist[i] = 1e12f; nh[i] = -1; }
+    for (int i = 0; i < N; i++) dist[i * N + i] = 0.0f;
+    for (int e = 0; e < E; e++) {
+        dist[g->src[e] * N + g->dst[e]] = t[e];
+        nh[g->src[e] * N + g->dst[e]] = g->dst[e];
+    }
+    for (int k = 0; k < N; k++) {
+        const float* rowk = dist + (long)k * N;
+        for (int i = 0; i < N; i++) {
+            if (i == k) continue;  /* alt[k][j] = 0 + d[k][j] and alt[i][k] = d[i][k] + 0 never improve */
+            const float dik = dist[(long)i * N + k];
+            const int32_t nik = nh[(long)i * N + k];
+            float* rowi = dist + (long)i * N;
+            int32_t* nhi = nh + (long)i * N;
+            for (int j = 0; j < N; j++) {
+                float alt = dik + rowk[j];
+                if (alt < rowi[j]) { rowi[j] = alt; nhi[j] = nik; }
+            }
+        }
+    }
+    for (int q = 0; q < g->P; q++) {
+        int o = g->od_o[q], d = g->od_d[q];
+        double demand = g->od_v[q];
+        if (o == d) continue;
+        int n = 0, cur = o, hops = 0, ok = 1;
+        while (cur != d && cur != -1 && hops < N) {
+            int nxt = nh[(long)cur * N + d];
+            if (nxt < 0) { ok = 0; break; }
+            path[n++] = g->eid_of[cur * N + nxt];
+            cur = nxt;
+            hops++;
+        }
+        if (!ok || cur != d) { unassigned += demand; continue; }
+        float dem32 = (float)demand;
+        for (int i = 0; i < n; i++) aux[path[i]] = aux[path[i]] + dem32;
+    }
+    return unassigned;
+}
+
+double orc_aon_fw(const orc_graph* g, const float* t, float* aux, int32_t* nh_out) {
+    int N = g->N;
+    float* dist = (float*)malloc(sizeof(float) * N * N);
+    int32_t* nh = nh_out ? nh_out : (int32_t*)malloc(sizeof(int32_t) * N * N);
+    int32_t* path = (int32_t*)malloc(sizeof(int32_t) * (N + 1));
+    double u = aon_fw(g, t, aux, dist, nh, path);
+    free(dist); free(path);
+    if (!nh_out) free(nh);
+    return u;
+}
+
 enum { ORC_MSA = 0, ORC_FW = 1, ORC_CFW = 2 };
+enum { ORC_SP_SCIPY = 0, ORC_SP_TORCH = 1 };
 
 /* repair_env.py:299-345.  flow: in = warm start, out = final flow.
  * t_out (optional) = BPR(final flow).  Returns tstt. */
@@ -412,7 +485,8 @@ static double assign_one(const orc_graph* g, int method, int iters, float alpha,
     int have_prev = 0;
     orc_bpr(E, flow, cap, g->t0, damaged, alpha, beta, t);
     for (int it = 0; it < iters; it++) {
-        double un = aon(g, t, ws->aux, ws);
+        double un = ws->sp == ORC_SP_TORCH ? aon_fw(g, t, ws->aux, ws->fw_dist, ws->fw_nh, ws->path)
+                                           : aon(g, t, ws->aux, ws);
         for (int e = 0; e < E; e++) ws->d_fw[e] = ws->aux[e] - flow[e];
         if (method == ORC_CFW) {
             float* dir = ws->dir;
@@ -464,7 +538,7 @@ static double assign_one(const orc_graph* g, int method, int iters, float alpha,
  * NULL.  OpenMP over envs when nthreads > 1 (CPU baseline).  Returns 0. */
 int orc_assign_batch(const orc_graph* g, int B, int method, int iters, float alpha, float beta,
                      double penalty_coef, const float* cap, const float* damaged, float* flow, float* t_out,
-                     double* tstt, double* unassigned, const uint8_t* env_mask, int nthreads) {
+                     double* tstt, double* unassigned, const uint8_t* env_mask, int nthreads, int sp) {
     int E = g->E;
     int err = 0;
 #ifdef _OPENMP
@@ -476,6 +550,7 @@ int orc_assign_batch(const orc_graph* g, int B, int method, int iters, float alp
         if (ws_alloc(&ws, g->N, E)) {
             err = 1;
         } else {
+            ws.sp = sp;
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic, 1)
 #endif
@@ -533,4 +608,196 @@ double orc_reward(int mode, double prev, double curr, double initial_tstt, int c
     reward = alpha * delta + bonus - gamma;
     if (clip > 0) reward = reward < -clip ? -clip : (reward > clip ? clip : reward);
     return reward;
+}
+
+/* ------------------------------------------------------------ get_state */
+/* repair_env.py:751-819 for B envs (the timed CPU baseline's observation
+ * leg; oracle.py's observation() is the pure-Python restatement it is
+ * checked against).  Betweenness: networkx 3.4 betweenness_centrality on
+ * G.edge_subgraph(active links), normalized, directed -- Brandes BFS
+ * (_single_source_shortest_path_basic) and accumulation (_accumulate_basic)
+ * with networkx's node order (first appearance in the link list) and
+ * adjacency order (link insertion order), float64.  node_x [B,N,4],
+ * edge_x [B,E,6], mask [B,E] (may be NULL). */
+typedef struct {
+    int32_t *order, *adj_ptr, *adj, *adj_e, *nodes, *D, *Q, *S, *P_ptr, *P_cnt, *P;
+    double *sigma, *delta, *bc;
+    uint8_t* on;
+    float *tmp, *bw;
+} orc_obs_ws;
+
+static int obs_ws_alloc(orc_obs_ws* w, int N, int E) {
+    int EE = E > 0 ? E : 1;
+    w->order = (int32_t*)malloc(sizeof(int32_t) * N);
+    w->adj_ptr = (int32_t*)calloc(N + 1, sizeof(int32_t));
+    w->adj = (int32_t*)malloc(sizeof(int32_t) * EE);
+    w->adj_e = (int32_t*)malloc(sizeof(int32_t) * EE);
+    w->nodes = (int32_t*)malloc(sizeof(int32_t) * N);
+    w->D = (int32_t*)malloc(sizeof(int32_t) * N);
+    w->Q = (int32_t*)malloc(sizeof(int32_t) * N);
+    w->S = (int32_t*)malloc(sizeof(int32_t) * N);
+    w->P_ptr = (int32_t*)malloc(sizeof(int32_t) * (N + 1));
+    w->P_cnt = (int32_t*)malloc(sizeof(int32_t) * N);
+    w->P = (int32_t*)malloc(sizeof(int32_t) * EE);
+    w->sigma = (double*)malloc(sizeof(double) * N);
+    w->delta = (double*)malloc(sizeof(double) * N);
+    w->bc = (double*)malloc(sizeof(double) * N);
+    w->on = (uint8_t*)malloc(N);
+    w->tmp = (float*)malloc(sizeof(float) * EE);
+    w->bw = (float*)malloc(sizeof(float) * N);
+    return (w->bw && w->order && w->adj_ptr && w->adj && w->adj_e && w->nodes && w->D && w->Q && w->S && w->P_ptr &&
+            w->P_cnt && w->P && w->sigma && w->delta && w->bc && w->on && w->tmp) ? 0 : -1;
+}
+static void obs_ws_free(orc_obs_ws* w) {
+    free(w->order); free(w->adj_ptr); free(w->adj); free(w->adj_e); free(w->nodes); free(w->D); free(w->Q);
+    free(w->S); free(w->P_ptr); free(w->P_cnt); free(w->P); free(w->sigma); free(w->delta); free(w->bc);
+    free(w->on); free(w->tmp); free(w->bw);
+}
+
+/* node order and adjacency of the reference's nx.DiGraph (repair_env.py:106-109) */
+static void obs_topology(const orc_graph* g, orc_obs_ws* w) {
+    int N = g->N, E = g->E, cnt = 0;
+    memset(w->on, 0, N);
+    for (int e = 0; e < E; e++) {
+        int uv[2] = {g->src[e], g->dst[e]};
+        for (int k = 0; k < 2; k++)
+            if (!w->on[uv[k]]) { w->on[uv[k]] = 1; w->order[cnt++] = uv[k]; }
+    }
+    for (int i = cnt; i < N; i++) w->order[i] = -1;  /* isolated nodes are not in the nx graph */
+    memset(w->adj_ptr, 0, sizeof(int32_t) * (N + 1));
+    for (int e = 0; e < E; e++) w->adj_ptr[g->src[e] + 1]++;
+    for (int u = 0; u < N; u++) w->adj_ptr[u + 1] += w->adj_ptr[u];
+    int* fill = (int*)calloc(N, sizeof(int));
+    for (int e = 0; e < E; e++) {
+        int u = g->src[e], k = w->adj_ptr[u] + fill[u]++;
+        w->adj[k] = g->dst[e];
+        w->adj_e[k] = e;
+    }
+    free(fill);
+    /* predecessor slots: at most the in-degree of each node */
+    memset(w->P_ptr, 0, sizeof(int32_t) * (N + 1));
+    for (int e = 0; e < E; e++) w->P_ptr[g->dst[e] + 1]++;
+    for (int u = 0; u < N; u++) w->P_ptr[u + 1] += w->P_ptr[u];
+}
+
+static void obs_betweenness(const orc_graph* g, orc_obs_ws* w, const float* damaged, float* bw_out) {
+    int N = g->N, n = 0;
+    /* edge_subgraph nodes: graph order, incident to an active link */
+    memset(w->on, 0, N);
+    for (int e = 0; e < g->E; e++)
+        if (damaged[e] == 0.0f) { w->on[g->src[e]] = 1; w->on[g->dst[e]] = 1; }
+    for (int i = 0; i < N && w->order[i] >= 0; i++)
+        if (w->on[w->order[i]]) w->nodes[n++] = w->order[i];
+    for (int v = 0; v < N; v++) w->bc[v] = 0.0;
+    for (int si = 0; si < n; si++) {
+        int s = w->nodes[si];
+        for (int v = 0; v < N; v++) { w->sigma[v] = 0.0; w->D[v] = -1; w->P_cnt[v] = 0; w->delta[v] = 0.0; }
+        w->sigma[s] = 1.0;
+        w->D[s] = 0;
+        int qh = 0, qt = 0, ns = 0;
+        w->Q[qt++] = s;
+        while (qh < qt) {
+            int v = w->Q[qh++];
+            w->S[ns++] = v;
+            int Dv = w->D[v];
+            double sv = w->sigma[v];
+            for (int k = w->adj_ptr[v]; k < w->adj_ptr[v + 1]; k++) {
+                if (damaged[w->adj_e[k]] != 0.0f) continue;
+                int x = w->adj[k];
+                if (w->D[x] < 0) { w->Q[qt++] = x; w->D[x] = Dv + 1; }
+                if (w->D[x] == Dv + 1) { w->sigma[x] += sv; w->P[w->P_ptr[x] + w->P_cnt[x]++] = v; }
+            }
+        }
+        while (ns > 0) {
+            int x = w->S[--ns];
+            double coeff = (1.0 + w->delta[x]) / w->sigma[x];
+            for (int k = 0; k < w->P_cnt[x]; k++) {
+                int v = w->P[w->P_ptr[x] + k];
+                w->delta[v] += w->sigma[v] * coeff;
+            }
+            if (x != s) w->bc[x] += w->delta[x];
+        }
+    }
+    if (n > 2) {
+        double scale = 1.0 / ((double)(n - 1) * (double)(n - 2));
+        for (int i = 0; i < n; i++) w->bc[w->nodes[i]] *= scale;
+    }
+    for (int v = 0; v < N; v++) bw_out[v] = w->on[v] ? (float)w->bc[v] : 0.0f;
+}
+
+static void obs_one(const orc_graph* g, orc_obs_ws* w, const float* cap, const float* damaged, const float* goal,
+                    const float* flow, double tstt, float* node_x, float* edge_x, float* mask) {
+    int N = g->N, E = g->E;
+    float* b = w->bw;
+    obs_betweenness(g, w, damaged, b);
+    float bmax = 0.0f;
+    for (int v = 0; v < N; v++) bmax = b[v] > bmax ? b[v] : bmax;
+    if (bmax > 0.0f)
+        for (int v = 0; v < N; v++) b[v] = b[v] / bmax;
+    /* goal_total / remaining: float(np.sum(float32)) -- integer-valued, exact */
+    double goal_total = 0.0, remaining = 0.0;
+    int n_und = 0;
+    for (int e = 0; e < E; e++) {
+        goal_total += goal[e];
+        remaining += (double)(goal[e] * damaged[e]);
+        if (damaged[e] == 0.0f) w->tmp[n_und++] = flow[e];
+    }
+    double rr = remaining / (goal_total > 1.0 ? goal_total : 1.0);
+    double avg = n_und > 0 ? (double)(pairwise_f32(w->tmp, n_und) / (float)n_und) : 0.0;
+    double dn = g->total_demand / (double)(E > 1 ? E : 1);
+    double afn = avg / (dn > 1.0 ? dn : 1.0);
+    double lt = log10(tstt > 1.0 ? tstt : 1.0);
+    for (int v = 0; v < N; v++) {
+        node_x[v * 4 + 0] = b[v];
+        node_x[v * 4 + 1] = (float)rr;
+        node_x[v * 4 + 2] = (float)afn;
+        node_x[v * 4 + 3] = (float)lt;
+    }
+    float max_t0 = 0.0f, max_cap = 0.0f;
+    for (int e = 0; e < E; e++) {
+        max_t0 = g->t0[e] > max_t0 ? g->t0[e] : max_t0;
+        max_cap = g->cap0[e] > max_cap ? g->cap0[e] : max_cap;
+    }
+    double lt0 = log10((double)max_t0 + 1.0), lcap = log10((double)max_cap + 1.0);
+    for (int e = 0; e < E; e++) {
+        float c = cap[e] > 1e-6f ? cap[e] : 1e-6f;
+        float raw = flow[e] / c;
+        float vc = damaged[e] > 0.0f ? 0.0f : raw;
+        vc = log1pf(vc);
+        vc = vc < 0.0f ? 0.0f : (vc > 10.0f ? 10.0f : vc);
+        float* ex = edge_x + (long)e * 6;
+        ex[0] = (float)((double)log10f(g->t0[e] + 1.0f) / lt0);
+        ex[1] = (float)((double)log10f(cap[e] + 1.0f) / lcap);
+        ex[2] = vc;
+        ex[3] = damaged[e];
+        ex[4] = goal[e];
+        ex[5] = (float)e / (float)(E > 1 ? E - 1 : 1);
+        if (mask) mask[e] = damaged[e];
+    }
+}
+
+int orc_observe_batch(const orc_graph* g, int B, const float* cap, const float* damaged, const float* goal,
+                      const float* flow, const double* tstt, float* node_x, float* edge_x, float* mask,
+                      int nthreads) {
+    int N = g->N, E = g->E, err = 0;
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads) reduction(| : err)
+#endif
+    {
+        orc_obs_ws w;
+        if (obs_ws_alloc(&w, N, E)) {
+            err = 1;
+        } else {
+            obs_topology(g, &w);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+            for (int b = 0; b < B; b++)
+                obs_one(g, &w, cap + (long)b * E, damaged + (long)b * E, goal + (long)b * E, flow + (long)b * E,
+                        tstt[b], node_x + (long)b * N * 4, edge_x + (long)b * E * 6, mask ? mask + (long)b * E : NULL);
+            obs_ws_free(&w);
+        }
+    }
+    return err ? -1 : 0;
 }

@@ -81,7 +81,7 @@ struct SmemQ {
 
 __host__ __device__ inline uint32_t align16q(uint32_t x) { return (x + 15u) & ~15u; }
 
-__host__ __device__ inline SmemQ smemq_layout(int E, int N, int Z, int NP, int EPW, int L) {
+__host__ __device__ inline SmemQ smemq_layout(int E, int N, int Z, int NP, int EPW, int L, bool fw = false) {
     SmemQ o{};
     uint32_t off = 0;
     auto take = [&off](uint32_t bytes) {
@@ -100,7 +100,8 @@ __host__ __device__ inline SmemQ smemq_layout(int E, int N, int Z, int NP, int E
     o.w = take((uint32_t)(EPW * NP * NP * 4));
     o.pred = take((uint32_t)(EPW * Z * NP));
     o.ord = take((uint32_t)(EPW * Z * NP));
-    o.dist = take((uint32_t)(EPW * Z * NP * 8));
+    // (torch rule: the [EPW][NP][NP] u8 next-hop tables live here instead)
+    o.dist = take((uint32_t)(fw && EPW * NP * NP > EPW * Z * NP * 8 ? EPW * NP * NP : EPW * Z * NP * 8));
     o.nscan = take((uint32_t)(EPW * Z * 4));
     o.inptr = take((uint32_t)((N + 1) * 2));
     o.insrc = take((uint32_t)E);
@@ -136,7 +137,17 @@ __device__ __forceinline__ void quad_min_step(double& best, int& bu) {
 
 }  // namespace
 
-template <int NP>
+// Shortest-path rule of the all-or-nothing step:
+//  kSpScipy  _all_or_nothing, scipy branch (repair_env.py:481-503, 707-722):
+//            Dijkstra, float64 labels, scipy heap order on ties;
+//  kSpTorch  _all_or_nothing_torch (repair_env.py:520-573): float32 all-pairs
+//            Floyd-Warshall (k ascending, strict <) and a next_hop walk per OD
+//            pair (at most N hops; a pair that misses its destination is
+//            unassigned; intrazonal pairs are skipped).
+constexpr int kSpScipy = 0;
+constexpr int kSpTorch = 1;
+
+template <int NP, int SP = kSpScipy>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))) env_kernel_q(const DevGraph g, const trx_params p, const trx_state s, int B,
                                                     int EPW, int mode, const int32_t* __restrict__ action,
                                                     double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
@@ -149,7 +160,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
     const int tid = threadIdx.x;
     const int EL = EPW * E;
     const int env0 = blockIdx.x * EPW;
-    const SmemQ O = smemq_layout(E, N, Z, NP, EPW, L);
+    const SmemQ O = smemq_layout(E, N, Z, NP, EPW, L, SP == kSpTorch);
     struct {
         float *flow, *cap, *dmg, *goal, *t, *aux, *dprev, *w, *dem, *unas;
         uint8_t *pred, *ord, *insrc;
@@ -263,6 +274,73 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
     float unassigned_lane = 0.0f;
 
     for (int it = 0; it < p.iters; ++it) {
+      if constexpr (SP == kSpTorch) {
+        // ---------------- _all_or_nothing_torch (repair_env.py:524-543): per env a
+        //                  row-major float32 dist table D[u][v] (the cost-table
+        //                  region) and u8 next-hop table H[u][v] (0xFF = -1)
+        float* D = S.w;
+        uint8_t* H = reinterpret_cast<uint8_t*>(S.dist);
+        for (int x = tid; x < EPW * NP * NP; x += L) {
+            const int el = x / (NP * NP), r = x - el * NP * NP;
+            const int u = r / NP, v = r - u * NP;
+            const int e = S.eid[r];
+            // dist = 1e12, diag 0, then dist[row, col] = t per link (524-535)
+            D[x] = e >= 0 ? S.t[el * E + e] : (u == v ? 0.0f : 1e12f);
+            H[x] = e >= 0 ? (uint8_t)v : (uint8_t)0xFF;
+        }
+        __syncthreads();
+        // k ascending, strict <; row k and column k do not change during step k
+        // (D[k][k] + w is never < w for w >= 0), so the in-place update is the
+        // reference's whole-matrix torch.where (537-542)
+        for (int k = 0; k < N; ++k) {
+            for (int x = tid; x < EPW * N * N; x += L) {
+                const int el = x / (N * N), r = x - el * N * N;
+                const int i = r / N, j2 = r - i * N;
+                const int base = el * NP * NP;
+                const float alt = __fadd_rn(D[base + i * NP + k], D[base + k * NP + j2]);
+                if (alt < D[base + i * NP + j2]) {
+                    D[base + i * NP + j2] = alt;
+                    H[base + i * NP + j2] = H[base + i * NP + k];
+                }
+            }
+            __syncthreads();
+        }
+        TRX_STAMP(2);
+        // next_hop walk per OD pair (548-568), lane j of the origin's quad walks
+        // destinations v = 4i + j; integer demands make the LDS float atomics exact
+        if (tree_on) {
+            const uint8_t* Hl = H + lenv * NP * NP;
+            const float* dm = S.dem + zi * N;
+            float* aux = S.aux + lenv * E;
+            float un = 0.0f;
+            for (int i = 0; i < NPL; ++i) {
+                const int v = kQuad * i + j;
+                if (v >= N || v == origin) continue;  // origin == dest: skipped (551-552)
+                const float dv = dm[v];
+                if (!(dv > 0.0f)) continue;
+                int cur = origin, hops = 0;
+                while (cur != v && hops < N) {
+                    const int nx = Hl[cur * NP + v];
+                    if (nx == 0xFF) break;
+                    cur = nx;
+                    ++hops;
+                }
+                if (cur != v) {
+                    un += dv;  // unassigned; the partial path is dropped (564-566)
+                    continue;
+                }
+                cur = origin;
+                while (cur != v) {
+                    const int nx = Hl[cur * NP + v];
+                    atomicAdd(&aux[S.eid[cur * NP + nx]], dv);
+                    cur = nx;
+                }
+            }
+            unassigned_lane = un;
+        }
+        __syncthreads();
+        TRX_STAMP(4);
+      } else {
         // ---------------- per-env cost rows in quad layout (LDS): the link entries
         //                  (u -> v = 4*ii + jj at column c = jj * NPL + ii of row u)
         if (wpos_reg) {
@@ -446,6 +524,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
         }
         __syncthreads();
         TRX_STAMP(4);
+      }  // SP
 
         // ---------------- flow update + BPR (repair_env.py:317-342)
         if (p.method == TRX_METHOD_CFW) {
@@ -541,7 +620,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(5, 8))
     TRX_STAMP(6);
 }
 
-LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs) {
+LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs, int sp_rule) {
     LaunchCfg c{};
     c.np = g.NP;
     // envs per workgroup: fill up to 512 threads with whole envs (Z quads each)
@@ -554,7 +633,7 @@ LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs) {
     while (epw > 1 && epw * per_env > 512) --epw;
     c.epw = epw;
     c.threads = ((epw * per_env + 63) / 64) * 64;
-    c.smem = smemq_layout(g.E, g.N, g.Z, c.np, c.epw, c.threads).total;
+    c.smem = smemq_layout(g.E, g.N, g.Z, c.np, c.epw, c.threads, sp_rule == TRX_SP_TORCH).total;
     c.blocks = (num_envs + c.epw - 1) / c.epw;
     return c;
 }
@@ -562,10 +641,31 @@ LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs) {
 hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream) {
-    LaunchCfg c = quad_launch_cfg(g, num_envs);
+    LaunchCfg c = quad_launch_cfg(g, num_envs, p.sp_rule);
     if (c.blocks == 0) return hipSuccess;
     if (c.threads > 512) return hipErrorInvalidConfiguration;
     dim3 grid(c.blocks), block(c.threads);
+    if (p.sp_rule == TRX_SP_TORCH) {
+        switch (c.np) {
+            case 8:
+                hipLaunchKernelGGL((env_kernel_q<8, kSpTorch>), grid, block, c.smem, stream, g, p, s, num_envs, c.epw,
+                                   mode, action, reward, done, valid, env_mask);
+                break;
+            case 16:
+                hipLaunchKernelGGL((env_kernel_q<16, kSpTorch>), grid, block, c.smem, stream, g, p, s, num_envs,
+                                   c.epw, mode, action, reward, done, valid, env_mask);
+                break;
+            case 24:
+                hipLaunchKernelGGL((env_kernel_q<24, kSpTorch>), grid, block, c.smem, stream, g, p, s, num_envs,
+                                   c.epw, mode, action, reward, done, valid, env_mask);
+                break;
+            default:
+                hipLaunchKernelGGL((env_kernel_q<32, kSpTorch>), grid, block, c.smem, stream, g, p, s, num_envs,
+                                   c.epw, mode, action, reward, done, valid, env_mask);
+                break;
+        }
+        return hipGetLastError();
+    }
     switch (c.np) {
         case 8:
             hipLaunchKernelGGL(env_kernel_q<8>, grid, block, c.smem, stream, g, p, s, num_envs, c.epw, mode, action,

@@ -65,6 +65,8 @@ int check_params(const trx_params* p) {
                     (double)p->bpr_beta);
     if (p->reward_mode < TRX_REWARD_DELTA || p->reward_mode > TRX_REWARD_REL_IMPROVE)
         return fail(TRX_EINVAL, "unsupported reward_mode %d", p->reward_mode);
+    if (p->sp_rule != TRX_SP_SCIPY && p->sp_rule != TRX_SP_TORCH)
+        return fail(TRX_EINVAL, "unsupported sp_rule %d", p->sp_rule);
     return TRX_OK;
 }
 
@@ -93,6 +95,9 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
         if (!s->gp) return fail(TRX_EINVAL, "state.gp is NULL (size it with trx_gp_state_bytes)");
         e = trx::launch_gp_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
                                   static_cast<hipStream_t>(stream));
+    } else if (p->sp_rule == TRX_SP_TORCH && g->dg.N > trx::kSmallMaxNodes) {
+        return fail(TRX_EUNSUP, "sp_rule TORCH (all-pairs Floyd-Warshall) supports N <= %d (got N=%d)",
+                    trx::kSmallMaxNodes, g->dg.N);
     } else if (g->dg.N <= trx::kSmallMaxNodes)
         e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
                                         static_cast<hipStream_t>(stream));

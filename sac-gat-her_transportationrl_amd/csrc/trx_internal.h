@@ -111,7 +111,7 @@ struct LaunchCfg {
     int blocks;    // grid
 };
 
-LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs);
+LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs, int sp_rule);
 hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream);

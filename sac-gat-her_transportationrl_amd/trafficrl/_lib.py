@@ -15,7 +15,8 @@ LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 3
+ABI_VERSION = 4
+SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
 # Every symbol include/trafficrl.h declares (tests check the export table).
@@ -37,7 +38,7 @@ class TrxParams(ctypes.Structure):
         ("bpr_alpha", ctypes.c_float), ("bpr_beta", ctypes.c_float),
         ("capacity_damage", ctypes.c_float), ("_pad0", ctypes.c_float),
         ("unassigned_penalty", ctypes.c_double),
-        ("reward_mode", ctypes.c_int32), ("_pad1", ctypes.c_int32),
+        ("reward_mode", ctypes.c_int32), ("sp_rule", ctypes.c_int32),
         ("reward_alpha", ctypes.c_double), ("reward_beta", ctypes.c_double),
         ("reward_gamma", ctypes.c_double), ("reward_clip", ctypes.c_double),
         ("gp_step", ctypes.c_double), ("gp_keep_paths", ctypes.c_int32), ("_pad2", ctypes.c_int32),

@@ -9,9 +9,13 @@ mutate those attributes and call compute_flow_assignment() (the greedy
 baseline does).  The numpy attributes are the source of truth between calls;
 each device call uploads the 4 x E link arrays and downloads the result.
 
-Backend keywords (sp_backend, use_torch, use_cugraph, force_gpu_sp) are
-accepted for compatibility; there is exactly one backend -- HIP on gfx950 --
-and it never falls back to the CPU.
+Backend keywords: everything runs on gfx950 and never falls back to the
+CPU.  sp_backend selects the shortest-path RULE of the all-or-nothing step,
+as in the reference: "torch" = _all_or_nothing_torch (float32 Floyd-Warshall,
+strict <, next_hop walk, repair_env.py:520-573; configs/sioux_falls.yaml and
+run_greedy.py), anything else = scipy dijkstra semantics (481-503; what "auto"
+resolves to without cupy/cugraph) -- see vec_env.resolve_sp_rule.  use_torch
+(torch BPR) and use_cugraph change no arithmetic here and are accepted as is.
 """
 from __future__ import annotations
 
@@ -102,7 +106,8 @@ class RepairEnv:
             assignment_iters=assignment_iters, assignment_method=self.assignment_method, reward_mode=reward_mode,
             reward_alpha=reward_alpha, reward_beta=reward_beta, reward_gamma=reward_gamma, reward_clip=reward_clip,
             capacity_damage=capacity_damage, unassigned_penalty=unassigned_penalty, gp_step=gp_step,
-            gp_keep_paths=gp_keep_paths, seeds=[seed], reset=False)
+            gp_keep_paths=gp_keep_paths, seeds=[seed], reset=False, sp_backend=self.sp_backend,
+            force_gpu_sp=self.force_gpu_sp)
         self._gp_cache = None    # GP path sets decoded from the device (od_paths, od_path_flows)
         self._gp_dirty = False   # set when a caller assigns od_paths / od_path_flows
         self._od_host = [{}, {}]
@@ -134,8 +139,9 @@ class RepairEnv:
         self.goal_mask = np.zeros(self.num_edges, dtype=np.float32)
         self.flow = np.zeros(self.num_edges, dtype=np.float32)
         if not _banner_done:
+            rule = "Floyd-Warshall (torch rule)" if self._vec.params.sp_rule == _lib.SP_TORCH else "Dijkstra (scipy rule)"
             print(f"[RepairEnv] backend=hip(gfx950) device={dev} method={self.assignment_method} "
-                  f"iters={self.assignment_iters}")
+                  f"iters={self.assignment_iters} sp_backend={self.sp_backend}: {rule}")
             _banner_done = True
         self._init_betweenness()
         self.reset(damaged_ratio=damaged_ratio)

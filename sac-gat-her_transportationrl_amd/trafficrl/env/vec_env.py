@@ -26,6 +26,30 @@ from .. import _lib
 from ..graph import DamageSampler, TrafficGraph
 
 
+def resolve_sp_rule(sp_backend: Optional[str], num_nodes: int, force_gpu_sp: bool = False) -> int:
+    """RepairEnv(sp_backend=...) -> the all-or-nothing shortest-path rule
+    (repair_env.py:111-161 backend resolution, 421-573 dispatch).
+
+    "torch": the reference's GPU backend _all_or_nothing_torch (float32
+      Floyd-Warshall, strict <, next_hop walk) -- what configs/sioux_falls.yaml
+      (sp_backend: torch, force_gpu_sp: true) and run_greedy.py select on a GPU;
+      here it runs as TRX_SP_TORCH inside the fused env kernel (N <= 32).
+    "scipy", "auto" and anything else: scipy's dijkstra semantics (float64
+      labels, heap order on ties) -- what "auto" resolves to where cupy and
+      cugraph are absent, as in the reference's own CPU runs.
+    "cupy" / "cugraph": their Dijkstra variants are not importable here, so
+      their tie order cannot be pinned; they get the scipy rule (a Dijkstra).
+    Every rule runs on the GPU, so force_gpu_sp never falls back; a rule this
+    build cannot run raises RuntimeError (never a silent substitution)."""
+    b = (sp_backend or "auto").lower()
+    if b == "torch":
+        if num_nodes > 32:
+            raise RuntimeError(f"sp_backend='torch' (all-pairs Floyd-Warshall rule) supports <= 32 nodes on this "
+                               f"build (got {num_nodes}); use sp_backend='scipy'")
+        return _lib.SP_TORCH
+    return _lib.SP_SCIPY
+
+
 @dataclass
 class VecObs:
     node_x: torch.Tensor     # [B, N, 4]
@@ -60,6 +84,8 @@ class VecRepairEnv:
         seeds: Optional[Sequence[int]] = None,
         graph: Optional[TrafficGraph] = None,
         reset: bool = True,
+        sp_backend: str = "auto",
+        force_gpu_sp: bool = False,
     ):
         if assignment_method.lower() not in _lib.METHODS:
             raise ValueError(f"assignment_method {assignment_method!r} not supported (msa, fw, cfw, gp)")
@@ -88,7 +114,8 @@ class VecRepairEnv:
             bpr_beta=bpr_beta, capacity_damage=capacity_damage, unassigned_penalty=unassigned_penalty,
             reward_mode=_lib.REWARD_MODES[reward_mode], reward_alpha=reward_alpha, reward_beta=reward_beta,
             reward_gamma=reward_gamma, reward_clip=reward_clip, gp_step=float(gp_step),
-            gp_keep_paths=int(gp_keep_paths))
+            gp_keep_paths=int(gp_keep_paths), sp_rule=resolve_sp_rule(sp_backend, N, force_gpu_sp))
+        self.sp_backend = (sp_backend or "auto").lower()
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         f64 = dict(dtype=torch.float64, device=dev)

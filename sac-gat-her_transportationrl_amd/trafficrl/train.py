@@ -16,10 +16,13 @@ GAT/SAC GEMMs).
 
 One iteration = every env takes one step: batched actor forward (one
 multinomial per env) -> trx_step + trx_observe -> transitions appended to the
-device replay.  Every `update_every` iterations, `updates_per_step` SAC
-updates on PER samples (+HER).  Multi-GPU (torchrun): envs and replay are
-per-rank shards; the only collective is one bucketed all-reduce of all SAC
-gradients per update (RCCL over xGMI) plus a few episode-metric reductions.
+device replay -> the SAC updates due (Trainer.updates_due: by default the
+reference's update-to-data ratio, updates_per_step / update_every updates per
+transition) on PER samples (+HER).  Multi-GPU (torchrun): envs and replay are
+per-rank shards; the only collective on the data path is one bucketed
+all-reduce of all SAC gradients per update (RCCL over xGMI); episode
+bookkeeping adds one 4-byte all-reduce per iteration and an all-gather of the
+finished episodes' metrics, so every rank stops at the same iteration.
 """
 from __future__ import annotations
 
@@ -41,17 +44,25 @@ from .rl.replay import DeviceReplay, her_relabel
 from . import _lib
 from .rl.sac import DiscreteSAC
 
+# Fallbacks of the reference trainer's cfg.get(...) calls (src/train.py:146-351):
+# a reference yaml that omits a key trains the same way here.  Keys the
+# reference reads without a default (cfg["..."]) take configs/sioux_falls.yaml's
+# values.  The Sioux Falls training setup itself is trafficrl/sf_sac.yaml
+# (sf_config()).  New keys: num_envs, amp (None = fp32 like the reference;
+# "bf16" autocast), graph_update, update_unit, log_every, save_every.
 DEFAULTS: Dict = dict(
-    damaged_ratio=0.3, assignment_iters=30, assignment_method="msa", reward_mode="rel_improve", reward_alpha=1.0,
-    reward_beta=0.0, reward_gamma=0.0, reward_clip=2.0, reward_scale=0.5, capacity_damage=1e-3,
-    unassigned_penalty=1e4, fixed_damage=True, fixed_damage_seed=42, episodes=2000, max_steps=100,
-    buffer_size=1_000_000, batch_start=2000, batch_size=256, update_every=4, updates_per_step=1, per_alpha=0.6,
-    per_beta=0.4, per_eps=1e-6, her_ratio=0.0, hidden_dim=256, embed_dim=256, gat_layers=3, lr=1e-4,
-    actor_lr=None, critic_lr=None, alpha_lr=None, gamma=0.99, target_tau=0.001, grad_clip=1.0,
-    share_critic_encoder=False, alpha_init=0.1, alpha_max=2.5, target_entropy_ratio=0.2, eval_every=20,
-    eval_seeds=[42], early_stop_patience=2000, seed=42, output_dir="outputs", num_envs=256, amp="bf16",
+    damaged_ratio=0.3, assignment_iters=30, assignment_method="msa", sp_backend="auto", force_gpu_sp=False,
+    reward_mode="delta", reward_alpha=1.0, reward_beta=10.0, reward_gamma=0.1, reward_clip=0.0, reward_scale=1.0,
+    capacity_damage=1e-3, unassigned_penalty=2e7, gp_step=1.0, gp_keep_paths=3, fixed_damage=False,
+    fixed_damage_seed=None, episodes=2000, max_steps=0, buffer_size=1_000_000, batch_start=2000, batch_size=256,
+    update_every=1, updates_per_step=1, update_unit="transitions", per_alpha=0.6, per_beta=0.4, per_eps=1e-6,
+    her_ratio=0.0, hidden_dim=256, embed_dim=256, gat_layers=3, lr=1e-4, actor_lr=None, critic_lr=None,
+    alpha_lr=None, gamma=0.99, target_tau=0.001, grad_clip=None, share_critic_encoder=True, alpha_init=0.1,
+    alpha_max=None, target_entropy_ratio=0.6, eval_every=50, eval_seeds=[1001, 1002, 1003, 1004, 1005],
+    early_stop_patience=500, early_stop_min_delta=0.0, seed=42, output_dir="outputs", num_envs=256, amp=None,
     log_every=10, save_every=50, net_path=None, trips_path=None, graph_update=True,
 )
+SF_CONFIG = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sf_sac.yaml")
 
 
 def load_config(path: Optional[str]) -> Dict:
@@ -60,10 +71,18 @@ def load_config(path: Optional[str]) -> Dict:
         import yaml
         with open(path) as fh:
             cfg.update(yaml.safe_load(fh) or {})
+    if not cfg.get("eval_seeds"):   # train.py:351 `cfg.get("eval_seeds") or [1001..1005]`
+        cfg["eval_seeds"] = list(DEFAULTS["eval_seeds"])
     if os.environ.get("SEED_OVERRIDE") is not None:  # train.py:218-222
         cfg["seed"] = int(os.environ["SEED_OVERRIDE"])
         cfg["output_dir"] = os.path.join(cfg["output_dir"], f"seed_{cfg['seed']}")
     return cfg
+
+
+def sf_config() -> Dict:
+    """The Sioux Falls GAT-SAC setup (trafficrl/sf_sac.yaml: the reference's
+    configs/sioux_falls.yaml values plus num_envs / amp)."""
+    return load_config(SF_CONFIG)
 
 
 def batched_topology(edge_index: torch.Tensor, num_nodes: int, B: int):
@@ -212,7 +231,8 @@ class Trainer:
             reward_alpha=cfg["reward_alpha"], reward_beta=cfg["reward_beta"], reward_gamma=cfg["reward_gamma"],
             reward_clip=cfg["reward_clip"], capacity_damage=cfg["capacity_damage"],
             unassigned_penalty=cfg["unassigned_penalty"], fixed_damage=cfg["fixed_damage"],
-            fixed_damage_seed=cfg["fixed_damage_seed"], seeds=seeds, reset=False)
+            fixed_damage_seed=cfg["fixed_damage_seed"], seeds=seeds, reset=False, sp_backend=cfg["sp_backend"],
+            force_gpu_sp=cfg["force_gpu_sp"], gp_step=cfg["gp_step"], gp_keep_paths=cfg["gp_keep_paths"])
         self.N, self.E = self.env.num_nodes, self.env.num_edges
         amp = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(str(cfg.get("amp")).lower())
         self.use_graphs = bool(cfg.get("graph_update", True)) and self.device.type == "cuda"
@@ -254,6 +274,7 @@ class Trainer:
         self._u = torch.empty(bs, dtype=torch.float64, device=self.device)      # PER draws
         self._her_u = torch.empty(bs, dtype=torch.float32, device=self.device)  # HER draws
         self._graphed = GraphedUpdate(self) if self.use_graphs else None
+        self._update_credit = 0.0
 
     # ------------------------------------------------------------ acting
     def act(self, obs, deterministic=False):
@@ -322,6 +343,41 @@ class Trainer:
         self.agent.apply_gradients(self.cfg.get("alpha_max"))
         self.replay.update_priorities(s.idx, out["td_errors"])
 
+    def updates_due(self, it: int) -> int:
+        """SAC updates to run after iteration `it` (its B transitions added).
+
+        update_unit "transitions" (default) keeps the reference's
+        update-to-data ratio: src/train.py:954-955 runs `updates_per_step`
+        updates every `update_every` env steps of its single env, i.e.
+        updates_per_step / update_every updates per transition; here B
+        transitions arrive per iteration, so the credit B * updates_per_step /
+        update_every accrues per iteration and whole updates are paid out.
+        update_unit "iterations": `updates_per_step` updates every
+        `update_every` vector iterations (B transitions each) -- the bench's
+        throughput workload, a UTD ratio B * update_every times lower.
+        No update until the replay holds more than batch_start transitions."""
+        cfg = self.cfg
+        if self.replay.size <= int(cfg["batch_start"]):
+            return 0
+        ups, every = int(cfg["updates_per_step"]), int(cfg["update_every"])
+        if str(cfg.get("update_unit", "transitions")) == "iterations":
+            return ups if it % every == 0 else 0
+        self._update_credit += self.B * ups / every
+        n = int(self._update_credit)
+        self._update_credit -= n
+        return n
+
+    def prime_update(self):
+        """Run the eager warm-up updates and the HIP-graph capture now, so that
+        later updates are graph replays (a steady-state timed region never
+        contains an eager update or a capture)."""
+        if self._graphed is None:
+            return
+        while self._graphed.g_grads is None:
+            self.update()
+        self.update()
+        torch.cuda.synchronize(self.device)
+
     # -------------------------------------------------------------- loop
     def iteration(self, obs, it: int):
         cfg, env = self.cfg, self.env
@@ -347,29 +403,53 @@ class Trainer:
         self.ep_tstt_sum += env.tstt
         self.ep_auc += 0.5 * (self.ep_prev_tstt + env.tstt) * (self.ep_len > 1)
         self.ep_prev_tstt.copy_(env.tstt)
-        if self.replay.size > int(cfg["batch_start"]) and it % int(cfg["update_every"]) == 0:
-            for _ in range(int(cfg["updates_per_step"])):
-                self.update()
+        for _ in range(self.updates_due(it)):
+            self.update()
         finished = done | trunc
         return next_obs, finished
 
-    def record(self, finished: torch.Tensor):
-        n = int(finished.sum())
-        if n == 0:
-            return
+    def _gather_episodes(self, finished: torch.Tensor):
+        """Per-episode metrics of the envs that finished this iteration, over
+        ALL ranks (env order: rank-major, env id within a rank), so that every
+        rank takes the same stop / eval / patience decisions.  Columns: mask,
+        reward, tstt_mean, tstt_last, auc."""
         f = finished
-        rec = {
-            "episodes": n,
-            "reward": float(self.ep_reward[f].mean()),
-            "tstt_mean": float((self.ep_tstt_sum[f] / self.ep_len[f]).mean()),
-            "tstt_last": float(self.env.tstt[f].mean()),
-            "auc": float(self.ep_auc[f].mean()),
-        }
-        self.episodes_done += n
-        self.history.append(rec)
+        ln = torch.clamp(self.ep_len, min=1).to(torch.float64)
+        rows = torch.stack([f.to(torch.float64), self.ep_reward, self.ep_tstt_sum / ln, self.env.tstt,
+                            self.ep_auc], dim=1)
+        if self.world > 1:
+            import torch.distributed as dist
+            parts = [torch.empty_like(rows) for _ in range(self.world)]
+            dist.all_gather(parts, rows)
+            rows = torch.cat(parts)
+        rows = rows[rows[:, 0] > 0].cpu().numpy()
+        return rows
+
+    def record(self, finished: torch.Tensor):
+        """Book the finished episodes (all ranks) into history; returns their
+        per-episode rows (see _gather_episodes)."""
+        rows = self._gather_episodes(finished)
+        n = len(rows)
+        f = finished
         for t in (self.ep_reward, self.ep_tstt_sum, self.ep_auc):
             t.masked_fill_(f, 0.0)
         self.ep_len.masked_fill_(f, 0)
+        if n == 0:
+            return rows
+        rec = {"episodes": n, "reward": float(rows[:, 1].mean()), "tstt_mean": float(rows[:, 2].mean()),
+               "tstt_last": float(rows[:, 3].mean()), "auc": float(rows[:, 4].mean())}
+        self.episodes_done += n
+        self.history.append(rec)
+        return rows
+
+    def _any_finished(self, finished: torch.Tensor) -> bool:
+        """finished.any() over all ranks (one tiny all-reduce per iteration
+        when world > 1; the single-GPU path syncs on the flag as before)."""
+        flag = finished.any().to(torch.int32).reshape(1)
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        return bool(flag.item())
 
     def evaluate(self, seeds=None) -> Dict:
         """Deterministic-policy episodes (src/train.py:590-664) on a separate env."""
@@ -382,7 +462,9 @@ class Trainer:
                           reward_gamma=cfg["reward_gamma"], reward_clip=cfg["reward_clip"],
                           capacity_damage=cfg["capacity_damage"], unassigned_penalty=cfg["unassigned_penalty"],
                           fixed_damage=cfg["fixed_damage"], fixed_damage_seed=cfg["fixed_damage_seed"],
-                          seeds=list(seeds), reset=False)
+                          seeds=list(seeds), reset=False, sp_backend=cfg["sp_backend"],
+                          force_gpu_sp=cfg["force_gpu_sp"], gp_step=cfg["gp_step"],
+                          gp_keep_paths=cfg["gp_keep_paths"])
         obs = ev.reset()
         n = len(seeds)
         ei, bv = batched_topology(ev.edge_index, self.N, n)
@@ -407,39 +489,55 @@ class Trainer:
             self.agent.save(os.path.join(self.cfg["output_dir"], f"model_{tag}.pt"))
 
     def run(self, max_iters: Optional[int] = None):
+        """Training loop (src/train.py:915-1041 serial path, vectorised).
+        Early stopping follows the reference per finished episode: an episode
+        whose TSTT mean beats the best by early_stop_min_delta resets the
+        patience, any other adds one; stop at early_stop_patience.  Episodes
+        are taken in a fixed (rank, env id) order from all ranks, so every
+        rank stops at the same iteration (no rank is left in an all-reduce)."""
         cfg = self.cfg
         self._reset_envs(None)
         obs = self.env.observe()
         best, patience = math.inf, 0
+        min_delta = float(cfg.get("early_stop_min_delta", 0.0) or 0.0)
         t0 = time.perf_counter()
         it = 0
         next_eval = int(cfg["eval_every"])
-        while self.episodes_done * self.world < int(cfg["episodes"]):
+        stop = False
+        while self.episodes_done < int(cfg["episodes"]) and not stop:
             if max_iters is not None and it >= max_iters:
                 break
             obs, finished = self.iteration(obs, it)
             it += 1
-            if bool(finished.any()):
-                self.record(finished)
-                self._reset_envs(finished)
-                obs = self.env.observe()
-                rec = self.history[-1]
-                if self.rank == 0:
-                    self.logger.info(f"it {it} episodes {self.episodes_done * self.world} reward {rec['reward']:.3f} "
-                                     f"tstt_mean {rec['tstt_mean']:.2f} auc {rec['auc']:.1f} "
-                                     f"steps/s {it * self.B * self.world / (time.perf_counter() - t0):.0f}")
-                if rec["tstt_mean"] < best - 1e-6:
-                    best, patience = rec["tstt_mean"], 0
+            if not self._any_finished(finished):
+                continue
+            rows = self.record(finished)
+            self._reset_envs(finished)
+            obs = self.env.observe()
+            if len(rows) == 0:
+                continue
+            rec = self.history[-1]
+            if self.rank == 0:
+                self.logger.info(f"it {it} episodes {self.episodes_done} reward {rec['reward']:.3f} "
+                                 f"tstt_mean {rec['tstt_mean']:.2f} auc {rec['auc']:.1f} "
+                                 f"steps/s {it * self.B * self.world / (time.perf_counter() - t0):.0f}")
+            for tm in rows[:, 2]:   # train.py:1031-1041, one finished episode at a time
+                if tm < best - min_delta:
+                    best, patience = float(tm), 0
                 else:
                     patience += 1
                 if patience >= int(cfg["early_stop_patience"]):
-                    break
-                if self.episodes_done >= next_eval and cfg["eval_every"] > 0:
-                    next_eval += int(cfg["eval_every"])
-                    ev = self.evaluate()
+                    stop = True
                     if self.rank == 0:
-                        self.logger.info(f"eval {ev}")
-                    self.save("last")
+                        self.logger.info(f"Early stopping at episode {self.episodes_done}: no TSTT-mean "
+                                         f"improvement for {patience} episodes")
+                    break
+            if not stop and self.episodes_done >= next_eval and cfg["eval_every"] > 0:
+                next_eval += int(cfg["eval_every"])
+                ev = self.evaluate()
+                if self.rank == 0:
+                    self.logger.info(f"eval {ev}")
+                self.save("last")
         self.save("last")
         if self.rank == 0:
             with open(os.path.join(cfg["output_dir"], "train_metrics.json"), "w") as fh:
@@ -449,7 +547,7 @@ class Trainer:
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description="vectorised GAT-SAC training (src/train.py equivalent)")
-    ap.add_argument("--config", default=None)
+    ap.add_argument("--config", default=SF_CONFIG)
     ap.add_argument("--num-envs", type=int, default=None)
     ap.add_argument("--episodes", type=int, default=None)
     ap.add_argument("--max-iters", type=int, default=None)

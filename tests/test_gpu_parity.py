@@ -150,15 +150,16 @@ def test_env_mask_leaves_other_envs_untouched(gd, tgraph):
     assert torch.equal(env.flow[keep.cuda()], before[keep.cuda()])
 
 
-@pytest.mark.parametrize("method", ["msa", "fw"])
-def test_greedy_episode_bitexact(method):
+@pytest.mark.parametrize("method,iters", [("msa", 30), ("fw", 30), ("msa", 60)])
+def test_greedy_episode_bitexact(method, iters):
     """Config #1: greedy one-step episode through the drop-in RepairEnv facade
-    + batched what-if; actions and TSTT curve == reference golden."""
+    + batched what-if; actions and TSTT curve == reference golden (K = 60 is
+    configs/sioux_falls.yaml's assignment_iters)."""
     from trafficrl.baselines import run_episode, select_greedy_one_step
     from trafficrl.data import sioux_falls
     from trafficrl.env import RepairEnv
-    z = np.load(golden(f"sf_greedy_{method}30_crpow.npz"))
-    env = RepairEnv(sioux_falls(), assignment_iters=30, assignment_method=method, fixed_damage=True,
+    z = np.load(golden(f"sf_greedy_{method}{iters}_crpow.npz"))
+    env = RepairEnv(sioux_falls(), assignment_iters=iters, assignment_method=method, fixed_damage=True,
                     fixed_damage_seed=42, seed=42, reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0,
                     reward_gamma=0.0, reward_clip=2.0, unassigned_penalty=1e4)
     assert env.initial_tstt == float(z["initial_tstt"])

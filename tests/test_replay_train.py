@@ -160,10 +160,10 @@ def test_her_relabel_quirks():
 
 
 def test_short_training_run(tmp_path):
-    from trafficrl.train import Trainer, load_config
-    cfg = load_config(None)
+    from trafficrl.train import Trainer, sf_config
+    cfg = sf_config()
     cfg.update(num_envs=64, batch_start=128, batch_size=32, hidden_dim=32, embed_dim=32, episodes=64,
-               eval_every=64, output_dir=str(tmp_path), update_every=1, her_ratio=0.5)
+               eval_every=64, output_dir=str(tmp_path), update_every=1, update_unit="iterations", her_ratio=0.5)
     tr = Trainer(cfg, device="cuda", log=False)
     hist = tr.run(max_iters=30)
     assert tr.episodes_done >= 64 and len(hist) >= 1
@@ -183,12 +183,13 @@ def test_graphed_update_matches_eager(tmp_path, her, hidden, embed):
     equal up to kernel-order rounding after several updates.  hidden 64 x 4
     heads / embed 256 puts the no-grad passes on the fused inference kernels
     inside the captured graph."""
-    from trafficrl.train import Trainer, load_config
+    from trafficrl.train import Trainer, sf_config
     trs = []
     for graphed in (False, True):
-        cfg = load_config(None)
+        cfg = sf_config()
         cfg.update(num_envs=32, batch_start=64, batch_size=16, hidden_dim=hidden, embed_dim=embed, eval_every=0,
-                   output_dir=str(tmp_path), update_every=1, her_ratio=her, graph_update=graphed)
+                   output_dir=str(tmp_path), update_every=1, update_unit="iterations", her_ratio=her,
+                   graph_update=graphed)
         tr = Trainer(cfg, device="cuda", log=False)
         trs.append(tr)
     ag = trs[0].agent   # same (device-side step count) Adam arithmetic in both

@@ -18,10 +18,10 @@ def main():
     if os.environ.get("TRX_LIB"):   # A/B a second build of libtrafficrl.so
         from trafficrl import _lib
         _lib.LIB_PATH = os.path.abspath(os.environ["TRX_LIB"])
-    from trafficrl.train import Trainer, load_config
+    from trafficrl.train import Trainer, sf_config
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-    cfg = load_config(None)
-    cfg.update(num_envs=B, batch_start=256, eval_every=0, output_dir="/tmp/trx_prof", buffer_size=65536)
+    cfg = sf_config()
+    cfg.update(num_envs=B, batch_start=256, update_unit="iterations", eval_every=0, output_dir="/tmp/trx_prof", buffer_size=65536)
     tr = Trainer(cfg, device="cuda:0", log=False)
     tr._reset_envs(None)
     obs = tr.env.observe()

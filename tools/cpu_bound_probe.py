@@ -12,10 +12,10 @@ sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
 
 
 def main():
-    from trafficrl.train import Trainer, load_config
+    from trafficrl.train import Trainer, sf_config
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-    cfg = load_config(None)
-    cfg.update(num_envs=B, batch_start=256, batch_size=256, update_every=4, eval_every=0,
+    cfg = sf_config()
+    cfg.update(num_envs=B, batch_start=256, batch_size=256, update_every=4, update_unit="iterations", eval_every=0,
                output_dir="/tmp/trx_probe", amp="bf16", fixed_damage=True)
     tr = Trainer(cfg, device="cuda:0", log=False)
     tr._reset_envs(None)

@@ -13,10 +13,10 @@ from trafficrl import _lib  # noqa: E402
 _lib.LIB_PATH = os.path.join(ROOT, "sac-gat-her_transportationrl_amd", "trafficrl", "libtrafficrl_stamps.so")
 L = _lib.load()
 L.trx_debug_infer_cycles.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-from trafficrl.train import Trainer, load_config  # noqa: E402
+from trafficrl.train import Trainer, sf_config  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-cfg = load_config(None)
+cfg = sf_config()
 cfg.update(num_envs=B, batch_start=10 ** 9, eval_every=0, output_dir="/tmp/trx_stamps", buffer_size=4096)
 tr = Trainer(cfg, device="cuda:0", log=False)
 tr._reset_envs(None)

@@ -15,10 +15,10 @@ sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
 def main():
     from torch.profiler import ProfilerActivity, profile
 
-    from trafficrl.train import Trainer, load_config
+    from trafficrl.train import Trainer, sf_config
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 60
-    cfg = load_config(None)
-    cfg.update(num_envs=512, batch_start=256, eval_every=0, output_dir="/tmp/trx_prof", buffer_size=65536)
+    cfg = sf_config()
+    cfg.update(num_envs=512, batch_start=256, update_unit="iterations", eval_every=0, output_dir="/tmp/trx_prof", buffer_size=65536)
     tr = Trainer(cfg, device="cuda:0", log=False)
     tr.use_graphs = False
     tr._graphed = None
