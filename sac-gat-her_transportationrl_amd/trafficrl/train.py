@@ -71,6 +71,17 @@ def load_config(path: Optional[str]) -> Dict:
         import yaml
         with open(path) as fh:
             cfg.update(yaml.safe_load(fh) or {})
+    # PyYAML (YAML 1.1) reads exponents without a sign ("1.0e4", as in the
+    # reference's configs/sioux_falls.yaml) as strings; the reference's float()
+    # / arithmetic accepts them, so numeric-looking strings become numbers here
+    for k, v in list(cfg.items()):
+        if isinstance(v, str):
+            try:
+                f = float(v)
+            except ValueError:
+                continue
+            cfg[k] = int(f) if isinstance(DEFAULTS.get(k), int) and not isinstance(DEFAULTS.get(k), bool) \
+                and f == int(f) else f
     if not cfg.get("eval_seeds"):   # train.py:351 `cfg.get("eval_seeds") or [1001..1005]`
         cfg["eval_seeds"] = list(DEFAULTS["eval_seeds"])
     if os.environ.get("SEED_OVERRIDE") is not None:  # train.py:218-222
@@ -274,7 +285,7 @@ class Trainer:
         self._u = torch.empty(bs, dtype=torch.float64, device=self.device)      # PER draws
         self._her_u = torch.empty(bs, dtype=torch.float32, device=self.device)  # HER draws
         self._graphed = GraphedUpdate(self) if self.use_graphs else None
-        self._update_credit = 0.0
+        self._transitions = 0   # env transitions added so far (update schedule)
 
     # ------------------------------------------------------------ acting
     def act(self, obs, deterministic=False):
@@ -348,24 +359,25 @@ class Trainer:
 
         update_unit "transitions" (default) keeps the reference's
         update-to-data ratio: src/train.py:954-955 runs `updates_per_step`
-        updates every `update_every` env steps of its single env, i.e.
-        updates_per_step / update_every updates per transition; here B
-        transitions arrive per iteration, so the credit B * updates_per_step /
-        update_every accrues per iteration and whole updates are paid out.
+        updates every `update_every` env steps of its single env.  Here the
+        B transitions of an iteration count as B consecutive env steps, so
+        after the iteration that takes the transition count from T0 to T1,
+        floor(T1 / update_every) - floor(T0 / update_every) update rounds of
+        `updates_per_step` updates are due (B = 1 reproduces the reference's
+        timing).
         update_unit "iterations": `updates_per_step` updates every
         `update_every` vector iterations (B transitions each) -- the bench's
         throughput workload, a UTD ratio B * update_every times lower.
         No update until the replay holds more than batch_start transitions."""
         cfg = self.cfg
+        ups, every = int(cfg["updates_per_step"]), int(cfg["update_every"])
+        t0 = self._transitions
+        self._transitions = t1 = t0 + self.B
         if self.replay.size <= int(cfg["batch_start"]):
             return 0
-        ups, every = int(cfg["updates_per_step"]), int(cfg["update_every"])
         if str(cfg.get("update_unit", "transitions")) == "iterations":
             return ups if it % every == 0 else 0
-        self._update_credit += self.B * ups / every
-        n = int(self._update_credit)
-        self._update_credit -= n
-        return n
+        return (t1 // every - t0 // every) * ups
 
     def prime_update(self):
         """Run the eager warm-up updates and the HIP-graph capture now, so that

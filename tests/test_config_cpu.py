@@ -1,0 +1,58 @@
+"""Trainer configuration (CPU): reference cfg.get fallbacks, YAML numeric
+strings, and the update schedule (update-to-data ratio)."""
+from types import SimpleNamespace
+
+from trafficrl.train import DEFAULTS, Trainer, load_config, sf_config
+
+
+def test_defaults_are_the_reference_fallbacks():
+    # src/train.py cfg.get(key, default) fallbacks
+    ref = dict(reward_mode="delta", reward_beta=10.0, reward_gamma=0.1, reward_clip=0.0, reward_scale=1.0,
+               update_every=1, updates_per_step=1, fixed_damage=False, early_stop_patience=500,
+               early_stop_min_delta=0.0, share_critic_encoder=True, target_entropy_ratio=0.6, max_steps=0,
+               unassigned_penalty=2e7, eval_every=50, sp_backend="auto", force_gpu_sp=False, gp_keep_paths=3,
+               per_alpha=0.6, per_beta=0.4, per_eps=1e-6, her_ratio=0.0, capacity_damage=1e-3, grad_clip=None,
+               alpha_max=None, alpha_init=0.1)
+    for k, v in ref.items():
+        assert DEFAULTS[k] == v, k
+    assert DEFAULTS["eval_seeds"] == [1001, 1002, 1003, 1004, 1005]
+    assert DEFAULTS["amp"] is None   # fp32 like the reference
+
+
+def test_yaml_numeric_strings(tmp_path):
+    p = tmp_path / "c.yaml"
+    p.write_text("unassigned_penalty: 1.0e4\nbuffer_size: 1.0e6\nlr: 1.0e-4\neval_seeds: []\nsp_backend: torch\n")
+    c = load_config(str(p))
+    assert c["unassigned_penalty"] == 1e4 and isinstance(c["unassigned_penalty"], float)
+    assert c["buffer_size"] == 1000000 and isinstance(c["buffer_size"], int)
+    assert c["lr"] == 1e-4 and c["sp_backend"] == "torch"
+    assert c["eval_seeds"] == [1001, 1002, 1003, 1004, 1005]
+
+
+def test_sf_config_mirrors_reference_yaml():
+    c = sf_config()
+    assert c["sp_backend"] == "torch" and c["force_gpu_sp"] is True
+    assert c["reward_mode"] == "rel_improve" and c["reward_clip"] == 2.0 and c["reward_scale"] == 0.5
+    assert c["update_every"] == 4 and c["update_unit"] == "transitions"
+
+
+def _fake(B, size, **cfg):
+    base = dict(batch_start=100, updates_per_step=1, update_every=4, update_unit="transitions")
+    base.update(cfg)
+    return SimpleNamespace(cfg=base, B=B, replay=SimpleNamespace(size=size), _transitions=0)
+
+
+def test_update_schedule_transitions_keeps_reference_ratio():
+    # reference: updates_per_step updates every update_every env steps (src/train.py:954-955)
+    f = _fake(B=10, size=1000)
+    n = [Trainer.updates_due(f, it) for it in range(8)]
+    assert sum(n) == 10 * 8 // 4 and n[:4] == [2, 3, 2, 3]
+    f = _fake(B=1, size=1000, updates_per_step=2)
+    assert [Trainer.updates_due(f, it) for it in range(8)] == [0, 0, 0, 2, 0, 0, 0, 2]
+    f = _fake(B=10, size=50)      # replay not yet past batch_start
+    assert Trainer.updates_due(f, 0) == 0 and f._transitions == 10
+
+
+def test_update_schedule_iterations():
+    f = _fake(B=4096, size=10 ** 6, update_unit="iterations", updates_per_step=1, update_every=4)
+    assert [Trainer.updates_due(f, it) for it in range(8)] == [1, 0, 0, 0, 1, 0, 0, 0]
