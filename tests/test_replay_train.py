@@ -188,6 +188,7 @@ def test_graphed_update_matches_eager(tmp_path, her, hidden, embed):
     for graphed in (False, True):
         cfg = sf_config()
         cfg.update(num_envs=32, batch_start=64, batch_size=16, hidden_dim=hidden, embed_dim=embed, eval_every=0,
+                   lr=1e-4, actor_lr=None, critic_lr=None, alpha_lr=None,
                    output_dir=str(tmp_path), update_every=1, update_unit="iterations", her_ratio=her,
                    graph_update=graphed)
         tr = Trainer(cfg, device="cuda", log=False)
