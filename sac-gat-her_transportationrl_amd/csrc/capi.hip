@@ -78,6 +78,15 @@ int check_state(const trx_state* s, bool need_initial) {
     return TRX_OK;
 }
 
+// TRX_KERNEL=quad selects the previous small-graph kernel (A/B runs)
+bool use_packed() {
+    static const bool on = [] {
+        const char* e = getenv("TRX_KERNEL");
+        return !(e && std::string(e) == "quad");
+    }();
+    return on;
+}
+
 int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mode, const int32_t* action,
         double* reward, uint8_t* done, uint8_t* valid, const uint8_t* env_mask, void* ws, void* stream) {
     int rc;
@@ -98,7 +107,11 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
     } else if (p->sp_rule == TRX_SP_TORCH && g->dg.N > trx::kSmallMaxNodes) {
         return fail(TRX_EUNSUP, "sp_rule TORCH (all-pairs Floyd-Warshall) supports N <= %d (got N=%d)",
                     trx::kSmallMaxNodes, g->dg.N);
-    } else if (g->dg.N <= trx::kSmallMaxNodes)
+    } else if (g->dg.N <= trx::kSmallMaxNodes && p->sp_rule == TRX_SP_SCIPY && use_packed() &&
+               trx::packed_ok(g->dg, *p))
+        e = trx::launch_env_kernel_packed(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
+                                          static_cast<hipStream_t>(stream));
+    else if (g->dg.N <= trx::kSmallMaxNodes)
         e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
                                         static_cast<hipStream_t>(stream));
     else
@@ -351,13 +364,27 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     d.KMAX = KMAX;
     d.big_g = big_g;
     d.total_demand = total;
-    float mt = 0.f, mc = 0.f;
+    float mt = 0.f, mc = 0.f, mn = E > 0 ? t0[0] : 1.0f;
     for (int e = 0; e < E; ++e) {
         mt = std::max(mt, t0[e]);
         mc = std::max(mc, cap0[e]);
+        mn = std::min(mn, t0[e]);
     }
     d.max_t0 = E > 0 ? mt : 1.0f;
     d.max_cap = E > 0 ? mc : 1.0f;
+    d.min_t0 = mn;
+    // tie candidates of the packed-key kernel: every pair of in-links of a node
+    std::vector<uint32_t> tie_pairs;
+    if (small)
+        for (int v = 0; v < N; ++v)
+            for (int a = in_ptr[v]; a < in_ptr[v + 1]; ++a)
+                for (int b = a + 1; b < in_ptr[v + 1]; ++b) {
+                    const uint32_t e1 = (uint32_t)std::min(in_eid[a], in_eid[b]);
+                    const uint32_t e2 = (uint32_t)std::max(in_eid[a], in_eid[b]);
+                    tie_pairs.push_back(e1 | (e2 << 16));
+                }
+    d.npairs = (int)tie_pairs.size();
+    if (tie_pairs.empty()) tie_pairs.push_back(0u);
     int rc = TRX_OK;
     std::vector<int32_t> vsrc(src, src + E), vdst(dst, dst + E);
     std::vector<float> vt0(t0, t0 + E), vcap(cap0, cap0 + E);
@@ -374,7 +401,7 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
         (rc = upload(g, od_dem, &d.od_dem)) || (rc = upload(g, b_origin, &d.b_origin)) ||
         (rc = upload(g, b_od_dst, &d.b_od_dst)) || (rc = upload(g, b_lsrc, &d.b_lsrc)) ||
         (rc = upload(g, b_indptr, &d.b_indptr)) || (rc = upload(g, b_indices, &d.b_indices)) ||
-        (rc = upload(g, b_csr_eid, &d.b_csr_eid))) {
+        (rc = upload(g, b_csr_eid, &d.b_csr_eid)) || (rc = upload(g, tie_pairs, &d.tie_pairs))) {
         trx_graph_destroy(g);
         return rc;
     }

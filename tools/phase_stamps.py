@@ -15,6 +15,10 @@ from trafficrl import _lib  # noqa: E402
 
 _lib.LIB_PATH = os.path.join(ROOT, "sac-gat-her_transportationrl_amd", "trafficrl", "libtrafficrl_stamps.so")
 L = _lib.load()
+# the packed-key kernel (assign_packed.hip) has its own counters
+PACKED = os.environ.get("TRX_KERNEL", "packed") != "quad"
+if PACKED:
+    L.trx_debug_phase_cycles = L.trx_debug_phase_cycles_p
 L.trx_debug_phase_cycles.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 from trafficrl.data import sioux_falls  # noqa: E402
 from trafficrl.env import VecRepairEnv  # noqa: E402
@@ -28,7 +32,8 @@ for _ in range(5):
     a = (torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32)
     env.step(a, observe=False)
 L.trx_debug_phase_cycles(buf, 1)
-names = ["load", "cost build", "dijkstra", "tie check+replay", "aon", "update+bpr", "tstt+store"]
+names = (["load", "dijkstra", "tie check+replay", "aon walk", "barrier wait", "update+bpr", "tie candidates"]
+         if PACKED else ["load", "cost build", "dijkstra", "tie check+replay", "aon", "update+bpr", "tstt+store"])
 tot = sum(buf[i] for i in range(7))
 for i, n in enumerate(names):
     print(f"{n:>14}: {buf[i] / tot * 100:6.2f} %  ({buf[i] / 5 / (B / 4) / 30:.0f} cycles/WG/iter)")
