@@ -141,7 +141,7 @@ __host__ __device__ inline SmemP smemp_layout(int E, int N, int Z, int NP, int E
 // DPP quad_perm: xor 1 = [1,0,3,2] (0xB1), xor 2 = [2,3,0,1] (0x4E)
 template <int CTRL>
 __device__ __forceinline__ uint32_t qp(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
 }
 template <int CTRL>
 __device__ __forceinline__ uint64_t qp64(uint64_t x) {
@@ -371,16 +371,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRX_PA
                 pr[i] = kNoPred;
             }
             for (int k = 0; k < N; ++k) {
-                uint64_t best = key[0];
+                // argmin over the lane's slots (pairwise: short dependency chain)
+                uint64_t m[NPL];
 #pragma unroll
-                for (int i = 1; i < NPL; ++i) best = key[i] < best ? key[i] : best;
+                for (int i = 0; i < NPL; ++i) m[i] = key[i];
+#pragma unroll
+                for (int w = 1; w < NPL; w *= 2)
+#pragma unroll
+                    for (int i = 0; i + w < NPL; i += 2 * w) m[i] = m[i + w] < m[i] ? m[i + w] : m[i];
+                uint64_t best = m[0];
                 uint64_t o = qp64<0xB1>(best);
                 best = o < best ? o : best;
                 o = qp64<0x4E>(best);
                 best = o < best ? o : best;
                 if (best >= kInfKey) break;  // quad-uniform: the rest is unreachable
                 const uint32_t u = (uint32_t)best & 31u;
-                if (j == 0) ol[k] = (uint8_t)u;
+                ol[k] = (uint8_t)u;  // the quad's 4 lanes store the same byte
                 nscan = k + 1;
                 const uint32_t bh = (uint32_t)(best >> 32) | kSign;
 #pragma unroll
