@@ -431,15 +431,20 @@ class DiscreteSAC:
                 weights_tensor = weights_tensor.unsqueeze(0).expand_as(reward)
         edge_batch = batch_vec[edge_index[0]]
         reg = is_regular_edges(edge_index, batch_vec, B)
+        # The no-grad passes get an autocast region of their own: autocast caches
+        # a weight's bf16 cast for the rest of its region, and a cast made under
+        # no_grad carries no autograd history -- reused by the actor's training
+        # forward below it would silently cut the gradient of every weight cast
+        # in both passes (the actor's GAT lin weights).
+        with self._amp(), torch.no_grad():
+            _, next_probs, _ = self.actor(next_node_x, edge_index, next_edge_attr, next_action_mask,
+                                          next_batch_vec, num_graphs=B)
+            q_next = torch.min(self.target1(next_node_x, edge_index, next_edge_attr, next_batch_vec, B),
+                               self.target2(next_node_x, edge_index, next_edge_attr, next_batch_vec, B))
+            v_next = scatter_sum(next_probs * (q_next - self.alpha * torch.log(next_probs + 1e-8)), edge_batch, B,
+                                 reg)
+            target = reward + (1.0 - done) * self.gamma * v_next
         with self._amp():
-            with torch.no_grad():
-                _, next_probs, _ = self.actor(next_node_x, edge_index, next_edge_attr, next_action_mask,
-                                              next_batch_vec, num_graphs=B)
-                q_next = torch.min(self.target1(next_node_x, edge_index, next_edge_attr, next_batch_vec, B),
-                                   self.target2(next_node_x, edge_index, next_edge_attr, next_batch_vec, B))
-                v_next = scatter_sum(next_probs * (q_next - self.alpha * torch.log(next_probs + 1e-8)), edge_batch, B,
-                                     reg)
-                target = reward + (1.0 - done) * self.gamma * v_next
             q1_all = self.critic1(node_x, edge_index, edge_attr, batch_vec, B)
             q2_all = self.critic2(node_x, edge_index, edge_attr, batch_vec, B)
             q1 = q1_all[action]

@@ -150,15 +150,24 @@ def _fp32_matmul():
 
 
 # ------------------------------------------------------------------ tests
-def test_fused_bf16_acting_vs_fp32_restatement():
+@pytest.mark.parametrize("head_scale", [1.0, 40.0])
+def test_fused_bf16_acting_vs_fp32_restatement(head_scale):
     """The bench's acting pass (fused bf16 kernels) at B = 4096 vs fp32.
-    bf16 has 8 mantissa bits; through 3 GAT layers + the edge MLP the logits
-    stay within 3 % of their per-graph range (measured ~0.5 %), the
-    probabilities within 2e-2 (measured ~2e-3), and the greedy action agrees
-    wherever the fp32 top-2 probability gap exceeds 5e-2."""
+    bf16 keeps 8 mantissa bits; through 3 GAT layers and the edge MLP the
+    logit error stays below 3e-2 x the logits' RMS (measured 1.4e-2 at random
+    init: 4.2e-3 absolute at RMS 0.29), probabilities within 2e-3 (measured
+    1.6e-4).  Softmax and the argmax see only differences between a graph's
+    logits: the error of the per-graph-centred logits, eps, bounds them, and
+    the greedy action must agree wherever the fp32 top-2 gap exceeds 2 eps.
+    Random-init logits of a graph span only ~1e-2, so the agreement is also
+    checked with the last layer's weight scaled by 40 (a trained-like spread;
+    bf16 then rounds logits of magnitude ~12 to 6e-2, and ~1.5 % of the graphs
+    have a top-2 gap above 2 eps)."""
     B = 4096
     env, obs, _ = observations(B)
     agent = make_agent()
+    with torch.no_grad():
+        agent.actor.edge_mlp[2].weight.mul_(head_scale)
     nx_, ei, ex_, mask, bv = flat(env, obs, B)
     with torch.no_grad():
         ref_logits, ref_probs = ref_actor(agent.actor, nx_, ei, ex_, mask, bv, B)
@@ -166,19 +175,28 @@ def test_fused_bf16_acting_vs_fp32_restatement():
             out = agent.actor._fused(nx_, ei, ex_, bv, B, mask=mask)
     assert out is not None, "fused acting path not taken"
     logits, probs = out[0].float(), out[1].float()
-    valid = mask > 0
-    rl = ref_logits.view(B, -1)
-    v = valid.view(B, -1)
-    span = torch.where(v, rl, torch.full_like(rl, float("nan")))
-    rng = (torch.nan_to_num(span, nan=-1e30).amax(1) - torch.nan_to_num(span, nan=1e30).amin(1)).clamp(min=1e-3)
-    err = ((logits.view(B, -1) - rl).abs() * v).amax(1) / rng
-    assert float(err.max()) < 3e-2, float(err.max())
-    assert float((probs - ref_probs).abs().max()) < 2e-2
-    assert torch.equal(probs.view(B, -1) * ~v, torch.zeros_like(probs.view(B, -1)))  # masked links: 0
-    top2 = ref_probs.view(B, -1).topk(2, dim=1).values
-    clear = (top2[:, 0] - top2[:, 1]) > 5e-2
+    v = mask > 0
+    rms = float(ref_logits[v].pow(2).mean().sqrt())
+    assert float((logits - ref_logits)[v].abs().max()) < 3e-2 * rms
+    assert torch.equal(logits[~v], ref_logits[~v])                 # masked: -1e9
+    assert torch.equal(probs[~v], torch.zeros_like(probs[~v]))
+    assert float((probs - ref_probs).abs().max()) < (2e-3 if head_scale == 1.0 else 5e-2)
+    vv = v.view(B, -1).float()
+    cnt = vv.sum(1, keepdim=True).clamp(min=1)
+
+    def centred(x):
+        x = x.view(B, -1) * vv
+        return (x - x.sum(1, keepdim=True) / cnt) * vv
+
+    eps = float((centred(logits) - centred(ref_logits)).abs().max())
+    assert eps < 3e-2 * rms
+    rl = ref_logits.view(B, -1).masked_fill(~v.view(B, -1), float("-inf"))
+    top2 = rl.topk(2, dim=1).values
+    clear = (top2[:, 0] - top2[:, 1]) > 2 * eps
     agree = probs.view(B, -1).argmax(1) == ref_probs.view(B, -1).argmax(1)
     assert bool(agree[clear].all()), int((~agree[clear]).sum())
+    if head_scale > 1:   # the comparison is not vacuous (measured 60 clear graphs of 4096)
+        assert int(clear.sum()) >= 30, int(clear.sum())
 
 
 def test_fp32_general_path_vs_restatement():
@@ -200,7 +218,7 @@ def test_fp32_general_path_vs_restatement():
 
 
 def test_fused_bf16_critic_vs_fp32_restatement():
-    """Target/critic fused pass (no mask): Q within 3 % of the per-graph range."""
+    """Target/critic fused pass (no mask): Q within 3e-2 x the RMS of Q."""
     B = 1024
     env, obs, _ = observations(B)
     agent = make_agent()
@@ -209,8 +227,8 @@ def test_fused_bf16_critic_vs_fp32_restatement():
         ref_q = ref_edge_head(agent.target1, nx_, ei, ex_, bv, B)[0].view(B, -1)
         with agent._amp():
             q = agent.target1(nx_, ei, ex_, bv, B).float().view(B, -1)
-    rng = (ref_q.amax(1) - ref_q.amin(1)).clamp(min=1e-3)
-    assert float(((q - ref_q).abs().amax(1) / rng).max()) < 3e-2
+    rms = float(ref_q.pow(2).mean().sqrt())
+    assert float((q - ref_q).abs().max()) < 3e-2 * rms   # measured 2e-2 x RMS (4.0e-3 at RMS 0.21)
 
 
 def _update_batch(B):
@@ -246,12 +264,19 @@ def test_update_gradients_vs_autograd_restatement(amp, tol):
     cl.backward()
     al.backward()
     aal.backward()
-    for name, g in got.items():
-        m, n = name.split(".", 1)
-        ref = dict(mods[m].named_parameters())[n].grad
-        assert ref is not None, name
-        rel = float((g.float() - ref).norm() / ref.norm().clamp(min=1e-12))
-        assert rel < tol, (name, rel)
+    # a tensor's error is measured against its own gradient norm, floored at
+    # 1e-2 x the module's RMS tensor norm: gradients that vanish analytically
+    # (the actor's last bias: softmax is shift-invariant) are pure rounding noise
+    worst = (0.0, "")
+    for m, mod in mods.items():
+        refs = {n: p.grad for n, p in mod.named_parameters() if p.grad is not None}
+        floor = 1e-2 * float(torch.stack([r.norm() for r in refs.values()]).pow(2).mean().sqrt())
+        for n, ref in refs.items():
+            g = got[f"{m}.{n}"]
+            rel = float((g.float() - ref).norm()) / (float(ref.norm()) + floor)
+            worst = max(worst, (rel, f"{m}.{n}"))
+    print(f"worst relative gradient error: {worst}")
+    assert worst[0] < tol, worst
     assert abs(float(got_alpha) - float(agent.log_alpha.grad)) <= tol * max(1e-6, abs(float(agent.log_alpha.grad)))
     for k, r in (("critic_loss", cl), ("actor_loss", al), ("alpha_loss", aal)):
         assert abs(float(out[k]) - float(r)) <= tol * max(1e-3, abs(float(r))), (k, float(out[k]), float(r))
