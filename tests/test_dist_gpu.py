@@ -1,0 +1,73 @@
+"""Multi-rank trainer on one GPU (config #4's data-parallel path, rehearsed).
+
+Two ranks share the card over gloo (the RCCL path's collectives through
+torch.distributed; TRX_DIST_BACKEND=gloo in bench.py), each with its own env
+shard (random damage: the host-side reset path), replay shard and PER draws.
+After several HIP-graph updates -- 3 eager warm-ups, then the update captured
+as two graphs around the eager gradient all-reduce (train.GraphedUpdate) --
+both ranks must hold bit-identical parameters (one bucketed all-reduce per
+update, src/rl/sac.py:157-263 semantics), while the same run without the
+all-reduce diverges.  Ranks are separate processes started with subprocess
+(no exec from a GPU-initialised process).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(tmp, sync, method="fw", iters=12, world=2):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_trainer_worker.py"), str(tmp),
+                                       str(iters), str(int(sync)), method], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(o.decode(errors="replace"))
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    return [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def test_two_ranks_stay_identical_with_graphed_updates(tmp_path):
+    res = _run(tmp_path, sync=True, iters=26)
+    assert all(r["graphed"] and r["split"] for r in res), [(r["graphed"], r["split"]) for r in res]
+    p0, p1 = res[0]["params"], res[1]["params"]
+    assert set(p0) == set(p1)
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
+    assert res[0]["episodes"] == res[1]["episodes"]   # episode bookkeeping is collective
+    # and the updates did move the weights (vs a fresh agent with the same seed)
+    from trafficrl.rl.sac import DiscreteSAC
+    torch.manual_seed(42)
+    fresh = DiscreteSAC(4, 6, 32, 32, num_layers=3, share_critic_encoder=False)
+    moved = sum(not torch.equal(fresh.actor.state_dict()[k], p0["actor." + k]) for k in fresh.actor.state_dict())
+    assert moved > 0
+
+
+def test_two_ranks_diverge_without_allreduce(tmp_path):
+    res = _run(tmp_path, sync=False, iters=8)
+    p0, p1 = res[0]["params"], res[1]["params"]
+    assert any(not torch.equal(p0[k], p1[k]) for k in p0)

@@ -256,3 +256,35 @@ def test_big_batch_properties(gd, tgraph):
     env.assign()
     np.testing.assert_array_equal(env.flow.cpu().numpy()[rows], f_o)
     np.testing.assert_array_equal(env.tstt.cpu().numpy()[rows], ts_o)
+
+
+def test_big_batch_fw30_vs_oracle(gd, tgraph):
+    """Config #3's env path at its size: B = 4096 FW-30 envs (random damage,
+    tie-heavy resets), reset + 3 random repairs; sampled rows == the oracle."""
+    og = O.OracleGraph.from_npz(golden("sf_graph.npz"))
+    gr = np.load(golden("sf_graph.npz"))
+    rng = np.random.default_rng(23)
+    B = 4096
+    dmg = np.zeros((B, 76), np.float32)
+    for b in range(B):
+        dmg[b, rng.choice(76, 22, replace=False)] = 1.0
+    env = make_vec(gd, tgraph, B, "fw", 30)
+    env.reset(damaged=torch.from_numpy(dmg), observe=False)
+    rows = rng.choice(B, 48, replace=False)
+    cap = np.where(dmg > 0, np.float32(1e-3), gr["cap0"]).astype(np.float32)
+    f_o, _, ts_o, _ = og.assign(cap[rows], dmg[rows], np.zeros((48, 76), np.float32), method="fw", iters=30,
+                                nthreads=8)
+    np.testing.assert_array_equal(env.flow.cpu().numpy()[rows], f_o)
+    np.testing.assert_array_equal(env.tstt.cpu().numpy()[rows], ts_o)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    for _ in range(3):
+        cap_b, dm_b, fl_b = env.capacity.cpu().numpy(), env.damaged.cpu().numpy(), env.flow.cpu().numpy()
+        a = (torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32)
+        env.step(a, observe=False)
+        an = a.cpu().numpy()[rows]
+        C, D = cap_b[rows].copy(), dm_b[rows].copy()
+        C[np.arange(48), an] = gr["cap0"][an]
+        D[np.arange(48), an] = 0.0
+        f_o, _, ts_o, _ = og.assign(C, D, fl_b[rows], method="fw", iters=30, nthreads=8)
+        np.testing.assert_array_equal(env.flow.cpu().numpy()[rows], f_o)
+        np.testing.assert_array_equal(env.tstt.cpu().numpy()[rows], ts_o)

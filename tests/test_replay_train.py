@@ -256,3 +256,24 @@ def test_graphed_column_reduction_replays():
         x.normal_()
         g.replay()
         torch.testing.assert_close(y, x.double().sum(0).float(), rtol=1e-4, atol=1e-3)
+
+
+def test_fw30_per_training_run(tmp_path):
+    """Config #3 in small: FW-30 envs, SAC+GAT with PER (prioritised sampling,
+    priority write-back) and HIP-graph updates; losses finite, priorities
+    moved off the insertion maximum, a checkpoint written."""
+    from trafficrl.train import Trainer, sf_config
+    cfg = sf_config()
+    cfg.update(num_envs=256, batch_start=256, batch_size=64, hidden_dim=32, embed_dim=32, eval_every=0,
+               output_dir=str(tmp_path), update_every=1, update_unit="iterations", assignment_method="fw",
+               assignment_iters=30, sp_backend="scipy", episodes=10 ** 6)
+    tr = Trainer(cfg, device="cuda", log=False)
+    tr.run(max_iters=12)
+    assert tr._graphed is None or tr._graphed.g_grads is not None
+    for k in ("critic_loss", "actor_loss", "alpha_loss"):
+        assert np.isfinite(float(tr.last_losses[k])), k
+    n = tr.replay.size
+    leaves = tr.replay.tree[tr.replay.capacity:tr.replay.capacity + n]
+    assert float(leaves.min()) < float(leaves.max())          # TD-error priorities written back
+    assert abs(float(tr.replay.tree[1]) - float(leaves.sum())) <= 1e-9 * float(leaves.sum())
+    assert os.path.exists(os.path.join(str(tmp_path), "model_last.pt"))
