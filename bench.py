@@ -213,6 +213,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workload", default=None, choices=["train", "env"], help="default train (sf) / env (anaheim)")
+    ap.add_argument("--damage", default="fixed", choices=["fixed", "random"],
+                    help="env workload: fixed = fixed_damage_seed=42 for every env; random = per-env "
+                         "default_rng(1000 + global env id) draws at every reset (host-side, repair_env.py:167-192; "
+                         "the resets are inside the timed region)")
     args = ap.parse_args()
     big = args.network != "sf"
     if args.envs is None:
@@ -300,15 +304,17 @@ def main():
         env = VecRepairEnv(gd, B, device=dev, assignment_method=args.method, assignment_iters=args.iters,
                            reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0, reward_gamma=0.0,
                            reward_clip=2.0, capacity_damage=1e-3, unassigned_penalty=1e4, reset=False,
-                           sp_backend=args.sp)
+                           sp_backend=args.sp, seeds=[1000 + rank * B + i for i in range(B)])
         E, N = env.num_edges, env.num_nodes
         dmg0 = torch.from_numpy(fixed_damage_mask(gd)).to(dev)
-        dmg_all = dmg0[None].expand(B, E).contiguous()
-        ep_len = int(dmg0.sum().item())
+        dmg_all = None if args.damage == "random" else dmg0[None].expand(B, E).contiguous()
+        ep_len = int(dmg0.sum().item())     # max(1, int(E * 0.3)) damaged links either way
         st = {"t": 0}
 
         def reset():
-            timed(lambda: env.reset(damaged=dmg_all, observe=False), ev_pairs)
+            # random: the host draws (one native call for all envs) stay outside the kernel events
+            dm = env.draw_damage() if dmg_all is None else dmg_all
+            timed(lambda: env.reset(damaged=dm, observe=False), ev_pairs)
             if observe:
                 env.observe()
             st["t"] = 0
@@ -386,7 +392,8 @@ def main():
             "dtype": "f32 (link flows/costs) + f64 (path labels)" + (
                 "; bf16 autocast GAT-SAC" if args.workload == "train" else ""),
             "data": (f"synthetic: {'Sioux Falls TNTP' if not big else 'seeded AnaheimSynth TNTP'}, "
-                     "fixed_damage_seed=42, " + ("random-init GAT-SAC (hidden 256, 4 heads, embed 256)"
+                     + ("fixed_damage_seed=42, " if args.damage == "fixed" or args.workload == "train" else
+                        "random damage per env (default_rng(1000 + env id), redrawn at every reset), ") + ("random-init GAT-SAC (hidden 256, 4 heads, embed 256)"
                                                  if args.workload == "train" else "uniform random valid repair actions")),
             "config": {
                 "workload": (f"{'SF' if not big else 'AnaheimSynth'} {B} vectorised envs/GPU, {args.method.upper()}-{args.iters} assignment"
@@ -395,6 +402,7 @@ def main():
                                 f"ratio 1/{4 * B} per transition)" if args.workload == "train" else ", uniform random valid actions")),
                 "sp_backend": args.sp,
                 "workload_kind": args.workload,
+                "damage": "fixed" if args.workload == "train" else args.damage,
                 "envs_per_gpu": B, "global_envs": B * world, "network": NETWORKS[args.network][2],
                 "method": args.method, "assignment_iters": args.iters, "episode_len": ep_len,
                 "parallelism": f"env-sharded x{world}",

@@ -337,6 +337,47 @@ int trx_per_update_range(double* tree, int64_t capacity, int64_t lo, const doubl
 int trx_per_add_range(double* tree, int64_t capacity, int64_t lo, int32_t n, double* max_priority, double eps,
                       double alpha, void* stream);
 
+/* The reference's float32 sum tree, bit for bit (src/train.py:27-91 under
+ * numpy >= 2 scalar rules): _set_priority adds the float32 delta fl32(p) - leaf
+ * to the leaf and to each ancestor in sequence (train.py:43-48); *max_priority
+ * is the reference's float64 max_priority.
+ * trx_per32_add_range: n sequential ReplayBuffer.add() calls at ring slots
+ *   lo .. lo+n-1 (lo + n <= capacity; replaces train.py:50-59): priority_k =
+ *   max_p + eps (float64, accumulated one add at a time), p_k = priority_k **
+ *   alpha.
+ * trx_per32_update: ReplayBuffer.update_priorities(idx, td_error) (train.py:
+ *   86-91), entries applied in order (a repeated idx sees the value left by
+ *   its earlier occurrences); td_error is float64 (the reference's .tolist()
+ *   of the float32 TD errors).  O(n^2) in LDS per 2048-entry chunk.
+ * trx_per32_sample: the descent of ReplayBuffer.sample (train.py:67-79) for
+ *   u[k] in [0,1): r = fl32(u[k] * tree[1]), then float32 `r <= tree[left] ?
+ *   left : (r -= tree[left], right)`; out_priority[k] = tree[leaf].        */
+int trx_per32_add_range(float* tree, int64_t capacity, int64_t lo, int32_t n, double* max_priority, double eps,
+                        double alpha, void* stream);
+int trx_per32_update(float* tree, int64_t capacity, const int64_t* idx, const double* td_error, int32_t n,
+                     double* max_priority, double eps, double alpha, void* stream);
+int trx_per32_sample(const float* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
+                     float* out_priority, void* stream);
+
+/* ------------------------------------------------------- damage draws (host)
+ * RepairEnv.reset's damage draw (src/env/repair_env.py:167-192) for num_envs
+ * envs, each with its own numpy Generator (PCG64) passed by state and updated
+ * in place -- the masks and the generator states afterwards are numpy's own:
+ * up to max_tries draws of rng.choice(num_edges, count, replace=False) until
+ * the active links' DiGraph (one arc per (u, v), the last link added for it,
+ * repair_env.py:107-109) is strongly connected, else one more draw unchecked.
+ * out_mask: float32 [num_envs, num_edges], 1 = damaged.  Host memory only; no
+ * device needed.  nthreads <= 0: min(16, hardware threads).
+ * The state fields are numpy's bit_generator.state: state/inc split in 64-bit
+ * halves, has_uint32/uinteger its buffered half-draw.  num_edges <= 10000
+ * (numpy's Floyd branch of choice). */
+typedef struct trx_pcg64 {
+    uint64_t state_hi, state_lo, inc_hi, inc_lo;
+    uint32_t has_uint32, uinteger;
+} trx_pcg64;
+int trx_damage_sample(int32_t num_nodes, int32_t num_edges, const int32_t* src, const int32_t* dst, int32_t count,
+                      int32_t max_tries, int32_t num_envs, trx_pcg64* rngs, float* out_mask, int32_t nthreads);
+
 /* ------------------------------------------------ GAT layer tail (training)
  * The autograd path's post-aggregation tail of a GATEncoder layer
  * (src/models/gat_encoder.py:40-49): z = out + bias, h = LayerNorm(z; ln_w,

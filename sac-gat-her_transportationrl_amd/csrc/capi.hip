@@ -36,6 +36,18 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+int trx::set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+namespace {
+
 template <typename T>
 int upload(trx_graph* g, const std::vector<T>& host, const T** out) {
     void* d = nullptr;
@@ -553,6 +565,36 @@ int trx_per_sample(const double* tree, int64_t capacity, const double* u, int32_
         return fail(TRX_EINVAL, "per_sample args");
     hipError_t e = trx::launch_per_sample(tree, capacity, u, n, out_idx, out_priority, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "per_sample launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_per32_add_range(float* tree, int64_t capacity, int64_t lo, int32_t n, double* max_priority, double eps,
+                        double alpha, void* stream) {
+    if (!tree || !max_priority || capacity < 1 || n < 0 || lo < 0 || lo + n > capacity)
+        return fail(TRX_EINVAL, "per32_add_range: need 0 <= lo, lo + n <= capacity");
+    hipError_t e = trx::launch_per32_add_range(tree, capacity, lo, n, max_priority, eps, alpha,
+                                               static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "per32_add_range launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_per32_update(float* tree, int64_t capacity, const int64_t* idx, const double* td_error, int32_t n,
+                     double* max_priority, double eps, double alpha, void* stream) {
+    if (!tree || !max_priority || capacity < 1 || n < 0 || (n > 0 && (!idx || !td_error)))
+        return fail(TRX_EINVAL, "per32_update args");
+    hipError_t e = trx::launch_per32_update(tree, capacity, idx, td_error, n, max_priority, eps, alpha,
+                                            static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "per32_update launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_per32_sample(const float* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
+                     float* out_priority, void* stream) {
+    if (!tree || capacity < 1 || n < 0 || (n > 0 && (!u || !out_idx || !out_priority)))
+        return fail(TRX_EINVAL, "per32_sample args");
+    hipError_t e = trx::launch_per32_sample(tree, capacity, u, n, out_idx, out_priority,
+                                            static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "per32_sample launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
 

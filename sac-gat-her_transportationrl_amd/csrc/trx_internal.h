@@ -8,6 +8,10 @@
 
 namespace trx {
 
+// records the message trx_last_error() returns (capi.hip); returns code
+int set_error(int code, const char* fmt, ...);
+
+
 // Largest node count handled by the register-resident small-graph kernel
 // (dist labels live in VGPRs, one lane per (env, origin) SSSP).
 constexpr int kSmallMaxNodes = 32;
@@ -192,5 +196,11 @@ hipError_t launch_per_add_range(double* tree, int64_t capacity, int64_t lo, int 
                                 double alpha, hipStream_t stream);
 hipError_t launch_per_sample(const double* tree, int64_t capacity, const double* u, int n, int64_t* out_idx,
                              double* out_pri, hipStream_t stream);
+hipError_t launch_per32_add_range(float* tree, int64_t capacity, int64_t lo, int n, double* max_priority, double eps,
+                                  double alpha, hipStream_t stream);
+hipError_t launch_per32_update(float* tree, int64_t capacity, const int64_t* idx, const double* err, int n,
+                               double* max_priority, double eps, double alpha, hipStream_t stream);
+hipError_t launch_per32_sample(const float* tree, int64_t capacity, const double* u, int n, int64_t* out_idx,
+                               float* out_pri, hipStream_t stream);
 
 }  // namespace trx

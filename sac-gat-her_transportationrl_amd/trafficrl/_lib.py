@@ -28,7 +28,8 @@ EXPORTS = (
     "trx_layer_tail_backward", "trx_att_dots_forward", "trx_att_dots_workspace_floats", "trx_att_dots_backward",
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
-    "trx_per_update_range", "trx_per_add_range",
+    "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
+    "trx_damage_sample",
 )
 
 
@@ -195,6 +196,11 @@ def load():
     L.trx_per_update_range.argtypes = [_vp, ctypes.c_int64, ctypes.c_int64, _vp, _i32, _vp]
     L.trx_per_add_range.argtypes = [_vp, ctypes.c_int64, ctypes.c_int64, _i32, _vp, ctypes.c_double, ctypes.c_double,
                                     _vp]
+    L.trx_per32_add_range.argtypes = [_vp, ctypes.c_int64, ctypes.c_int64, _i32, _vp, ctypes.c_double,
+                                      ctypes.c_double, _vp]
+    L.trx_per32_update.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _i32, _vp, ctypes.c_double, ctypes.c_double, _vp]
+    L.trx_per32_sample.argtypes = [_vp, ctypes.c_int64, _vp, _i32, _vp, _vp, _vp]
+    L.trx_damage_sample.argtypes = [_i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]
     L.trx_graph_pool_backward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_layer_tail_forward.argtypes = [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]
     L.trx_att_dots_forward.argtypes = [_i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp]
@@ -216,7 +222,8 @@ def load():
                  "trx_att_dots_backward", "trx_small_ln_forward", "trx_small_ln_backward",
                  "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward",
                  "trx_bf16_round", "trx_multi_copy",
-                 "trx_per_update_range", "trx_per_add_range"):
+                 "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
+                 "trx_per32_sample", "trx_damage_sample"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

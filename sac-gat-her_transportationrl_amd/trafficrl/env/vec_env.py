@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from .. import _lib
-from ..graph import DamageSampler, TrafficGraph
+from ..graph import DamageSampler, TrafficGraph, damage_sample_batch, pcg_states
 
 
 def resolve_sp_rule(sp_backend: Optional[str], num_nodes: int, force_gpu_sp: bool = False) -> int:
@@ -145,6 +145,7 @@ class VecRepairEnv:
         self._seeds = list(seeds) if seeds is not None else [seed + i for i in range(B)]
         self._fixed = (fixed_damage, fixed_damage_seed)
         self._samplers = None
+        self._rng_states = None   # PCG64 records of default_rng(seed_b), the non-fixed reset path
         if reset:
             self.reset()
 
@@ -183,8 +184,7 @@ class VecRepairEnv:
         ids = list(range(B)) if env_ids is None else [int(i) for i in (env_ids.tolist() if torch.is_tensor(env_ids)
                                                                        else env_ids)]
         if damaged is None:
-            masks = np.stack([self.samplers[i].sample(ratio) for i in ids])
-            damaged = torch.from_numpy(masks)
+            damaged = self.draw_damage(ids, ratio)
         damaged = damaged.to(device=self.device, dtype=torch.float32)
         env_mask = None
         if env_ids is None:
@@ -198,6 +198,22 @@ class VecRepairEnv:
         _lib.check(L.trx_reset(self.graph.handle, ctypes.byref(self.params), B, ctypes.byref(self._state),
                                _lib.ptr(env_mask), _lib.ptr(self.workspace), self._stream()), "trx_reset")
         return self.observe() if observe else None
+
+    def draw_damage(self, ids=None, damaged_ratio: Optional[float] = None) -> torch.Tensor:
+        """The next damage masks (float32 [len(ids), E], host) of envs `ids`
+        (default all) from their own RNG streams, as RepairEnv.reset draws them."""
+        ratio = self.damaged_ratio if damaged_ratio is None else damaged_ratio
+        ids = list(range(self.num_envs)) if ids is None else ids
+        if self._fixed[0] or self._samplers is not None:
+            masks = np.stack([self.samplers[i].sample(ratio) for i in ids])
+        else:   # every env's own default_rng(seed) stream, one native call for the batch
+            if self._rng_states is None:
+                self._rng_states = pcg_states(self._seeds)
+            sel = np.asarray(ids, np.int64)
+            st = np.ascontiguousarray(self._rng_states[sel])
+            masks = damage_sample_batch(self.num_nodes, self.graph.src, self.graph.dst, st, ratio)
+            self._rng_states[sel] = st
+        return torch.from_numpy(masks)
 
     def reset_where(self, env_mask: torch.Tensor, damaged: torch.Tensor, observe: bool = False):
         """Reset the envs where env_mask (bool/uint8 [B]) is set, with damage

@@ -4,12 +4,13 @@ TrafficGraph wraps trx_graph (include/trafficrl.h): the immutable,
 device-resident network built from a GraphData exactly as RepairEnv.__init__
 lays it out (src/env/repair_env.py:85-96).
 
-DamageSampler reproduces RepairEnv.reset's damage draw
-(repair_env.py:168-192): numpy PCG64 ``rng.choice(E, floor(E*ratio),
+DamageSampler / damage_sample_batch reproduce RepairEnv.reset's damage draw
+(repair_env.py:167-192): numpy PCG64 ``rng.choice(E, floor(E*ratio),
 replace=False)`` with up to 50 rejections until the active-edge subgraph
-(networkx edge_subgraph: only nodes incident to an active link) is strongly
-connected.  The RNG stays on the host, so damage sets match the reference
-seed-for-seed.
+(networkx DiGraph edge_subgraph: only nodes incident to an active arc) is
+strongly connected -- natively (trx_damage_sample, csrc/damage_host.hip, a
+restatement of numpy's Generator), for a whole env batch per call, so damage
+sets AND generator states match the reference seed-for-seed.
 """
 from __future__ import annotations
 
@@ -88,36 +89,55 @@ class TrafficGraph:
             self._h = None
 
 
-def _strongly_connected_active(num_nodes, src, dst, active):
-    """nx.is_strongly_connected(G.edge_subgraph(active edges)) for a small graph."""
-    us, vs = src[active], dst[active]
-    if us.size == 0:
-        return False
-    nodes = np.unique(np.concatenate([us, vs]))
-    adj = [[] for _ in range(num_nodes)]
-    radj = [[] for _ in range(num_nodes)]
-    for u, v in zip(us.tolist(), vs.tolist()):
-        adj[u].append(v)
-        radj[v].append(u)
+PCG64_DTYPE = np.dtype([("state_hi", "<u8"), ("state_lo", "<u8"), ("inc_hi", "<u8"), ("inc_lo", "<u8"),
+                        ("has_uint32", "<u4"), ("uinteger", "<u4")])   # trx_pcg64 (include/trafficrl.h)
+_M64 = (1 << 64) - 1
 
-    def reach(start, g):
-        seen = {start}
-        stack = [start]
-        while stack:
-            x = stack.pop()
-            for y in g[x]:
-                if y not in seen:
-                    seen.add(y)
-                    stack.append(y)
-        return seen
 
-    s0 = int(nodes[0])
-    need = set(nodes.tolist())
-    return need <= reach(s0, adj) and need <= reach(s0, radj)
+def pcg_states(rngs) -> np.ndarray:
+    """trx_pcg64 records of numpy Generators (PCG64) -- or of default_rng(seed)
+    for int seeds -- in order."""
+    out = np.zeros(len(rngs), PCG64_DTYPE)
+    for i, r in enumerate(rngs):
+        st = (np.random.default_rng(int(r)) if isinstance(r, (int, np.integer)) else r).bit_generator.state
+        if st["bit_generator"] != "PCG64":
+            raise ValueError(f"damage draws need a PCG64 generator, got {st['bit_generator']}")
+        s, inc = int(st["state"]["state"]), int(st["state"]["inc"])
+        out[i] = (s >> 64, s & _M64, inc >> 64, inc & _M64, int(st["has_uint32"]), int(st["uinteger"]))
+    return out
+
+
+def set_generator_state(rng: np.random.Generator, rec) -> None:
+    """Write a trx_pcg64 record back into a numpy Generator."""
+    rng.bit_generator.state = {
+        "bit_generator": "PCG64",
+        "state": {"state": (int(rec["state_hi"]) << 64) | int(rec["state_lo"]),
+                  "inc": (int(rec["inc_hi"]) << 64) | int(rec["inc_lo"])},
+        "has_uint32": int(rec["has_uint32"]), "uinteger": int(rec["uinteger"])}
+
+
+def damage_sample_batch(num_nodes: int, src: np.ndarray, dst: np.ndarray, states: np.ndarray,
+                        damaged_ratio: float = 0.3, nthreads: int = 0) -> np.ndarray:
+    """RepairEnv.reset's damage draw for len(states) envs in one native call
+    (trx_damage_sample): float32 masks [n, E]; `states` (PCG64_DTYPE) advance
+    in place exactly as each env's numpy Generator would."""
+    E = len(src)
+    count = max(1, int(E * damaged_ratio))
+    if not (isinstance(states, np.ndarray) and states.dtype == PCG64_DTYPE and states.flags.c_contiguous):
+        raise TypeError("states must be a C-contiguous PCG64_DTYPE array (pcg_states)")
+    src = np.ascontiguousarray(src, np.int32)
+    dst = np.ascontiguousarray(dst, np.int32)
+    out = np.zeros((len(states), E), np.float32)
+    L = _lib.load()
+    _lib.check(L.trx_damage_sample(int(num_nodes), E, src.ctypes.data, dst.ctypes.data, count, 50, len(states),
+                                   states.ctypes.data, out.ctypes.data, int(nthreads)), "trx_damage_sample")
+    return out
 
 
 class DamageSampler:
-    """Per-env damage draws (repair_env.py:168-192, 77-83)."""
+    """Per-env damage draws (repair_env.py:168-192, 77-83) through the native
+    batch sampler; self.rng stays the env's numpy Generator, advanced exactly as
+    the reference's self.rng is."""
 
     def __init__(self, graph: TrafficGraph, seed: int = 0, fixed_damage: bool = False,
                  fixed_damage_seed: int | None = None):
@@ -128,24 +148,14 @@ class DamageSampler:
         self._fixed_indices = None
 
     def sample(self, damaged_ratio: float = 0.3) -> np.ndarray:
-        E = self.g.num_edges
-        count = max(1, int(E * damaged_ratio))
-        idx = self._fixed_indices if self.fixed_damage else None
-        if idx is None:
-            rng = self._fixed_rng if self.fixed_damage and self._fixed_rng is not None else self.rng
-            for _ in range(50):
-                cand = rng.choice(E, size=count, replace=False)
-                active = np.ones(E, dtype=bool)
-                active[cand] = False
-                if not active.any():
-                    continue
-                if _strongly_connected_active(self.g.num_nodes, self.g.src, self.g.dst, active):
-                    idx = cand
-                    break
-            if idx is None:
-                idx = rng.choice(E, size=count, replace=False)
-            if self.fixed_damage:
-                self._fixed_indices = idx
-        mask = np.zeros(E, dtype=np.float32)
-        mask[idx] = 1.0
+        if self.fixed_damage and self._fixed_indices is not None:
+            mask = np.zeros(self.g.num_edges, dtype=np.float32)
+            mask[self._fixed_indices] = 1.0
+            return mask
+        rng = self._fixed_rng if self.fixed_damage and self._fixed_rng is not None else self.rng
+        st = pcg_states([rng])
+        mask = damage_sample_batch(self.g.num_nodes, self.g.src, self.g.dst, st, damaged_ratio)[0]
+        set_generator_state(rng, st[0])
+        if self.fixed_damage:
+            self._fixed_indices = np.flatnonzero(mask)
         return mask

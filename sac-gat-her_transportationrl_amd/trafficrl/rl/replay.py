@@ -12,6 +12,10 @@ from the reference ReplayBuffer:
     weights = (size * probs)^-beta / max;
   * update_priorities(): abs(err)+eps, max_priority, **alpha; for duplicate
     indices the last one wins (sequential semantics).
+tree_dtype="float32" is the reference's own tree bit for bit (float32 nodes,
+float32 deltas added down each leaf's ancestor chain in update order, the
+float32 NEP 50 descent; trx_per32_*); "float64" recomputes ancestors as sums of
+their children (no drift; trx_per_*).
 HER (train.py:805-823) reproduces the reference's behaviour including two
 quirks, flagged here: apply_goal writes the goal into edge-feature column -1
 (edge_id_norm; get_state's goal column is 4, repair_env.py:799-808), and the
@@ -68,7 +72,11 @@ def _last_wins(idx: torch.Tensor, val: torch.Tensor) -> torch.Tensor:
 
 class DeviceReplay:
     def __init__(self, capacity: int, num_nodes: int, num_edges: int, node_dim: int = 4, edge_dim: int = 6,
-                 alpha: float = 0.6, beta: float = 0.4, eps: float = 1e-6, device="cuda"):
+                 alpha: float = 0.6, beta: float = 0.4, eps: float = 1e-6, device="cuda",
+                 tree_dtype: str = "float64"):
+        if tree_dtype not in ("float32", "float64"):
+            raise ValueError(f"tree_dtype must be 'float32' (reference) or 'float64', got {tree_dtype!r}")
+        self.tree_dtype = tree_dtype
         self.capacity = int(capacity)
         self.alpha, self.beta, self.eps = alpha, beta, eps
         dev = self.device = torch.device(device)
@@ -87,7 +95,7 @@ class DeviceReplay:
         self.prev_tstt = torch.zeros(C, dtype=torch.float64, device=dev)
         self.next_tstt = torch.zeros(C, dtype=torch.float64, device=dev)
         self.init_tstt = torch.zeros(C, dtype=torch.float64, device=dev)
-        self.tree = torch.zeros(2 * C, dtype=torch.float64, device=dev)
+        self.tree = torch.zeros(2 * C, dtype=getattr(torch, tree_dtype), device=dev)
         self.max_priority = torch.ones((), dtype=torch.float64, device=dev)
         self.ptr = 0
         self.size = 0
@@ -139,7 +147,15 @@ class DeviceReplay:
 
     def _priorities_for_new(self, idx, B: int):
         # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
-        if self.ptr + B <= self.capacity and self.device.type == "cuda":
+        if self.tree_dtype == "float32":
+            L, lo, left = _lib.load(), self.ptr, B
+            while left > 0:          # ring order: [ptr, capacity) then from 0 (each piece one launch)
+                n = min(left, self.capacity - lo)
+                _lib.check(L.trx_per32_add_range(_lib.ptr(self.tree), self.capacity, lo, n,
+                                                 _lib.ptr(self.max_priority), float(self.eps), float(self.alpha),
+                                                 _lib.stream_ptr(self.device)), "trx_per32_add_range")
+                lo, left = (lo + n) % self.capacity, left - n
+        elif self.ptr + B <= self.capacity and self.device.type == "cuda":
             L = _lib.load()     # one launch: leaves, ancestors and max_priority (updated in place)
             _lib.check(L.trx_per_add_range(_lib.ptr(self.tree), self.capacity, self.ptr, B, _lib.ptr(self.max_priority),
                                            float(self.eps), float(self.alpha), _lib.stream_ptr(self.device)),
@@ -176,19 +192,37 @@ class DeviceReplay:
         if u is None:
             u = torch.rand(batch_size, dtype=torch.float64, device=self.device, generator=generator)
         idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
-        pri = torch.empty(batch_size, dtype=torch.float64, device=self.device)
+        pri = torch.empty(batch_size, dtype=self.tree.dtype, device=self.device)
         L = _lib.load()
-        _lib.check(L.trx_per_sample(_lib.ptr(self.tree), self.capacity, _lib.ptr(u), batch_size, _lib.ptr(idx),
-                                    _lib.ptr(pri), _lib.stream_ptr(self.device)), "trx_per_sample")
-        probs = pri / self.total
-        w = (self.size_t * probs) ** (-self.beta)
-        w = w / torch.clamp(w.max(), min=1e-300)
+        if self.tree_dtype == "float32":
+            # train.py:80-82 in float32: probs = pri / total, (size * probs) ** -beta, / max
+            _lib.check(L.trx_per32_sample(_lib.ptr(self.tree), self.capacity, _lib.ptr(u.contiguous()), batch_size,
+                                          _lib.ptr(idx), _lib.ptr(pri), _lib.stream_ptr(self.device)),
+                       "trx_per32_sample")
+            probs = pri / self.total
+            w = (self.size_t.float() * probs) ** (-self.beta)
+            wmax = w.max()
+            w = w / torch.where(wmax > 0, wmax, torch.ones_like(wmax))
+        else:
+            _lib.check(L.trx_per_sample(_lib.ptr(self.tree), self.capacity, _lib.ptr(u), batch_size, _lib.ptr(idx),
+                                        _lib.ptr(pri), _lib.stream_ptr(self.device)), "trx_per_sample")
+            probs = pri / self.total
+            w = (self.size_t * probs) ** (-self.beta)
+            w = w / torch.clamp(w.max(), min=1e-300)
         return Sample(idx, w.float(), self.node_x[idx], self.edge_x[idx], self.mask[idx], self.action[idx],
                       self.reward[idx], self.next_node_x[idx], self.next_edge_x[idx], self.next_mask[idx],
                       self.done[idx], self.goal[idx], self.prev_tstt[idx], self.next_tstt[idx], self.init_tstt[idx],
                       pri)
 
     def update_priorities(self, idx: torch.Tensor, td_errors: torch.Tensor):
+        if self.tree_dtype == "float32":
+            err = td_errors.detach().to(torch.float64).contiguous()
+            idx = idx.contiguous()
+            L = _lib.load()
+            _lib.check(L.trx_per32_update(_lib.ptr(self.tree), self.capacity, _lib.ptr(idx), _lib.ptr(err), idx.numel(),
+                                          _lib.ptr(self.max_priority), float(self.eps), float(self.alpha),
+                                          _lib.stream_ptr(self.device)), "trx_per32_update")
+            return
         pr = td_errors.detach().to(torch.float64).abs() + self.eps
         self.max_priority.copy_(torch.maximum(self.max_priority, pr.max()))
         self._set(idx, pr ** self.alpha)

@@ -56,6 +56,7 @@ DEFAULTS: Dict = dict(
     capacity_damage=1e-3, unassigned_penalty=2e7, gp_step=1.0, gp_keep_paths=3, fixed_damage=False,
     fixed_damage_seed=None, episodes=2000, max_steps=0, buffer_size=1_000_000, batch_start=2000, batch_size=256,
     update_every=1, updates_per_step=1, update_unit="transitions", per_alpha=0.6, per_beta=0.4, per_eps=1e-6,
+    per_tree="float32",
     her_ratio=0.0, hidden_dim=256, embed_dim=256, gat_layers=3, lr=1e-4, actor_lr=None, critic_lr=None,
     alpha_lr=None, gamma=0.99, target_tau=0.001, grad_clip=None, share_critic_encoder=True, alpha_init=0.1,
     alpha_max=None, target_entropy_ratio=0.6, eval_every=50, eval_seeds=[1001, 1002, 1003, 1004, 1005],
@@ -267,7 +268,7 @@ class Trainer:
             self.agent.grad_sync = GradAllReduce(world)
         cap = min(int(cfg["buffer_size"]), max(int(cfg["buffer_size"]) // world, B))
         self.replay = DeviceReplay(cap, self.N, self.E, alpha=cfg["per_alpha"], beta=cfg["per_beta"],
-                                   eps=cfg["per_eps"], device=self.device)
+                                   eps=cfg["per_eps"], device=self.device, tree_dtype=cfg["per_tree"])
         ei = self.env.edge_index
         self.act_ei, self.act_batch = batched_topology(ei, self.N, B)
         bs = int(cfg["batch_size"])

@@ -101,6 +101,68 @@ def test_damage_sampler_matches_reference_seeds():
     np.testing.assert_array_equal(fixed, r["msa30_damaged"])
 
 
+def _reference_draw(rng, num_nodes, src, dst, ratio):
+    """repair_env.py:167-192 restated with networkx (test-only checker)."""
+    import networkx as nx
+    E = len(src)
+    G = nx.DiGraph()
+    for i, (u, v) in enumerate(zip(src.tolist(), dst.tolist())):
+        G.add_edge(u, v, edge_id=i)
+    count = max(1, int(E * ratio))
+    for _ in range(50):
+        cand = rng.choice(E, size=count, replace=False)
+        m = np.zeros(E, np.float32)
+        m[cand] = 1.0
+        active = [(u, v) for u, v, d in G.edges(data=True) if m[d["edge_id"]] == 0]
+        if not active:
+            continue
+        if nx.is_strongly_connected(G.edge_subgraph(active).copy()):
+            return m
+    m = np.zeros(E, np.float32)
+    m[rng.choice(E, size=count, replace=False)] = 1.0
+    return m
+
+
+@pytest.mark.parametrize("net", ["sf", "ana", "parallel"])
+def test_batch_damage_sampler_matches_numpy_generator(net):
+    """trx_damage_sample (numpy's PCG64 + choice restated natively) == the
+    reference's loop on numpy Generators: masks over 3 successive resets per
+    env, and the generator states afterwards (so later draws stay in step).
+    'parallel' adds a duplicate (u, v) link: the DiGraph keeps the last id."""
+    from trafficrl.graph import damage_sample_batch, pcg_states, set_generator_state
+    if net == "sf":
+        from trafficrl.data import sioux_falls
+        g = sioux_falls()
+        src = np.array([e.u - 1 for e in g.edges], np.int32)
+        dst = np.array([e.v - 1 for e in g.edges], np.int32)
+        N, envs, ratios = g.num_nodes, 64, (0.3, 0.1, 0.5)
+    elif net == "ana":
+        z = np.load(golden("ana_graph.npz"))
+        src, dst, N, envs, ratios = z["src"].astype(np.int32), z["dst"].astype(np.int32), int(z["num_nodes"]), 6, \
+            (0.3, 0.05, 0.3)
+    else:
+        rng = np.random.default_rng(3)
+        N = 8
+        ring = [(i, (i + 1) % N) for i in range(N)] + [((i + 1) % N, i) for i in range(N)]
+        extra = [tuple(map(int, rng.integers(0, N, 2))) for _ in range(10)]
+        pairs = ring + extra + ring[:4]     # ring[:4] again: parallel links
+        src = np.array([p[0] for p in pairs], np.int32)
+        dst = np.array([p[1] for p in pairs], np.int32)
+        envs, ratios = 40, (0.3, 0.2, 0.4)
+    seeds = [1000 + i for i in range(envs)]
+    gens = [np.random.default_rng(s) for s in seeds]
+    st = pcg_states(seeds)
+    for ratio in ratios:
+        got = damage_sample_batch(N, src, dst, st, ratio, nthreads=3)
+        want = np.stack([_reference_draw(r, N, src, dst, ratio) for r in gens])
+        np.testing.assert_array_equal(got, want)
+    for r, rec in zip(gens, st):
+        probe = np.random.default_rng(0)
+        set_generator_state(probe, rec)
+        assert probe.bit_generator.state == r.bit_generator.state
+        assert probe.random() == r.random()
+
+
 def test_fused_args_layout_matches_header(tmp_path):
     """Every field offset of trx_gat_layer_args / trx_edge_head_args as the C
     compiler lays them out equals the ctypes mirror in trafficrl/_lib.py."""

@@ -1,0 +1,129 @@
+"""The reference's float32 PER sum tree (src/train.py:27-91) pinned bit for bit.
+
+tests/golden/per_tree_ref.npz holds the reference ReplayBuffer's own outputs
+(tools/gen_golden_r2.py): capacity 1000 (not a power of two, leaves at two
+depths), 1500 adds (the ring wraps), three rounds of sample(256) with fixed
+uniforms + update_priorities with float32 TD errors, then 300 more adds.
+
+CPU: the restatement oracle/per_tree.py replays the protocol and must match
+every tree, index, weight and max_priority exactly.  GPU: DeviceReplay with
+tree_dtype="float32" (trx_per32_add_range / trx_per32_update /
+trx_per32_sample) must match the same fixture -- trees, sampled indices and
+max_priority bit-exact; IS weights within 4 float32 ulps (numpy's float32 pow
+on the host vs the device powf) -- and the restatement at the reference's
+buffer_size 1e6 with 4096-transition ring adds and repeated update indices.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from per_tree import RefTree
+
+ADD_BATCHES = (700, 500, 300)     # 1500 adds in ring pieces (the second and third wrap)
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return dict(np.load(golden("per_tree_ref.npz")))
+
+
+def test_restatement_matches_reference_fixture(fx):
+    rb = RefTree(int(fx["capacity"]), float(fx["alpha"]), float(fx["beta"]), float(fx["eps"]))
+    for _ in range(1500):
+        rb.add()
+    np.testing.assert_array_equal(rb.tree, fx["tree_after_add"])
+    for r in range(3):
+        idx, _, w = rb.sample(fx[f"s{r}_u"])
+        np.testing.assert_array_equal(idx, fx[f"s{r}_idx"])
+        np.testing.assert_array_equal(w, fx[f"s{r}_w"])
+        rb.update_priorities(idx, fx[f"s{r}_td"])
+        np.testing.assert_array_equal(rb.tree, fx[f"s{r}_tree"])
+        assert rb.max_p == float(fx[f"s{r}_max_p"])
+    for _ in range(300):
+        rb.add()
+    np.testing.assert_array_equal(rb.tree, fx["tree_final"])
+    assert (rb.ptr, rb.size, rb.max_p) == (int(fx["final_ptr"]), int(fx["final_size"]), float(fx["final_max_p"]))
+
+
+def test_fixture_exercises_the_float32_semantics(fx):
+    """The fixture is not also what a float64 tree would give: float32 delta
+    propagation leaves the root different from the exact leaf sum."""
+    t = fx["tree_final"]
+    cap = int(fx["capacity"])
+    assert float(t[1]) != float(np.sum(t[cap:].astype(np.float64)))
+
+
+def _device_replay(cap, fx_or_none=None, device="cuda"):
+    from trafficrl.rl.replay import DeviceReplay
+    kw = {} if fx_or_none is None else dict(alpha=float(fx_or_none["alpha"]), beta=float(fx_or_none["beta"]),
+                                            eps=float(fx_or_none["eps"]))
+    return DeviceReplay(cap, 1, 1, node_dim=1, edge_dim=1, device=device, tree_dtype="float32", **kw)
+
+
+def _adds(rb, B):
+    d = rb.device
+    z = lambda *s, **kw: torch.zeros(*s, device=d, **kw)
+    rb.add_batch(z(B, 1, 1), z(B, 1, 1), z(B, 1), torch.zeros(B, dtype=torch.int64, device=d), z(B), z(B, 1, 1),
+                 z(B, 1, 1), z(B, 1), z(B), z(B, 1), z(B, dtype=torch.float64), z(B, dtype=torch.float64),
+                 z(B, dtype=torch.float64))
+
+
+def _ulps32(a, b):
+    a, b = np.asarray(a, np.float32).view(np.int32), np.asarray(b, np.float32).view(np.int32)
+    return np.abs(a.astype(np.int64) - b.astype(np.int64))
+
+
+def test_tree_dtype_validated():
+    from trafficrl.rl.replay import DeviceReplay
+    with pytest.raises(ValueError):
+        DeviceReplay(8, 1, 1, device="cpu", tree_dtype="float16")
+
+
+@pytest.mark.gpu
+def test_device_tree_matches_reference_fixture(fx):
+    cap = int(fx["capacity"])
+    rb = _device_replay(cap, fx)
+    for B in ADD_BATCHES:
+        _adds(rb, B)
+    np.testing.assert_array_equal(rb.tree.cpu().numpy(), fx["tree_after_add"])
+    for r in range(3):
+        u = torch.tensor(fx[f"s{r}_u"], dtype=torch.float64, device="cuda")
+        s = rb.sample(256, u=u)
+        np.testing.assert_array_equal(s.idx.cpu().numpy(), fx[f"s{r}_idx"])
+        assert _ulps32(s.weights.cpu().numpy(), fx[f"s{r}_w"]).max() <= 4
+        td = torch.tensor(fx[f"s{r}_td"], dtype=torch.float32, device="cuda")   # the trainer's float32 TD errors
+        rb.update_priorities(s.idx, td)
+        np.testing.assert_array_equal(rb.tree.cpu().numpy(), fx[f"s{r}_tree"])
+        assert rb.max_priority.item() == float(fx[f"s{r}_max_p"])
+    _adds(rb, 300)
+    np.testing.assert_array_equal(rb.tree.cpu().numpy(), fx["tree_final"])
+    assert (rb.ptr, rb.size, rb.max_priority.item()) == (int(fx["final_ptr"]), int(fx["final_size"]),
+                                                         float(fx["final_max_p"]))
+
+
+@pytest.mark.gpu
+def test_device_tree_at_reference_buffer_size():
+    """buffer_size 1e6 (configs/*.yaml) with 4096-env ring adds, a 256-draw
+    sample and an update whose indices repeat (leaf chains), vs the restatement."""
+    cap = 1_000_000
+    ref = RefTree(cap)
+    rb = _device_replay(cap)
+    rng = np.random.default_rng(5)
+    for B in (4096, 4096, 1000):
+        _adds(rb, B)
+        for _ in range(B):
+            ref.add()
+    np.testing.assert_array_equal(rb.tree.cpu().numpy(), ref.tree)
+    for r in range(2):
+        u = rng.random(256)
+        s = rb.sample(256, u=torch.tensor(u, device="cuda"))
+        idx, _, w = ref.sample(u)
+        np.testing.assert_array_equal(s.idx.cpu().numpy(), idx)
+        assert _ulps32(s.weights.cpu().numpy(), w).max() <= 4
+        idx_u = np.concatenate([idx, idx[:40], idx[10:20]])          # repeats: later occurrences see earlier ones
+        td = (rng.standard_normal(len(idx_u)) * 3).astype(np.float32)
+        rb.update_priorities(torch.tensor(idx_u, device="cuda"), torch.tensor(td, device="cuda"))
+        ref.update_priorities(idx_u, td.astype(np.float64))
+        np.testing.assert_array_equal(rb.tree.cpu().numpy(), ref.tree)
+        assert rb.max_priority.item() == ref.max_p

@@ -227,7 +227,7 @@ def test_graphed_update_matches_eager(tmp_path, her, hidden, embed):
     assert trs[1]._graphed.g_grads is not None
     for (k, p_e), p_g in zip(trs[0].agent.actor.state_dict().items(), trs[1].agent.actor.state_dict().values()):
         torch.testing.assert_close(p_g, p_e, rtol=1e-3, atol=1e-4, msg=k)
-    torch.testing.assert_close(trs[1].replay.tree, trs[0].replay.tree, rtol=1e-6, atol=1e-9)
+    torch.testing.assert_close(trs[1].replay.tree, trs[0].replay.tree, rtol=1e-5, atol=1e-9)
     torch.testing.assert_close(trs[1].agent.log_alpha, trs[0].agent.log_alpha)
 
 
@@ -275,5 +275,7 @@ def test_fw30_per_training_run(tmp_path):
     n = tr.replay.size
     leaves = tr.replay.tree[tr.replay.capacity:tr.replay.capacity + n]
     assert float(leaves.min()) < float(leaves.max())          # TD-error priorities written back
-    assert abs(float(tr.replay.tree[1]) - float(leaves.sum())) <= 1e-9 * float(leaves.sum())
+    assert tr.replay.tree.dtype == torch.float32      # the reference's float32 tree (per_tree default)
+    # float32 deltas accumulated down the chain: the root drifts by a few ulps per update at most
+    assert abs(float(tr.replay.tree[1]) - float(leaves.double().sum())) <= 1e-4 * float(leaves.double().sum())
     assert os.path.exists(os.path.join(str(tmp_path), "model_last.pt"))

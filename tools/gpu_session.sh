@@ -23,6 +23,8 @@ for s in "$@"; do
         bench) step bench 600 python bench.py ;;
         benchq) step bench 400 python bench.py --steps 44 --warmup 22 --cpu-seconds 5 ;;
         benchenv) step bench_env 400 python bench.py --workload env --steps 66 --warmup 22 --no-cpu ;;
+        benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
+        pertests) step per_tests 300 python -u -m pytest tests/test_per_tree.py tests/test_replay_train.py -x -v --timeout 120 --timeout-method thread ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 44 --warmup 22 --no-cpu ;;
         profenv) step profenv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profenv -o run --output-format csv -- python3 bench.py --workload env --steps 44 --warmup 22 --no-cpu ;;
         pmc) step pmc1 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d gpurun_out/pmc1 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu
