@@ -183,16 +183,25 @@ def gemm_mfma(rows, graphs, hidden=256, heads=4, embed=256, reps=20):
 
 def measured_traffic(network):
     """HBM bytes per env-kernel launch from the committed rocprofv3 PMC summary
-    of this workload (profiles/r01_v3_pmc.json for Sioux Falls,
+    of this workload (profiles/r02_sf_pmc.json for Sioux Falls,
     profiles/r01_ana_pmc.json for the Anaheim-size network; separate
     FETCH_SIZE / WRITE_SIZE passes, see tools/pmc_summary.py)."""
-    name = {"sf": "r01_v3_pmc.json", "anaheim": "r01_ana_pmc.json"}[network]
+    name = {"sf": "r02_sf_pmc.json", "anaheim": "r01_ana_pmc.json"}[network]
     path = os.path.join(ROOT, "profiles", name)
     try:
         d = json.load(open(path))
-        return d.get("hbm_bytes_per_launch_raw"), os.path.relpath(path, ROOT)
+        return d.get("hbm_bytes_per_launch_raw"), os.path.relpath(path, ROOT), d.get("valu_busy_frac")
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
+
+
+def env_kernel_name(big, sp):
+    """The env kernel trx_step launches for this workload (capi.hip run())."""
+    if big:
+        return "trx::env_kernel_big"
+    if sp == "scipy" and os.environ.get("TRX_KERNEL", "") != "quad":
+        return "trx::env_kernel_p<24>"     # packed-key Dijkstra (assign_packed.hip)
+    return "trx::env_kernel_q<24>"
 
 
 def main():
@@ -370,9 +379,11 @@ def main():
     P = len(env.graph.od_o)
     bpa = bytes_per_assign(N, E, Z, P, args.iters)
     achieved = bpa * B / mean_kernel_s
-    traffic, traffic_src = measured_traffic(args.network)
-    if (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")):
-        traffic, traffic_src = None, None  # the committed PMC passes are for the default workloads
+    traffic, traffic_src, valu_frac = measured_traffic(args.network)
+    kname = env_kernel_name(big, args.sp)
+    if (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")) or \
+            (not big and kname != "trx::env_kernel_p<24>"):
+        traffic, traffic_src, valu_frac = None, None, None  # the committed PMC passes are for the default workloads
     mfma = gemm_mfma(B * N, B) if (args.workload == "train" and rank == 0) else None
     if rank == 0:
         cpu = None
@@ -412,7 +423,11 @@ def main():
                 "frac": achieved / HBM_PEAK, "traffic": traffic,
                 "traffic_note": (f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {traffic_src} "
                                  "(raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic else None,
-                "kernel": "trx::env_kernel_big" if big else "trx::env_kernel_q<24>", "kernel_mean_ms": mean_kernel_s * 1e3,
+                "kernel": kname, "kernel_mean_ms": mean_kernel_s * 1e3,
+                "valu_busy_frac": valu_frac,
+                "valu_note": ("SIMD VALU issue share of the same kernel from the committed PMC passes "
+                              "(4 x SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)); the kernel is issue-bound, "
+                              "not HBM-bound") if valu_frac else None,
                 "bytes_per_assign": bpa, "assigns_per_launch": B,
                 "mfma": mfma,
             },

@@ -139,7 +139,11 @@ hipError_t launch_per_sample(const double* tree, int64_t capacity, const double*
 // each node accumulates its subtree's deltas sequentially, in update order.
 // A parallel restatement has to keep that order per node: every touched node is
 // owned by one thread that walks the deltas of the leaves below it in update
-// order.  max_priority stays a float64 accumulated sequentially (train.py:52-54).
+// order.  Nodes of different tree levels are independent, so each level gets
+// its own workgroup (the long chains near the root run side by side on
+// different CUs); the deltas are computed from the leaves as they were before
+// the call, so the leaves themselves are written by a second launch.
+// max_priority stays a float64 accumulated sequentially (train.py:52-54).
 //
 // Leaves of a capacity that is not a power of two sit at two depths: leaf t in
 // [capacity, 2 capacity) has bit length d1 = bitlen(capacity) or d2 =
@@ -147,8 +151,35 @@ hipError_t launch_per_sample(const double* tree, int64_t capacity, const double*
 
 __device__ __forceinline__ int bitlen64(int64_t x) { return 64 - __clzll((unsigned long long)x); }
 
-constexpr int kPer32Chunk = 2048;   // ring-add leaves per pass (deltas staged in LDS)
-constexpr int kPer32MaxUpd = 2048;  // update_priorities entries per launch
+constexpr int kPer32Chunk = 8192;   // ring-add leaves per launch pair (deltas staged in LDS)
+constexpr int kPer32MaxUpd = 2048;  // update_priorities entries per launch pair
+
+// The float64 running max_priority of k sequential adds, mp_k = fl(mp_{k-1} +
+// eps) (train.py:52-54).  Inside one binade, away from a rounding tie, every
+// step adds the same s = fl(mp_0 + eps) - mp_0, so mp_k = mp_0 + k s exactly;
+// otherwise the sequence is replayed.
+struct MpSeq {
+    double mp0, step;
+    bool closed;
+};
+
+__device__ inline MpSeq mp_sequence(double mp0, double eps, int n) {
+    MpSeq q{mp0, (mp0 + eps) - mp0, false};
+    int e0, e1;
+    frexp(mp0, &e0);
+    frexp(mp0 + (double)n * q.step, &e1);
+    const double u = ldexp(1.0, e0 - 53);     // ulp of mp0
+    const double r = eps / u;                 // exact (power-of-two scaling)
+    q.closed = mp0 > 0.0 && e0 == e1 && (r - floor(r)) != 0.5;
+    return q;
+}
+
+__device__ inline double mp_at(const MpSeq& q, double eps, int k) {   // mp after k + 1 adds
+    if (q.closed) return q.mp0 + (double)(k + 1) * q.step;
+    double m = q.mp0;
+    for (int i = 0; i <= k; ++i) m = m + eps;
+    return m;
+}
 
 // Node m (internal, bit length b) += deltas of the leaves t in [T0, T1) below it,
 // in t order (depth d1 leaves precede depth d2 leaves in t, and t order is
@@ -161,100 +192,198 @@ __device__ __forceinline__ float per32_node_sum(float acc, int64_t m, int b, int
         int64_t lo = m << s, hi = ((m + 1) << s) - 1;
         if (lo < T0) lo = T0;
         if (hi > T1 - 1) hi = T1 - 1;
+        // order kept: ((acc + a) + b) + c ...; the long chains near the root are
+        // the critical path, so 16-float LDS groups are fetched one group ahead
         int64_t t = lo;
-        for (; t + 3 <= hi; t += 4) {   // order kept: ((acc + a) + b) + c ...
-            const float a0 = sdelta[t - T0], a1 = sdelta[t + 1 - T0], a2 = sdelta[t + 2 - T0], a3 = sdelta[t + 3 - T0];
-            acc = acc + a0;
-            acc = acc + a1;
-            acc = acc + a2;
-            acc = acc + a3;
+        for (; t <= hi && ((t - T0) & 3); ++t) acc = acc + sdelta[t - T0];
+        const float4* v = reinterpret_cast<const float4*>(sdelta + (t - T0));
+        const int64_t nq = (hi - t + 1) >> 2;   // whole float4s
+        int64_t i = 0;
+        if (nq >= 4) {
+            float4 c0 = v[0], c1 = v[1], c2 = v[2], c3 = v[3];
+            for (; i + 8 <= nq; i += 4) {
+                const float4 n0 = v[i + 4], n1 = v[i + 5], n2 = v[i + 6], n3 = v[i + 7];
+                acc = acc + c0.x; acc = acc + c0.y; acc = acc + c0.z; acc = acc + c0.w;
+                acc = acc + c1.x; acc = acc + c1.y; acc = acc + c1.z; acc = acc + c1.w;
+                acc = acc + c2.x; acc = acc + c2.y; acc = acc + c2.z; acc = acc + c2.w;
+                acc = acc + c3.x; acc = acc + c3.y; acc = acc + c3.z; acc = acc + c3.w;
+                c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+            }
+            acc = acc + c0.x; acc = acc + c0.y; acc = acc + c0.z; acc = acc + c0.w;
+            acc = acc + c1.x; acc = acc + c1.y; acc = acc + c1.z; acc = acc + c1.w;
+            acc = acc + c2.x; acc = acc + c2.y; acc = acc + c2.z; acc = acc + c2.w;
+            acc = acc + c3.x; acc = acc + c3.y; acc = acc + c3.z; acc = acc + c3.w;
+            i += 4;
         }
-        for (; t <= hi; ++t) acc = acc + sdelta[t - T0];
+        for (; i < nq; ++i) {
+            const float4 c = v[i];
+            acc = acc + c.x; acc = acc + c.y; acc = acc + c.z; acc = acc + c.w;
+        }
+        for (t += 4 * nq; t <= hi; ++t) acc = acc + sdelta[t - T0];
     }
     return acc;
 }
 
 // n sequential ReplayBuffer.add(item) calls at ring slots lo .. lo+n-1
-// (lo + n <= capacity): priority_k = max_p_{k-1} + eps, max_p_k = priority_k,
-// leaf += fl32(priority_k ** alpha) - leaf, ancestors += the same delta.
-__global__ void __launch_bounds__(1024) per32_add_range_kernel(float* __restrict__ tree, int64_t capacity, int64_t lo,
-                                                               int n, double* __restrict__ max_priority, double eps,
-                                                               double alpha) {
-    __shared__ double smp[kPer32Chunk];
-    __shared__ float sdelta[kPer32Chunk];
-    __shared__ double s_mp;
-    if (threadIdx.x == 0) s_mp = *max_priority;
-    const int d1 = bitlen64(capacity), d2 = bitlen64(2 * capacity - 1);
-    for (int c0 = 0; c0 < n; c0 += kPer32Chunk) {
-        const int cn = min(kPer32Chunk, n - c0);
-        __syncthreads();
-        if (threadIdx.x == 0) {   // the float64 running max_priority: sequential, as in the reference
-            double m = s_mp;
-            for (int k = 0; k < cn; ++k) {
-                m = m + eps;
-                smp[k] = m;
-            }
-            s_mp = m;
-        }
-        __syncthreads();
-        const int64_t T0 = capacity + lo + c0, T1 = T0 + cn;
-        for (int k = threadIdx.x; k < cn; k += blockDim.x) {
-            const float p32 = (float)pow(smp[k], alpha);
-            const float old = tree[T0 + k];
-            const float d = p32 - old;
-            sdelta[k] = d;
-            tree[T0 + k] = old + d;
-        }
-        __syncthreads();
-        // internal ancestors, bit length 1 .. d2-1; each node owned by one thread
-        for (int b = 1; b < d2; ++b) {
-            // ancestors of the depth-d1 leaves [T0, min(T1, 2^d1)) and of the depth-d2
-            // leaves [max(T0, 2^d1), T1) (d2 > d1 only)
-            const int64_t split = (int64_t)1 << d1;
-            int64_t a1 = 1, z1 = 0, a2 = 1, z2 = 0;   // empty ranges
-            if (d1 > b && T0 < split) {
-                a1 = T0 >> (d1 - b);
-                z1 = (min(T1, split) - 1) >> (d1 - b);
-            }
-            if (d2 > d1 && d2 > b && T1 > split) {
-                a2 = max(T0, split) >> (d2 - b);
-                z2 = (T1 - 1) >> (d2 - b);
-            }
-            const int64_t c1 = z1 >= a1 ? z1 - a1 + 1 : 0, c2 = z2 >= a2 ? z2 - a2 + 1 : 0;
-            for (int64_t j = threadIdx.x; j < c1 + c2; j += blockDim.x) {
-                const int64_t m = j < c1 ? a1 + j : a2 + (j - c1);
-                if (j >= c1 && m >= a1 && m <= z1) continue;   // owned through the first range
-                tree[m] = per32_node_sum(tree[m], m, b, T0, T1, d1, d2, sdelta);
-            }
-        }
-    }
+// (lo + n <= capacity, n <= kPer32Chunk): priority_k = max_p_{k-1} + eps,
+// max_p_k = priority_k, leaf += fl32(priority_k ** alpha) - leaf, ancestors +=
+// the same delta.  Launch 1: workgroup w owns the ancestors of bit length w + 1.
+__global__ void __launch_bounds__(1024) per32_add_levels_kernel(float* __restrict__ tree, int64_t capacity, int64_t lo,
+                                                               int n, const double* __restrict__ max_priority,
+                                                               double eps, double alpha) {
+    __shared__ __attribute__((aligned(16))) float sdelta[kPer32Chunk];
+    const MpSeq q = mp_sequence(*max_priority, eps, n);
+    const int64_t T0 = capacity + lo, T1 = T0 + n;
+    for (int k = threadIdx.x; k < n; k += blockDim.x)
+        sdelta[k] = (float)pow(mp_at(q, eps, k), alpha) - tree[T0 + k];
     __syncthreads();
-    if (threadIdx.x == 0) *max_priority = s_mp;
+    const int d1 = bitlen64(capacity), d2 = bitlen64(2 * capacity - 1);
+    const int b = blockIdx.x + 1;
+    // ancestors of the depth-d1 leaves [T0, min(T1, 2^d1)) and of the depth-d2
+    // leaves [max(T0, 2^d1), T1) (d2 > d1 only)
+    const int64_t split = (int64_t)1 << d1;
+    int64_t a1 = 1, z1 = 0, a2 = 1, z2 = 0;   // empty ranges
+    if (d1 > b && T0 < split) {
+        a1 = T0 >> (d1 - b);
+        z1 = (min(T1, split) - 1) >> (d1 - b);
+    }
+    if (d2 > d1 && d2 > b && T1 > split) {
+        a2 = max(T0, split) >> (d2 - b);
+        z2 = (T1 - 1) >> (d2 - b);
+    }
+    const int64_t c1 = z1 >= a1 ? z1 - a1 + 1 : 0, c2 = z2 >= a2 ? z2 - a2 + 1 : 0;
+    for (int64_t j = threadIdx.x; j < c1 + c2; j += blockDim.x) {
+        const int64_t m = j < c1 ? a1 + j : a2 + (j - c1);
+        if (j >= c1 && m >= a1 && m <= z1) continue;   // owned through the first range
+        tree[m] = per32_node_sum(tree[m], m, b, T0, T1, d1, d2, sdelta);
+    }
+}
+
+// Launch 2 (one workgroup): the leaves, then max_priority.
+__global__ void __launch_bounds__(1024) per32_add_leaves_kernel(float* __restrict__ tree, int64_t capacity,
+                                                                int64_t lo, int n, double* __restrict__ max_priority,
+                                                                double eps, double alpha) {
+    const MpSeq q = mp_sequence(*max_priority, eps, n);
+    const int64_t T0 = capacity + lo;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const float old = tree[T0 + k];
+        tree[T0 + k] = old + ((float)pow(mp_at(q, eps, k), alpha) - old);
+    }
+    __syncthreads();   // every thread has read *max_priority
+    if (threadIdx.x == 0) *max_priority = mp_at(q, eps, n - 1);
 }
 
 // ReplayBuffer.update_priorities(idx, err) (train.py:86-91) for n <= kPer32MaxUpd
 // entries in order: priority_k = |err_k| + eps, max_p = max(max_p, priority_k),
 // leaf += fl32(priority_k ** alpha) - leaf (a repeated leaf sees the value its
 // earlier occurrences left), ancestors += the same deltas in k order.
-__global__ void __launch_bounds__(1024) per32_update_kernel(float* __restrict__ tree, int64_t capacity,
-                                                            const int64_t* __restrict__ idx,
-                                                            const double* __restrict__ err, int n,
-                                                            double* __restrict__ max_priority, double eps,
-                                                            double alpha) {
-    __shared__ int64_t st[kPer32MaxUpd];
-    __shared__ float sp[kPer32MaxUpd], sd[kPer32MaxUpd], sval[kPer32MaxUpd];
-    __shared__ int sprev[kPer32MaxUpd], sround[kPer32MaxUpd];
-    __shared__ unsigned char slast[kPer32MaxUpd];
-    __shared__ double smax[32];
-    __shared__ int s_pending;
+struct UpdLds {
+    int64_t st[kPer32MaxUpd];
+    float sp[kPer32MaxUpd], sd[kPer32MaxUpd], sval[kPer32MaxUpd];
+    int sprev[kPer32MaxUpd], sround[kPer32MaxUpd];
+    unsigned char sbl[kPer32MaxUpd], slast[kPer32MaxUpd];
+    int pending;
+};
+
+// Leaf chains of the batch from the tree's leaves as they are on entry: sd[k]
+// (delta of entry k), sval[k] (leaf after entry k), slast[k] (k is the last
+// entry for its leaf).
+__device__ void per32_leaf_chains(UpdLds& L, const float* __restrict__ tree, int64_t capacity,
+                                  const int64_t* __restrict__ idx, const double* __restrict__ err, int n, double eps,
+                                  double alpha) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int64_t t = capacity + idx[k];
+        L.st[k] = t;
+        L.sbl[k] = (unsigned char)bitlen64(t);
+        L.sp[k] = (float)pow(fabs(err[k]) + eps, alpha);
+        L.sround[k] = -1;
+        L.slast[k] = 1;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {   // previous occurrence of the same leaf
+        const int64_t t = L.st[k];
+        int p = -1;
+#pragma unroll 8
+        for (int q = 0; q < k; ++q) p = L.st[q] == t ? q : p;
+        L.sprev[k] = p;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += blockDim.x)
+        if (L.sprev[k] >= 0) L.slast[L.sprev[k]] = 0;
+    // round r resolves the entries whose previous occurrence was resolved in an
+    // earlier round (rounds = longest run of one repeated leaf)
+    for (int r = 0;; ++r) {
+        if (threadIdx.x == 0) L.pending = 0;
+        __syncthreads();
+        for (int k = threadIdx.x; k < n; k += blockDim.x) {
+            if (L.sround[k] >= 0) continue;
+            const int p = L.sprev[k];
+            float before;
+            if (p < 0) {
+                before = tree[L.st[k]];
+            } else if (L.sround[p] >= 0 && L.sround[p] < r) {
+                before = L.sval[p];
+            } else {
+                L.pending = 1;
+                continue;
+            }
+            const float d = L.sp[k] - before;
+            L.sd[k] = d;
+            L.sval[k] = before + d;
+            L.sround[k] = r;
+        }
+        __syncthreads();
+        const int more = L.pending;
+        __syncthreads();
+        if (!more) break;
+    }
+}
+
+// Launch 1: workgroup w owns the touched ancestors of bit length w + 1; entry k
+// owns node anc(t_k) when no earlier entry has it, and adds every member's
+// delta in entry order.
+__global__ void __launch_bounds__(256) per32_update_levels_kernel(float* __restrict__ tree, int64_t capacity,
+                                                                  const int64_t* __restrict__ idx,
+                                                                  const double* __restrict__ err, int n, double eps,
+                                                                  double alpha) {
+    __shared__ UpdLds L;
+    per32_leaf_chains(L, tree, capacity, idx, err, n, eps, alpha);
+    const int b = blockIdx.x + 1;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int bt = L.sbl[k];
+        if (bt <= b) continue;
+        const int64_t m = L.st[k] >> (bt - b);
+        bool owner = true;
+#pragma unroll 8
+        for (int q = 0; q < k; ++q) {   // an earlier entry below m owns it
+            const int bq = L.sbl[q];
+            owner = owner && !(bq > b && (L.st[q] >> (bq - b)) == m);
+        }
+        if (!owner) continue;
+        float acc = tree[m];
+#pragma unroll 8
+        for (int q = k; q < n; ++q) {   // members in entry order (k itself first)
+            const int bq = L.sbl[q];
+            const bool member = bq > b && (L.st[q] >> (bq - b)) == m;
+            acc = member ? acc + L.sd[q] : acc;
+        }
+        tree[m] = acc;
+    }
+}
+
+// Launch 2 (one workgroup): the leaves and max_priority.
+__global__ void __launch_bounds__(1024) per32_update_leaves_kernel(float* __restrict__ tree, int64_t capacity,
+                                                                   const int64_t* __restrict__ idx,
+                                                                   const double* __restrict__ err, int n,
+                                                                   double* __restrict__ max_priority, double eps,
+                                                                   double alpha) {
+    __shared__ UpdLds L;
+    __shared__ double smax[16];
+    per32_leaf_chains(L, tree, capacity, idx, err, n, eps, alpha);
     double mymax = 0.0;
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const double pr = fabs(err[k]) + eps;
-        mymax = fmax(mymax, pr);
-        st[k] = capacity + idx[k];
-        sp[k] = (float)pow(pr, alpha);
-        sround[k] = -1;
-        slast[k] = 1;
+        mymax = fmax(mymax, fabs(err[k]) + eps);
+        if (L.slast[k]) tree[L.st[k]] = L.sval[k];
     }
     for (int o = 32; o > 0; o >>= 1) mymax = fmax(mymax, __shfl_xor(mymax, o));
     if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = mymax;
@@ -263,67 +392,6 @@ __global__ void __launch_bounds__(1024) per32_update_kernel(float* __restrict__ 
         double m = *max_priority;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = fmax(m, smax[w]);
         *max_priority = m;
-    }
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {   // previous occurrence of the same leaf
-        int p = -1;
-        for (int q = k - 1; q >= 0; --q)
-            if (st[q] == st[k]) {
-                p = q;
-                break;
-            }
-        sprev[k] = p;
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < n; k += blockDim.x)
-        if (sprev[k] >= 0) slast[sprev[k]] = 0;
-    // leaf chains: round r resolves the entries whose previous occurrence was
-    // resolved in an earlier round (depth = longest run of one repeated leaf)
-    for (int r = 0;; ++r) {
-        if (threadIdx.x == 0) s_pending = 0;
-        __syncthreads();
-        for (int k = threadIdx.x; k < n; k += blockDim.x) {
-            if (sround[k] >= 0) continue;
-            const int p = sprev[k];
-            float before;
-            if (p < 0) {
-                before = tree[st[k]];
-            } else if (sround[p] >= 0 && sround[p] < r) {
-                before = sval[p];
-            } else {
-                s_pending = 1;
-                continue;
-            }
-            const float d = sp[k] - before;
-            sd[k] = d;
-            sval[k] = before + d;
-            sround[k] = r;
-        }
-        __syncthreads();
-        if (!s_pending) break;
-        __syncthreads();
-    }
-    for (int k = threadIdx.x; k < n; k += blockDim.x)
-        if (slast[k]) tree[st[k]] = sval[k];
-    // ancestors: pair (b, k) owns node anc(t_k, b) when no earlier k' has it
-    const int d2 = bitlen64(2 * capacity - 1);
-    for (int64_t j = threadIdx.x; j < (int64_t)n * (d2 - 1); j += blockDim.x) {
-        const int b = 1 + (int)(j / n), k = (int)(j % n);
-        const int64_t t = st[k];
-        const int bt = bitlen64(t);
-        if (bt <= b) continue;
-        const int64_t m = t >> (bt - b);
-        bool owner = true;
-        for (int q = 0; q < k && owner; ++q) {
-            const int bq = bitlen64(st[q]);
-            owner = !(bq > b && (st[q] >> (bq - b)) == m);
-        }
-        if (!owner) continue;
-        float acc = tree[m];
-        for (int q = k; q < n; ++q) {
-            const int bq = bitlen64(st[q]);
-            if (bq > b && (st[q] >> (bq - b)) == m) acc = acc + sd[q];
-        }
-        tree[m] = acc;
     }
 }
 
@@ -350,20 +418,38 @@ __global__ void per32_sample_kernel(const float* __restrict__ tree, int64_t capa
     out_pri[k] = tree[node];
 }
 
+static int tree_levels(int64_t capacity) {   // internal bit lengths 1 .. d2-1
+    int d2 = 0;
+    while ((2 * capacity - 1) >> d2) ++d2;
+    return d2 - 1;
+}
+
 hipError_t launch_per32_add_range(float* tree, int64_t capacity, int64_t lo, int n, double* max_priority, double eps,
                                   double alpha, hipStream_t stream) {
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(per32_add_range_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, lo, n, max_priority,
-                       eps, alpha);
-    return hipGetLastError();
+    const int levels = tree_levels(capacity);
+    for (int c0 = 0; c0 < n; c0 += kPer32Chunk) {   // sequential chunks keep the add order
+        const int cn = n - c0 < kPer32Chunk ? n - c0 : kPer32Chunk;
+        if (levels > 0)
+            hipLaunchKernelGGL(per32_add_levels_kernel, dim3(levels), dim3(1024), 0, stream, tree, capacity, lo + c0,
+                               cn, max_priority, eps, alpha);
+        hipLaunchKernelGGL(per32_add_leaves_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, lo + c0, cn,
+                           max_priority, eps, alpha);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_per32_update(float* tree, int64_t capacity, const int64_t* idx, const double* err, int n,
                                double* max_priority, double eps, double alpha, hipStream_t stream) {
+    const int levels = tree_levels(capacity);
     for (int c0 = 0; c0 < n; c0 += kPer32MaxUpd) {   // sequential chunks keep the update order
         const int cn = n - c0 < kPer32MaxUpd ? n - c0 : kPer32MaxUpd;
-        hipLaunchKernelGGL(per32_update_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, idx + c0, err + c0,
-                           cn, max_priority, eps, alpha);
+        if (levels > 0)
+            hipLaunchKernelGGL(per32_update_levels_kernel, dim3(levels), dim3(256), 0, stream, tree, capacity,
+                               idx + c0, err + c0, cn, eps, alpha);
+        hipLaunchKernelGGL(per32_update_leaves_kernel, dim3(1), dim3(1024), 0, stream, tree, capacity, idx + c0,
+                           err + c0, cn, max_priority, eps, alpha);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

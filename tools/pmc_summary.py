@@ -17,14 +17,22 @@ from collections import defaultdict
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+src_glob = sys.argv[2] if len(sys.argv) > 2 else "pmc[0-9]"
 agg = defaultdict(list)
-for f in sorted(glob.glob(os.path.join(root, "gpurun_out", "pmc*", "run_counter_collection.csv"))):
+names = defaultdict(int)
+for f in sorted(glob.glob(os.path.join(root, "gpurun_out", src_glob, "run_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         if "env_kernel" in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            names[r["Kernel_Name"].split("(")[0].replace("void ", "")] += 1
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
-out = {"kernel": "trx::env_kernel_q<24>", "dispatches": {k: len(v) for k, v in agg.items()},
+out = {"kernel": max(names, key=names.get) if names else None, "dispatches": {k: len(v) for k, v in agg.items()},
        "per_dispatch_mean": mean}
+if "SQ_INSTS_VALU" in mean and "GRBM_GUI_ACTIVE" in mean:
+    # VALU issue: a wave64 VALU instruction holds its SIMD 4 cycles; GRBM_GUI_ACTIVE
+    # is summed over the 8 XCDs; 256 CUs x 4 SIMDs
+    cyc = mean["GRBM_GUI_ACTIVE"] / 8
+    out["valu_busy_frac"] = 4 * mean["SQ_INSTS_VALU"] / (cyc * 1024)
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     raw = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
     out["hbm_bytes_per_launch_raw"] = raw
