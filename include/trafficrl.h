@@ -462,6 +462,12 @@ typedef struct trx_copy_list {
     void* dst[TRX_MAX_COPY];
 } trx_copy_list;
 int trx_multi_copy(const trx_copy_list* l, void* stream);
+/* Row gather: for r < nrows, dst[k] bytes [r*bytes[k], (r+1)*bytes[k]) =
+ * src[k] bytes [idx[r]*bytes[k], ...) -- bytes[k] is the ROW size here; the
+ * caller guarantees idx[r] is a valid row of every src[k].  The replay
+ * sample's field gathers (src/train.py:83 `[self.data[i] for i in indices]`)
+ * in one launch.                                                          */
+int trx_multi_gather(const trx_copy_list* l, const int64_t* idx, int32_t nrows, void* stream);
 
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t

@@ -820,6 +820,17 @@ int trx_bf16_round(const trx_round_list* l, void* stream) {
     return TRX_OK;
 }
 
+int trx_multi_gather(const trx_copy_list* l, const int64_t* idx, int32_t nrows, void* stream) {
+    if (!l || l->count < 0 || l->count > TRX_MAX_COPY || nrows < 0 || (nrows > 0 && !idx))
+        return fail(TRX_EINVAL, "multi_gather: count must be 0..16, nrows >= 0, idx");
+    for (int k = 0; k < l->count; ++k) {
+        if (!l->src[k] || !l->dst[k] || l->bytes[k] < 0) return fail(TRX_EINVAL, "multi_gather: bad entry %d", k);
+    }
+    hipError_t e = trx::launch_multi_gather(*l, idx, nrows, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "multi_gather launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_multi_copy(const trx_copy_list* l, void* stream) {
     if (!l || l->count < 0 || l->count > TRX_MAX_COPY) return fail(TRX_EINVAL, "multi_copy: count must be 0..16");
     for (int k = 0; k < l->count; ++k)

@@ -116,7 +116,32 @@ __global__ void __launch_bounds__(256) multi_copy_kernel(trx_copy_list l) {
         for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += stride) dst[i] = src[i];
     }
 }
+
+// Row gather (trx_multi_gather): dst[k] row r = src[k] row idx[r], rows of
+// l.bytes[k] bytes -- the replay sample's ~13 index_selects in one launch.
+__global__ void __launch_bounds__(256) multi_gather_kernel(trx_copy_list l, const int64_t* __restrict__ idx) {
+    const int k = blockIdx.y;
+    if (k >= l.count) return;
+    const int64_t rb = l.bytes[k], r = blockIdx.x, sr = idx[r];
+    const char* src = static_cast<const char*>(l.src[k]) + sr * rb;
+    char* dst = static_cast<char*>(l.dst[k]) + r * rb;
+    if ((((uintptr_t)src | (uintptr_t)dst | (uintptr_t)rb) & 15) == 0) {
+        for (int64_t i = threadIdx.x; i < rb / 16; i += 256)
+            reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    } else if ((((uintptr_t)src | (uintptr_t)dst | (uintptr_t)rb) & 3) == 0) {
+        for (int64_t i = threadIdx.x; i < rb / 4; i += 256)
+            reinterpret_cast<uint32_t*>(dst)[i] = reinterpret_cast<const uint32_t*>(src)[i];
+    } else {
+        for (int64_t i = threadIdx.x; i < rb; i += 256) dst[i] = src[i];
+    }
+}
 }  // namespace
+
+hipError_t launch_multi_gather(const trx_copy_list& l, const int64_t* idx, int nrows, hipStream_t stream) {
+    if (nrows <= 0 || l.count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(multi_gather_kernel, dim3(nrows, l.count), dim3(256), 0, stream, l, idx);
+    return hipGetLastError();
+}
 
 hipError_t launch_multi_copy(const trx_copy_list& l, hipStream_t stream) {
     int64_t mx = 16;

@@ -166,6 +166,7 @@ int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
 int small_ln_blocks(int N);
 hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream);
+hipError_t launch_multi_gather(const trx_copy_list& l, const int64_t* idx, int nrows, hipStream_t stream);
 hipError_t launch_multi_copy(const trx_copy_list& l, hipStream_t stream);
 hipError_t launch_graph_pool_fwd(int B, int n, int F, const float* x, float* out, float* ties, hipStream_t stream);
 hipError_t launch_graph_pool_bwd(int B, int n, int F, const float* x, const float* out, const float* ties,

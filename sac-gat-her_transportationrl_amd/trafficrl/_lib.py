@@ -29,7 +29,7 @@ EXPORTS = (
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
-    "trx_damage_sample",
+    "trx_damage_sample", "trx_multi_gather",
 )
 
 
@@ -148,6 +148,22 @@ def multi_copy(pairs, device):
     check(L.trx_multi_copy(lst, stream_ptr(device)), "trx_multi_copy")
 
 
+def multi_gather(pairs, idx, device):
+    """One trx_multi_gather launch: dst[r] = src[idx[r]] along dim 0 for
+    [(dst, src), ...] (contiguous, same dtype and row shape; idx int64 on the
+    device, values < every src's row count -- not checked on the device)."""
+    L = load()
+    lst = TrxCopyList()
+    lst.count = len(pairs)
+    n = idx.numel()
+    for k, (dst, src) in enumerate(pairs):
+        assert dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype and dst.shape[0] == n
+        assert dst.shape[1:] == src.shape[1:]
+        lst.bytes[k] = (dst.numel() // max(1, n)) * dst.element_size()
+        lst.src[k], lst.dst[k] = src.data_ptr(), dst.data_ptr()
+    check(L.trx_multi_gather(lst, ptr(idx), n, stream_ptr(device)), "trx_multi_gather")
+
+
 class TrafficRLError(RuntimeError):
     pass
 
@@ -200,6 +216,7 @@ def load():
                                       ctypes.c_double, _vp]
     L.trx_per32_update.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _i32, _vp, ctypes.c_double, ctypes.c_double, _vp]
     L.trx_per32_sample.argtypes = [_vp, ctypes.c_int64, _vp, _i32, _vp, _vp, _vp]
+    L.trx_multi_gather.argtypes = [ctypes.POINTER(TrxCopyList), _vp, _i32, _vp]
     L.trx_damage_sample.argtypes = [_i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]
     L.trx_graph_pool_backward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_layer_tail_forward.argtypes = [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp]
@@ -223,7 +240,7 @@ def load():
                  "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward",
                  "trx_bf16_round", "trx_multi_copy",
                  "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
-                 "trx_per32_sample", "trx_damage_sample"):
+                 "trx_per32_sample", "trx_damage_sample", "trx_multi_gather"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

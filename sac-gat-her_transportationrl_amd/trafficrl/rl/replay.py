@@ -209,10 +209,14 @@ class DeviceReplay:
             probs = pri / self.total
             w = (self.size_t * probs) ** (-self.beta)
             w = w / torch.clamp(w.max(), min=1e-300)
-        return Sample(idx, w.float(), self.node_x[idx], self.edge_x[idx], self.mask[idx], self.action[idx],
-                      self.reward[idx], self.next_node_x[idx], self.next_edge_x[idx], self.next_mask[idx],
-                      self.done[idx], self.goal[idx], self.prev_tstt[idx], self.next_tstt[idx], self.init_tstt[idx],
-                      pri)
+        fields = (self.node_x, self.edge_x, self.mask, self.action, self.reward, self.next_node_x, self.next_edge_x,
+                  self.next_mask, self.done, self.goal, self.prev_tstt, self.next_tstt, self.init_tstt)
+        if self.device.type == "cuda":   # every field's rows in one trx_multi_gather launch
+            rows = [torch.empty((batch_size,) + f.shape[1:], dtype=f.dtype, device=self.device) for f in fields]
+            _lib.multi_gather(list(zip(rows, fields)), idx, self.device)
+        else:
+            rows = [f[idx] for f in fields]
+        return Sample(idx, w.float(), *rows, pri)
 
     def update_priorities(self, idx: torch.Tensor, td_errors: torch.Tensor):
         if self.tree_dtype == "float32":

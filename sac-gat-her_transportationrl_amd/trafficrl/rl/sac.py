@@ -229,26 +229,27 @@ class _EdgeHead(nn.Module):
         gathers then scatter back with incidence products (models/skinny.py)."""
         W1, b1 = self.edge_mlp[0].weight, self.edge_mlp[0].bias
         d, k = self.embed, self.edge_in
-        w_nodes = torch.cat([W1[:, :d], W1[:, d:2 * d]], 0)          # [2H, embed]
+        # torch.split: the backward is one cat, not a zero-fill + add per slice
+        w_src, w_dst, w_e, w_ctx = torch.split(W1, [d, d, k, W1.shape[1] - 2 * d - k], dim=1)
+        w_nodes = torch.cat([w_src, w_dst], 0)                        # [2H, embed]
         p = node_emb @ w_nodes.t()                                    # per-node projections
         hdim = W1.shape[0]
-        c = global_ctx @ W1[:, 2 * d + k:].t() + b1                   # [B, H] per-graph context
+        c = global_ctx @ w_ctx.t() + b1                               # [B, H] per-graph context
         W2, b2 = self.edge_mlp[2].weight, self.edge_mlp[2].bias
         if (FUSED_EDGE_TRAIN and regular is not None and p.is_cuda and fused.autocast_bf16() and hdim % 4 == 0
                 and hdim <= 256
                 and k <= 8 and node_emb.shape[0] % regular[0] == 0 and node_emb.shape[0] // regular[0] <= 64):
             # one kernel each way for the gathers, link term, context, ReLU and 256->1 product
             B = regular[0]
-            return fused.edge_scores_train(p, c, edge_attr, W1[:, 2 * d:2 * d + k], W2, b2, src, dst, B,
-                                           node_emb.shape[0] // B)
+            return fused.edge_scores_train(p, c, edge_attr, w_e, W2, b2, src, dst, B, node_emb.shape[0] // B)
         if regular is not None:
             B, src_l, dst_l = regular
             z = regular_gather(p[:, :hdim], src_l, B) + regular_gather(p[:, hdim:], dst_l, B)
-            z = z + skinny_linear(edge_attr, W1[:, 2 * d:2 * d + k])
+            z = z + skinny_linear(edge_attr, w_e)
             z = z + c.unsqueeze(1).expand(B, src_l.numel(), hdim).reshape(-1, hdim)
         else:
             z = p[src, :hdim] + p[dst, hdim:]
-            z = z + skinny_linear(edge_attr, W1[:, 2 * d:2 * d + k])
+            z = z + skinny_linear(edge_attr, w_e)
             z = z + c[edge_batch]
         return skinny_linear(torch.relu(z), W2, b2).squeeze(-1)
 

@@ -279,3 +279,24 @@ def test_fw30_per_training_run(tmp_path):
     # float32 deltas accumulated down the chain: the root drifts by a few ulps per update at most
     assert abs(float(tr.replay.tree[1]) - float(leaves.double().sum())) <= 1e-4 * float(leaves.double().sum())
     assert os.path.exists(os.path.join(str(tmp_path), "model_last.pt"))
+
+
+@pytest.mark.gpu
+def test_sample_rows_match_indexing():
+    """sample() gathers every field in one trx_multi_gather launch: rows equal
+    plain indexing, repeated indices included."""
+    from trafficrl.rl.replay import DeviceReplay
+    d = torch.device("cuda", 0)
+    rb = DeviceReplay(64, 24, 76, device=d, tree_dtype="float32")
+    g = torch.Generator(device=d).manual_seed(3)
+    B = 48
+    r = lambda *s, **kw: torch.rand(*s, device=d, generator=g, **kw)  # noqa: E731
+    rb.add_batch(r(B, 24, 4), r(B, 76, 6), r(B, 76), torch.randint(0, 76, (B,), device=d, generator=g), r(B),
+                 r(B, 24, 4), r(B, 76, 6), r(B, 76), r(B), r(B, 76), r(B, dtype=torch.float64),
+                 r(B, dtype=torch.float64), r(B, dtype=torch.float64))
+    u = torch.rand(200, dtype=torch.float64, device=d, generator=g)
+    s = rb.sample(200, u=u)
+    assert int(torch.unique(s.idx).numel()) < 200      # repeats present
+    for name in ("node_x", "edge_x", "mask", "action", "reward", "next_node_x", "next_edge_x", "next_mask", "done",
+                 "goal", "prev_tstt", "next_tstt", "init_tstt"):
+        assert torch.equal(getattr(s, name), getattr(rb, name)[s.idx]), name
