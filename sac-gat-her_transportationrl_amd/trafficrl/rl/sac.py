@@ -358,6 +358,10 @@ class DiscreteSAC:
         self.amp_dtype = amp_dtype
         # data-parallel hook: called once per update with every gradient tensor
         self.grad_sync: Optional[Callable[[list], None]] = None
+        # independent forwards (and their backwards) on side streams (_concurrent)
+        self.concurrent = True
+        self._side = None
+        self._warm = False
 
     @property
     def alpha(self):
@@ -437,24 +441,46 @@ class DiscreteSAC:
         # no_grad carries no autograd history -- reused by the actor's training
         # forward below it would silently cut the gradient of every weight cast
         # in both passes (the actor's GAT lin weights).
-        with self._amp(), torch.no_grad():
-            _, next_probs, _ = self.actor(next_node_x, edge_index, next_edge_attr, next_action_mask,
-                                          next_batch_vec, num_graphs=B)
-            q_next = torch.min(self.target1(next_node_x, edge_index, next_edge_attr, next_batch_vec, B),
-                               self.target2(next_node_x, edge_index, next_edge_attr, next_batch_vec, B))
+        # The three networks of each phase are independent until the losses:
+        # on the GPU they run on three side streams (after a first sequential
+        # call has built every topology cache), so their hundreds of small
+        # kernels overlap instead of queueing behind each other; each has an
+        # autocast region of its own (no cached cast is shared across streams).
+        def no_grad_pass(net, *args):
+            def run():
+                with self._amp(), torch.no_grad():
+                    return net(*args)
+            return run
+
+        next_out, qt1, qt2 = self._concurrent([
+            no_grad_pass(self.actor, next_node_x, edge_index, next_edge_attr, next_action_mask, next_batch_vec,
+                         False, B),
+            no_grad_pass(self.target1, next_node_x, edge_index, next_edge_attr, next_batch_vec, B),
+            no_grad_pass(self.target2, next_node_x, edge_index, next_edge_attr, next_batch_vec, B)])
+        with torch.no_grad():
+            next_probs = next_out[1]
+            q_next = torch.min(qt1, qt2)
             v_next = scatter_sum(next_probs * (q_next - self.alpha * torch.log(next_probs + 1e-8)), edge_batch, B,
                                  reg)
             target = reward + (1.0 - done) * self.gamma * v_next
-        with self._amp():
-            q1_all = self.critic1(node_x, edge_index, edge_attr, batch_vec, B)
-            q2_all = self.critic2(node_x, edge_index, edge_attr, batch_vec, B)
-            q1 = q1_all[action]
-            q2 = q2_all[action]
-            td_error = (target - q1).detach().abs()
-            loss1 = F.mse_loss(q1, target, reduction="none")
-            loss2 = F.mse_loss(q2, target, reduction="none")
-            critic_loss = (weights_tensor * (loss1 + loss2)).mean()
-            logits, probs, _ = self.actor(node_x, edge_index, edge_attr, action_mask, batch_vec, num_graphs=B)
+
+        def train_pass(net, *args):
+            def run():
+                with self._amp():
+                    return net(*args)
+            return run
+
+        q1_all, q2_all, act_out = self._concurrent([
+            train_pass(self.critic1, node_x, edge_index, edge_attr, batch_vec, B),
+            train_pass(self.critic2, node_x, edge_index, edge_attr, batch_vec, B),
+            train_pass(self.actor, node_x, edge_index, edge_attr, action_mask, batch_vec, False, B)])
+        logits, probs = act_out[0], act_out[1]
+        q1 = q1_all[action]
+        q2 = q2_all[action]
+        td_error = (target - q1).detach().abs()
+        loss1 = F.mse_loss(q1, target, reduction="none")
+        loss2 = F.mse_loss(q2, target, reduction="none")
+        critic_loss = (weights_tensor * (loss1 + loss2)).mean()
         q_all = torch.min(q1_all, q2_all).detach()
         # alpha detached: the reference zeroes log_alpha.grad (alpha_opt.zero_grad,
         # sac.py:236) after actor_loss.backward, so this term never reaches it
@@ -483,6 +509,7 @@ class DiscreteSAC:
         critic_loss.backward()
         actor_loss.backward()
         alpha_loss.backward()
+        self._warm = True
         return {
             "critic_loss": critic_loss.detach(),
             "actor_loss": actor_loss.detach(),
@@ -494,6 +521,29 @@ class DiscreteSAC:
             "logp_mean": logp_mean,
             "td_errors": td_error,
         }
+
+    def _concurrent(self, fns):
+        """Run the callables on side streams forked from (and joined back into)
+        the current stream; sequentially on the CPU, with concurrent=False, or
+        before the first compute_gradients has completed."""
+        dev = self.log_alpha.device
+        if dev.type != "cuda" or not self.concurrent or not self._warm:
+            return [fn() for fn in fns]
+        main = torch.cuda.current_stream(dev)
+        if self._side is None:
+            self._side = [torch.cuda.Stream(dev) for _ in range(3)]
+        outs = []
+        for st, fn in zip(self._side, fns):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                outs.append(fn())
+        for st in self._side[:len(fns)]:
+            main.wait_stream(st)
+        for o in outs:   # consumed (and freed) on the main stream from here on
+            for t in (o if isinstance(o, (tuple, list)) else (o,)):
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(main)
+        return outs
 
     def apply_gradients(self, alpha_max: float = None):
         """Clipping, the three optimizer steps, the log_alpha clamps and the

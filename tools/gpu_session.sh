@@ -24,6 +24,7 @@ for s in "$@"; do
         benchq) step bench 400 python bench.py --steps 44 --warmup 22 --cpu-seconds 5 ;;
         benchenv) step bench_env 400 python bench.py --workload env --steps 66 --warmup 22 --no-cpu ;;
         benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
+        opprobe) step op_probe 300 python tools/op_probe.py ;;
         castprobe) step cast_probe 300 python tools/cast_probe.py ;;
         perbench) step per_bench 200 rocprofv3 --kernel-trace --stats -d gpurun_out/perb -o run --output-format csv -- python3 tools/per_bench.py 50 ;;
         pertests) step per_tests 300 python -u -m pytest tests/test_per_tree.py tests/test_replay_train.py -x -v --timeout 120 --timeout-method thread ;;
