@@ -1,5 +1,5 @@
 """A/B timing of the env kernel from two builds of libtrafficrl.so in one
-process each: python tools/ab_env.py <lib.so> [B] [reps]."""
+process each: python tools/ab_env.py <lib.so> [B] [reps] [scipy|torch]."""
 import os
 import sys
 
@@ -14,7 +14,8 @@ from trafficrl.env import VecRepairEnv  # noqa: E402
 
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
-env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=True, fixed_damage_seed=42)
+sp = sys.argv[4] if len(sys.argv) > 4 else "scipy"
+env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=True, fixed_damage_seed=42, sp_backend=sp)
 gen = torch.Generator(device="cuda").manual_seed(0)
 acts = [(torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32) for _ in range(2)]
 flow0, cap0, dmg0 = env.flow.clone(), env.capacity.clone(), env.damaged.clone()
@@ -28,4 +29,4 @@ for r in range(reps):
     torch.cuda.synchronize()
     ms.append(s.elapsed_time(e))
 ms = sorted(ms)[2:-2]
-print(f"{os.path.basename(sys.argv[1])}: step kernel {sum(ms) / len(ms):.4f} ms (B={B})")
+print(f"{os.path.basename(sys.argv[1])} [{sp}]: step kernel {sum(ms) / len(ms):.4f} ms (B={B})")

@@ -23,6 +23,9 @@ for s in "$@"; do
         bench) step bench 600 python bench.py ;;
         benchq) step bench 400 python bench.py --steps 44 --warmup 22 --cpu-seconds 5 ;;
         benchenv) step bench_env 400 python bench.py --workload env --steps 66 --warmup 22 --no-cpu ;;
+        benchtorch) step bench_torch 400 python bench.py --sp torch --steps 44 --warmup 22 --no-cpu
+                    step bench_env_torch 400 python bench.py --workload env --sp torch --steps 66 --warmup 22 --no-cpu ;;
+        benchana) step bench_ana 600 python bench.py --network anaheim --steps 10 --warmup 3 --cpu-seconds 5 ;;
         benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
         opprobe) step op_probe 300 python tools/op_probe.py ;;
         castprobe) step cast_probe 300 python tools/cast_probe.py ;;
@@ -49,6 +52,7 @@ for s in "$@"; do
         abact) TRX_LIB=${TRX_LIB_A:-} step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act
                TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         abk) step ab_quad 200 env TRX_KERNEL=quad python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 && step ab_packed 200 python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
+        abt) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step abt_$n 200 python tools/ab_env.py $f 4096 20 torch || exit 1; done ;;
         abx) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step ab_$n 200 python tools/ab_env.py $f 4096 30 || exit 1; done ;;
         pmcab) for k in quad packed; do
                  step pmc_${k}_1 200 env TRX_KERNEL=$k rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d gpurun_out/pmc_${k}_1 -o run --output-format csv -- python3 tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 6 || exit 1
