@@ -47,6 +47,14 @@ __device__ __forceinline__ float wave_sum_f(float v) {
            (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
 }
+// every lane gets the total of its 16-lane row
+__device__ __forceinline__ float row_sum16_f(float v) {
+    v = v + TRX_DPP(v, 0xB1);
+    v = v + TRX_DPP(v, 0x4E);
+    v = v + TRX_DPP(v, 0x141);
+    v = v + TRX_DPP(v, 0x140);
+    return v;
+}
 #define TRX_DPPM(v, ctrl) \
     __int_as_float(__builtin_amdgcn_update_dpp((int)0xff800000, __float_as_int(v), ctrl, 0xf, 0xf, false))
 __device__ __forceinline__ float wave_max_f(float v) {
@@ -225,36 +233,32 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
     }
     TRX_ISTAMP(1);
 
-    // 2. attention dot products <xh[i,h,:], att[h,:]>: one wave per (node, head)
-    //    pair, lane owns channels 4*lane .. 4*lane+3 (C <= 256; conflict-free LDS
-    //    reads), wave sums.  Pairs t = h*n + i in contiguous per-wave ranges.
+    // 2. attention dot products <xh[i,h,:], att[h,:]>: four (node, head) pairs per
+    //    wave at a time, one per 16-lane row; a lane owns channels 4*sl + 64*m
+    //    (conflict-free LDS reads) and the row sums by DPP (no readlane chain).
+    //    Pairs t = h*n + i, groups of four dealt round-robin to the waves.
     {
-        const int P = n * H, per = (P + kInferWaves - 1) / kInferWaves;
-        const int t0 = wave * per, t1 = t0 + per < P ? t0 + per : P;
-        const int c = 4 * lane;
-        const bool cok = c < C;
-        int hcur = -1;
-        float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), da = sa;
-        for (int t = t0; t < t1; ++t) {
-            const int h = t / n, i = t - h * n;
-            if (h != hcur) {
-                hcur = h;
-                if (cok) {
-                    sa = *reinterpret_cast<const float4*>(a.att_src + h * C + c);
-                    da = *reinterpret_cast<const float4*>(a.att_dst + h * C + c);
+        const int P = n * H, groups = (P + 3) / 4;
+        const int sub = lane >> 4, sl = lane & 15;
+        for (int gi = wave; gi < groups; gi += kInferWaves) {
+            const int t = 4 * gi + sub;
+            const bool ok = t < P;
+            const int h = ok ? t / n : 0, i = ok ? t - h * n : 0;
+            float s1 = 0.0f, s2 = 0.0f;
+            if (ok) {
+                for (int c = 4 * sl; c < C; c += 64) {
+                    const float4 sa = *reinterpret_cast<const float4*>(a.att_src + h * C + c);
+                    const float4 da = *reinterpret_cast<const float4*>(a.att_dst + h * C + c);
+                    const uint2 u = *reinterpret_cast<const uint2*>(xs + i * HC + h * C + c);
+                    const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
+                    const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
+                    s1 += (v0 * sa.x + v1 * sa.y) + (v2 * sa.z + v3 * sa.w);
+                    s2 += (v0 * da.x + v1 * da.y) + (v2 * da.z + v3 * da.w);
                 }
             }
-            float s1 = 0.0f, s2 = 0.0f;
-            if (cok) {
-                const uint2 u = *reinterpret_cast<const uint2*>(xs + i * HC + h * C + c);
-                const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
-                const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
-                s1 = (v0 * sa.x + v1 * sa.y) + (v2 * sa.z + v3 * sa.w);
-                s2 = (v0 * da.x + v1 * da.y) + (v2 * da.z + v3 * da.w);
-            }
-            s1 = wave_sum_f(s1);
-            s2 = wave_sum_f(s2);
-            if (lane == 0) {
+            s1 = row_sum16_f(s1);
+            s2 = row_sum16_f(s2);
+            if (ok && sl == 0) {
                 as_[i * H + h] = s1;
                 ad_[i * H + h] = s2;
             }
