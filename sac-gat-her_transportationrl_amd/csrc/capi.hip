@@ -90,7 +90,8 @@ int check_state(const trx_state* s, bool need_initial) {
     return TRX_OK;
 }
 
-// TRX_KERNEL=quad selects the previous small-graph kernel (A/B runs)
+// TRX_KERNEL=quad selects the previous small-graph kernels (A/B runs): env_kernel_q
+// for both shortest-path rules instead of env_kernel_p (scipy) / env_kernel_t (torch)
 bool use_packed() {
     static const bool on = [] {
         const char* e = getenv("TRX_KERNEL");
@@ -119,6 +120,9 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
     } else if (p->sp_rule == TRX_SP_TORCH && g->dg.N > trx::kSmallMaxNodes) {
         return fail(TRX_EUNSUP, "sp_rule TORCH (all-pairs Floyd-Warshall) supports N <= %d (got N=%d)",
                     trx::kSmallMaxNodes, g->dg.N);
+    } else if (p->sp_rule == TRX_SP_TORCH && use_packed() && trx::torch_kernel_ok(g->dg)) {
+        e = trx::launch_env_kernel_torch(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
+                                         static_cast<hipStream_t>(stream));
     } else if (g->dg.N <= trx::kSmallMaxNodes && p->sp_rule == TRX_SP_SCIPY && use_packed() &&
                trx::packed_ok(g->dg, *p))
         e = trx::launch_env_kernel_packed(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,

@@ -131,6 +131,11 @@ hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const 
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream);
 
+bool torch_kernel_ok(const DevGraph& g);
+hipError_t launch_env_kernel_torch(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
+                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                                   const uint8_t* env_mask, hipStream_t stream);
+
 size_t big_smem_bytes(const DevGraph& g, int waves);
 int big_waves(const DevGraph& g);  // waves per workgroup that fit the LDS budget (0 = none)
 size_t big_workspace_bytes(const DevGraph& g, int num_envs);
