@@ -161,6 +161,8 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
     float* cap = (float*)(smem_raw + O.cap);
     float* tt = (float*)(smem_raw + O.t);
     float* aux = (float*)(smem_raw + O.aux);
+    uint32_t* const auxi = (uint32_t*)(smem_raw + O.aux);  // the AON loads, as integers (u32 LDS atomics are
+                                                           // native and fast; float ones are not)
     uint8_t* dmg = smem_raw + O.dmg;
     int16_t* lsrc = (int16_t*)(smem_raw + O.lsrc);
     uint2* ent = (uint2*)(smem_raw + O.ent);
@@ -347,7 +349,7 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
                     for (int h = 0; h < N && v != origin; ++h) {
                         const int pk = pe[v];
                         if (pk < 0) break;
-                        atomicAdd(&aux[pk & 0xFFFF], dm);
+                        atomicAdd(&auxi[pk & 0xFFFF], (uint32_t)dm);  // integral demands: u32 atomics
                         v = pk >> 16;
                     }
                 }
@@ -356,6 +358,8 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
             TRX_BIG_COUNT(5, TRX_BIG_CLOCK() - clk2);
         }
         unassigned_lane = un;
+        __syncthreads();
+        for (int e = tid; e < E; e += L) aux[e] = (float)auxi[e];  // exact: < 2^24
         __syncthreads();
 
         // ---------------- flow update + BPR (repair_env.py:317-342)
