@@ -199,9 +199,11 @@ def env_kernel_name(big, sp):
     """The env kernel trx_step launches for this workload (capi.hip run())."""
     if big:
         return "trx::env_kernel_big"
-    if sp == "scipy" and os.environ.get("TRX_KERNEL", "") != "quad":
+    if os.environ.get("TRX_KERNEL", "") == "quad":
+        return "trx::env_kernel_q<24>"     # the round-1 quad kernel (A/B runs)
+    if sp == "scipy":
         return "trx::env_kernel_p<24>"     # packed-key Dijkstra (assign_packed.hip)
-    return "trx::env_kernel_q<24>"
+    return "trx::env_kernel_t<24>"         # torch rule: per-wave Floyd-Warshall (assign_torch.hip)
 
 
 def main():
