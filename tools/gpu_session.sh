@@ -27,6 +27,7 @@ for s in "$@"; do
                     step bench_env_torch 400 python bench.py --workload env --sp torch --steps 66 --warmup 22 --no-cpu ;;
         benchana) step bench_ana 600 python bench.py --network anaheim --steps 10 --warmup 3 --cpu-seconds 5 ;;
         benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
+        wgrad) step wgrad 200 python tools/wgrad_probe.py ;;
         opprobe) step op_probe 300 python tools/op_probe.py ;;
         castprobe) step cast_probe 300 python tools/cast_probe.py ;;
         perbench) step per_bench 200 rocprofv3 --kernel-trace --stats -d gpurun_out/perb -o run --output-format csv -- python3 tools/per_bench.py 50 ;;
