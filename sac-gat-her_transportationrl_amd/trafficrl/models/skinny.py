@@ -28,11 +28,19 @@ _SPLIT = 256
 
 
 def _splitk_wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-    """dW[o, i] = sum_k dy[k, o] x[k, i] in (at least) float32, split-K when K allows."""
+    """dW[o, i] = sum_k dy[k, o] x[k, i] in (at least) float32, split-K when K allows.
+    bf16 operands (autocast): the 256-row partial products run in bf16 on the
+    MFMA path (float32 accumulation, one bf16 rounding per partial) and are
+    summed in float32 -- no float32 copies of dy and x."""
     K = dy.shape[0]
     acc = torch.float64 if dy.dtype == torch.float64 else torch.float32
+    split = K % _SPLIT == 0 and K >= 4 * _SPLIT
+    if split and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
+        S = K // _SPLIT
+        part = torch.bmm(dy.reshape(S, _SPLIT, -1).transpose(1, 2), x.reshape(S, _SPLIT, -1))
+        return part.sum(0, dtype=torch.float32)
     dy32, x32 = dy.to(acc), x.to(acc)
-    if K % _SPLIT or K < 4 * _SPLIT:
+    if not split:
         return dy32.t() @ x32
     S = K // _SPLIT
     part = torch.bmm(dy32.view(S, _SPLIT, -1).transpose(1, 2), x32.view(S, _SPLIT, -1))
