@@ -469,6 +469,17 @@ int trx_multi_copy(const trx_copy_list* l, void* stream);
  * in one launch.                                                          */
 int trx_multi_gather(const trx_copy_list* l, const int64_t* idx, int32_t nrows, void* stream);
 
+/* --------------------------------------------- trainer episode bookkeeping
+ * One vector step of src/train.py's per-env bookkeeping (916-935) for all envs:
+ * ep_len += 1; scaled = reward * reward_scale (float64; scaled_f32 its float32
+ * replay copy); done_f32 = done; ep_reward += scaled; ep_tstt_sum += tstt;
+ * ep_auc += 0.5 * (ep_prev_tstt + tstt) * (ep_len > 1); ep_prev_tstt = tstt;
+ * finished = done | (max_steps > 0 && ep_len >= max_steps).            */
+int trx_episode_step(int32_t num_envs, const double* reward, const uint8_t* done, const double* tstt,
+                     double reward_scale, int64_t max_steps, double* scaled, float* scaled_f32, float* done_f32,
+                     double* ep_reward, double* ep_tstt_sum, double* ep_auc, double* ep_prev_tstt, int64_t* ep_len,
+                     uint8_t* finished, void* stream);
+
 /* ------------------------------------------------------ graph support
  * Rewrites every memset node of a captured, not yet instantiated hipGraph_t
  * (passed as void*) into an equivalent fill-kernel node with the same

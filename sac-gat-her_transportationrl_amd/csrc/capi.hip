@@ -824,6 +824,21 @@ int trx_bf16_round(const trx_round_list* l, void* stream) {
     return TRX_OK;
 }
 
+int trx_episode_step(int32_t num_envs, const double* reward, const uint8_t* done, const double* tstt,
+                     double reward_scale, int64_t max_steps, double* scaled, float* scaled_f32, float* done_f32,
+                     double* ep_reward, double* ep_tstt_sum, double* ep_auc, double* ep_prev_tstt, int64_t* ep_len,
+                     uint8_t* finished, void* stream) {
+    if (num_envs < 0 || (num_envs > 0 && (!reward || !done || !tstt || !scaled || !scaled_f32 || !done_f32 ||
+                                          !ep_reward || !ep_tstt_sum || !ep_auc || !ep_prev_tstt || !ep_len ||
+                                          !finished)))
+        return fail(TRX_EINVAL, "episode_step args");
+    hipError_t e = trx::launch_episode_step(num_envs, reward, done, tstt, reward_scale, max_steps, scaled, scaled_f32,
+                                            done_f32, ep_reward, ep_tstt_sum, ep_auc, ep_prev_tstt, ep_len, finished,
+                                            static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "episode_step launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_multi_gather(const trx_copy_list* l, const int64_t* idx, int32_t nrows, void* stream) {
     if (!l || l->count < 0 || l->count > TRX_MAX_COPY || nrows < 0 || (nrows > 0 && !idx))
         return fail(TRX_EINVAL, "multi_gather: count must be 0..16, nrows >= 0, idx");

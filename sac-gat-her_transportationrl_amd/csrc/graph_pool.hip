@@ -151,4 +151,44 @@ hipError_t launch_multi_copy(const trx_copy_list& l, hipStream_t stream) {
     hipLaunchKernelGGL(multi_copy_kernel, dim3(bx, l.count), dim3(256), 0, stream, l);
     return hipGetLastError();
 }
+// ------------------------------------------------------------------------
+// Per-step episode bookkeeping of the vectorised trainer (src/train.py:916-935:
+// reward scaling, episode reward / TSTT sum / AUC, truncation) for all B envs
+// in one launch instead of ~12 elementwise torch ops; float64 like the
+// reference's Python floats, in the same operation order.
+namespace {
+__global__ void episode_step_kernel(int B, const double* __restrict__ reward, const uint8_t* __restrict__ done,
+                                    const double* __restrict__ tstt, double reward_scale, int64_t max_steps,
+                                    double* __restrict__ scaled, float* __restrict__ scaled_f32,
+                                    float* __restrict__ done_f32, double* __restrict__ ep_reward,
+                                    double* __restrict__ ep_tstt_sum, double* __restrict__ ep_auc,
+                                    double* __restrict__ ep_prev_tstt, int64_t* __restrict__ ep_len,
+                                    uint8_t* __restrict__ finished) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int64_t ln = ep_len[b] + 1;
+    ep_len[b] = ln;
+    const double sv = reward[b] * reward_scale;
+    scaled[b] = sv;
+    scaled_f32[b] = (float)sv;
+    done_f32[b] = done[b] ? 1.0f : 0.0f;
+    ep_reward[b] = ep_reward[b] + sv;
+    const double t = tstt[b];
+    ep_tstt_sum[b] = ep_tstt_sum[b] + t;
+    ep_auc[b] = ep_auc[b] + (0.5 * (ep_prev_tstt[b] + t)) * (ln > 1 ? 1.0 : 0.0);
+    ep_prev_tstt[b] = t;
+    finished[b] = (done[b] != 0 || (max_steps > 0 && ln >= max_steps)) ? 1 : 0;
+}
+}  // namespace
+
+hipError_t launch_episode_step(int B, const double* reward, const uint8_t* done, const double* tstt,
+                               double reward_scale, int64_t max_steps, double* scaled, float* scaled_f32,
+                               float* done_f32, double* ep_reward, double* ep_tstt_sum, double* ep_auc,
+                               double* ep_prev_tstt, int64_t* ep_len, uint8_t* finished, hipStream_t stream) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(episode_step_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, B, reward, done, tstt,
+                       reward_scale, max_steps, scaled, scaled_f32, done_f32, ep_reward, ep_tstt_sum, ep_auc,
+                       ep_prev_tstt, ep_len, finished);
+    return hipGetLastError();
+}
 }  // namespace trx

@@ -171,6 +171,10 @@ int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
 int small_ln_blocks(int N);
 hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream);
+hipError_t launch_episode_step(int B, const double* reward, const uint8_t* done, const double* tstt,
+                               double reward_scale, int64_t max_steps, double* scaled, float* scaled_f32,
+                               float* done_f32, double* ep_reward, double* ep_tstt_sum, double* ep_auc,
+                               double* ep_prev_tstt, int64_t* ep_len, uint8_t* finished, hipStream_t stream);
 hipError_t launch_multi_gather(const trx_copy_list& l, const int64_t* idx, int nrows, hipStream_t stream);
 hipError_t launch_multi_copy(const trx_copy_list& l, hipStream_t stream);
 hipError_t launch_graph_pool_fwd(int B, int n, int F, const float* x, float* out, float* ties, hipStream_t stream);

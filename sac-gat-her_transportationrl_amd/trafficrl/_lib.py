@@ -29,7 +29,7 @@ EXPORTS = (
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
-    "trx_damage_sample", "trx_multi_gather",
+    "trx_damage_sample", "trx_multi_gather", "trx_episode_step",
 )
 
 
@@ -216,6 +216,7 @@ def load():
                                       ctypes.c_double, _vp]
     L.trx_per32_update.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _i32, _vp, ctypes.c_double, ctypes.c_double, _vp]
     L.trx_per32_sample.argtypes = [_vp, ctypes.c_int64, _vp, _i32, _vp, _vp, _vp]
+    L.trx_episode_step.argtypes = [_i32, _vp, _vp, _vp, ctypes.c_double, ctypes.c_int64] + [_vp] * 9 + [_vp]
     L.trx_multi_gather.argtypes = [ctypes.POINTER(TrxCopyList), _vp, _i32, _vp]
     L.trx_damage_sample.argtypes = [_i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]
     L.trx_graph_pool_backward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]
@@ -240,7 +241,8 @@ def load():
                  "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward",
                  "trx_bf16_round", "trx_multi_copy",
                  "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
-                 "trx_per32_sample", "trx_damage_sample", "trx_multi_gather"):
+                 "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
+                 "trx_episode_step"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

@@ -101,6 +101,9 @@ class DeviceReplay:
         self.size = 0
         self.size_t = torch.zeros((), dtype=torch.float64, device=dev)  # device copy for graph-captured sampling
 
+    def _ring_idx(self, B: int) -> torch.Tensor:
+        return (self.ptr + torch.arange(B, device=self.device)) % self.capacity
+
     def _set(self, idx: torch.Tensor, leaf: torch.Tensor, distinct: bool = False):
         """distinct: the caller guarantees no repeated index (ring-buffer adds of
         at most `capacity` entries), so no last-wins resolution is needed."""
@@ -119,6 +122,7 @@ class DeviceReplay:
                               src.reshape((B,) + dst.shape[1:]).to(dst.dtype).contiguous()) for dst, src in pairs],
                             self.device)
         else:
+            idx = self._ring_idx(B) if idx is None else idx
             for dst, src in pairs:
                 dst.index_copy_(0, idx, src.reshape((B,) + dst.shape[1:]).to(dst.dtype))
 
@@ -139,7 +143,7 @@ class DeviceReplay:
         B = action.shape[0]
         assert getattr(self, "_staged", None) == B, "stage_prev() first"
         self._staged = None
-        idx = (self.ptr + torch.arange(B, device=self.device)) % self.capacity
+        idx = None   # staged slots are contiguous: no index tensor needed (see _ring_idx)
         self._write(idx, ((self.action, action), (self.reward, reward), (self.next_node_x, next_node_x),
                           (self.next_edge_x, next_edge_x), (self.next_mask, next_mask), (self.done, done),
                           (self.next_tstt, next_tstt), (self.init_tstt, init_tstt)), B)
@@ -161,6 +165,7 @@ class DeviceReplay:
                                            float(self.eps), float(self.alpha), _lib.stream_ptr(self.device)),
                        "trx_per_add_range")
         else:
+            idx = self._ring_idx(B) if idx is None else idx
             pr = self.max_priority + self.eps * torch.arange(1, B + 1, device=self.device, dtype=torch.float64)
             self.max_priority.copy_(pr[-1])   # in place: graph-captured updates read this tensor
             self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)

@@ -280,6 +280,11 @@ class Trainer:
         self.ep_auc = torch.zeros(B, dtype=torch.float64, device=self.device)
         self.ep_prev_tstt = torch.zeros(B, dtype=torch.float64, device=self.device)
         self.ep_len = torch.zeros(B, dtype=torch.int64, device=self.device)
+        # per-step outputs of trx_episode_step (scaled reward f64 / f32, done as float, finished)
+        self._scaled = torch.zeros(B, dtype=torch.float64, device=self.device)
+        self._scaled32 = torch.zeros(B, dtype=torch.float32, device=self.device)
+        self._done32 = torch.zeros(B, dtype=torch.float32, device=self.device)
+        self._finished = torch.zeros(B, dtype=torch.uint8, device=self.device)
         self.episodes_done = 0
         self.history = []
         self.last_losses: Dict = {}
@@ -402,23 +407,36 @@ class Trainer:
             goal = env.goal.clone()
             prev_tstt = env.tstt.clone()
         next_obs, reward, done, info = env.step(actions.to(torch.int32), check=False)
-        scaled = reward * cfg["reward_scale"]
-        self.ep_len += 1
-        trunc = (self.ep_len >= int(cfg["max_steps"])) if cfg["max_steps"] > 0 else torch.zeros_like(done)
+        if self.device.type == "cuda":
+            # reward scaling + episode stats + truncation: one trx_episode_step launch
+            L = _lib.load()
+            _lib.check(L.trx_episode_step(self.B, _lib.ptr(env.reward), _lib.ptr(env.done), _lib.ptr(env.tstt),
+                                          float(cfg["reward_scale"]), int(cfg["max_steps"]), _lib.ptr(self._scaled),
+                                          _lib.ptr(self._scaled32), _lib.ptr(self._done32), _lib.ptr(self.ep_reward),
+                                          _lib.ptr(self.ep_tstt_sum), _lib.ptr(self.ep_auc),
+                                          _lib.ptr(self.ep_prev_tstt), _lib.ptr(self.ep_len), _lib.ptr(self._finished),
+                                          _lib.stream_ptr(self.device)), "trx_episode_step")
+            scaled, done_f = self._scaled32, self._done32
+            finished = self._finished.view(torch.bool)
+        else:
+            scaled = reward * cfg["reward_scale"]
+            self.ep_len += 1
+            trunc = (self.ep_len >= int(cfg["max_steps"])) if cfg["max_steps"] > 0 else torch.zeros_like(done)
+            self.ep_reward += scaled
+            self.ep_tstt_sum += env.tstt
+            self.ep_auc += 0.5 * (self.ep_prev_tstt + env.tstt) * (self.ep_len > 1)
+            self.ep_prev_tstt.copy_(env.tstt)
+            done_f = done.float()
+            finished = done | trunc
         if staged:
             self.replay.add_staged(actions, scaled, next_obs.node_x, next_obs.edge_x, next_obs.action_mask,
-                                   done.float(), env.tstt, env.initial_tstt)
+                                   done_f, env.tstt, env.initial_tstt)
         else:
             self.replay.add_batch(prev_obs[0], prev_obs[1], prev_obs[2], actions, scaled, next_obs.node_x,
-                                  next_obs.edge_x, next_obs.action_mask, done.float(), goal, prev_tstt, env.tstt,
+                                  next_obs.edge_x, next_obs.action_mask, done_f, goal, prev_tstt, env.tstt,
                                   env.initial_tstt)
-        self.ep_reward += scaled
-        self.ep_tstt_sum += env.tstt
-        self.ep_auc += 0.5 * (self.ep_prev_tstt + env.tstt) * (self.ep_len > 1)
-        self.ep_prev_tstt.copy_(env.tstt)
         for _ in range(self.updates_due(it)):
             self.update()
-        finished = done | trunc
         return next_obs, finished
 
     def _gather_episodes(self, finished: torch.Tensor):

@@ -300,3 +300,43 @@ def test_sample_rows_match_indexing():
     for name in ("node_x", "edge_x", "mask", "action", "reward", "next_node_x", "next_edge_x", "next_mask", "done",
                  "goal", "prev_tstt", "next_tstt", "init_tstt"):
         assert torch.equal(getattr(s, name), getattr(rb, name)[s.idx]), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_steps", [0, 3])
+def test_episode_step_kernel_matches_torch_ops(max_steps):
+    """trx_episode_step == the trainer's torch bookkeeping (float64, same op order), bit for bit."""
+    from trafficrl import _lib
+    d = torch.device("cuda", 0)
+    g = torch.Generator(device=d).manual_seed(9)
+    B = 1000
+    reward = torch.randn(B, dtype=torch.float64, device=d, generator=g) * 3
+    done = (torch.rand(B, device=d, generator=g) < 0.3).to(torch.uint8)
+    tstt = torch.rand(B, dtype=torch.float64, device=d, generator=g) * 1e6
+    st = {k: torch.randn(B, dtype=torch.float64, device=d, generator=g) for k in ("rew", "sum", "auc", "prev")}
+    ep_len = torch.randint(0, 4, (B,), device=d, generator=g)
+    ref = {k: v.clone() for k, v in st.items()}
+    ref_len = ep_len.clone()
+    scale = 0.5
+    # torch ops of Trainer.iteration (CPU branch)
+    scaled_ref = reward * scale
+    ref_len += 1
+    trunc = (ref_len >= max_steps) if max_steps > 0 else torch.zeros_like(done, dtype=torch.bool)
+    ref["rew"] += scaled_ref
+    ref["sum"] += tstt
+    ref["auc"] += 0.5 * (ref["prev"] + tstt) * (ref_len > 1)
+    ref["prev"].copy_(tstt)
+    fin_ref = done.bool() | trunc
+    out = dict(scaled=torch.empty(B, dtype=torch.float64, device=d), s32=torch.empty(B, device=d),
+               d32=torch.empty(B, device=d), fin=torch.empty(B, dtype=torch.uint8, device=d))
+    L = _lib.load()
+    _lib.check(L.trx_episode_step(B, _lib.ptr(reward), _lib.ptr(done), _lib.ptr(tstt), scale, max_steps,
+                                  _lib.ptr(out["scaled"]), _lib.ptr(out["s32"]), _lib.ptr(out["d32"]), _lib.ptr(st["rew"]),
+                                  _lib.ptr(st["sum"]), _lib.ptr(st["auc"]), _lib.ptr(st["prev"]), _lib.ptr(ep_len),
+                                  _lib.ptr(out["fin"]), _lib.stream_ptr(d)), "trx_episode_step")
+    torch.cuda.synchronize()
+    assert torch.equal(out["scaled"], scaled_ref) and torch.equal(out["s32"], scaled_ref.float())
+    assert torch.equal(out["d32"], done.float()) and torch.equal(out["fin"].bool(), fin_ref)
+    assert torch.equal(ep_len, ref_len)
+    for k in st:
+        assert torch.equal(st[k], ref[k]), k
