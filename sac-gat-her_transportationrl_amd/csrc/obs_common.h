@@ -36,6 +36,35 @@ __device__ float pairwise_any(const float* a, int n) {
     return __fadd_rn(pairwise_any(a, n2), pairwise_any(a + n2, n - n2));
 }
 
+// remaining goal ratio, avg undamaged flow (np.mean), log10 tstt (repair_env.py:772-785)
+// from the three float32 link sums: rem = sum(goal * damaged), gtot = sum(goal),
+// fsum = sum(flow of the nund undamaged links), each in numpy's pairwise order.
+__device__ void obs_env_scalars(const DevGraph& g, const trx_state& s, int gb, float rem, float gtot, float fsum,
+                                int nund, float* out3) {
+    const int E = g.E;
+    double remaining_ratio = (double)rem / ((double)gtot > 1.0 ? (double)gtot : 1.0);
+    double avg_flow = nund > 0 ? (double)(float)((double)fsum / (double)nund) : 0.0;
+    double denom = g.total_demand / (double)(E > 1 ? E : 1);
+    double avg_norm = avg_flow / (denom > 1.0 ? denom : 1.0);
+    double ts = s.tstt[gb];
+    double log_tstt = log10(ts > 1.0 ? ts : 1.0);
+    out3[0] = (float)remaining_ratio;
+    out3[1] = (float)avg_norm;
+    out3[2] = (float)log_tstt;
+}
+
+// node v of env gb: betweenness / max betweenness and the three per-env scalars
+__device__ void obs_node_features(int N, int gb, int v, float bw, float bmax, const float* sc3,
+                                  float* __restrict__ node_x) {
+    float b = bw;
+    if (bmax > 0.0f) b = __fdiv_rn(b, bmax);
+    float* nx = node_x + ((size_t)gb * N + v) * 4;
+    nx[0] = b;
+    nx[1] = sc3[0];
+    nx[2] = sc3[1];
+    nx[3] = sc3[2];
+}
+
 // One thread per env: bw [N] = normalised-by-networkx betweenness (float32,
 // before division by its max); prod = scratch of >= E floats.
 // goal / dmg / flow: the env's [E] rows (global memory, or LDS copies staged by the caller).
@@ -44,33 +73,17 @@ __device__ void obs_env_features(const DevGraph& g, const trx_state& s, int gb, 
     const int N = g.N, E = g.E;
     float bmax = 0.0f;
     for (int v = 0; v < N; ++v) bmax = fmaxf(bmax, bw[v]);
-    // remaining goal ratio, avg undamaged flow (np.mean), log10 tstt (772-785)
     for (int e = 0; e < E; ++e) prod[e] = __fmul_rn(goal[e], dmg[e]);
     float rem = pairwise_any(prod, E);
     for (int e = 0; e < E; ++e) prod[e] = goal[e];
     float gtot = pairwise_any(prod, E);
-    double remaining_ratio = (double)rem / ((double)gtot > 1.0 ? (double)gtot : 1.0);
     int nund = 0;
     for (int e = 0; e < E; ++e)
         if (dmg[e] == 0.0f) prod[nund++] = flow[e];
-    double avg_flow = 0.0;
-    if (nund > 0) {
-        float sm = pairwise_any(prod, nund);
-        avg_flow = (double)(float)((double)sm / (double)nund);
-    }
-    double denom = g.total_demand / (double)(E > 1 ? E : 1);
-    double avg_norm = avg_flow / (denom > 1.0 ? denom : 1.0);
-    double ts = s.tstt[gb];
-    double log_tstt = log10(ts > 1.0 ? ts : 1.0);
-    for (int v = 0; v < N; ++v) {
-        float b = bw[v];
-        if (bmax > 0.0f) b = __fdiv_rn(b, bmax);
-        float* nx = node_x + ((size_t)gb * N + v) * 4;
-        nx[0] = b;
-        nx[1] = (float)remaining_ratio;
-        nx[2] = (float)avg_norm;
-        nx[3] = (float)log_tstt;
-    }
+    float fsum = nund > 0 ? pairwise_any(prod, nund) : 0.0f;
+    float sc3[3];
+    obs_env_scalars(g, s, gb, rem, gtot, fsum, nund, sc3);
+    for (int v = 0; v < N; ++v) obs_node_features(N, gb, v, bw[v], bmax, sc3, node_x);
 }
 
 // Link e of env gb: t0_norm, cap_norm, clip(log1p(v/c)), damaged, goal, id/(E-1) (767-770, 796-808)

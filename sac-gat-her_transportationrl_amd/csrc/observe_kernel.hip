@@ -8,6 +8,8 @@
 // dependency sweep pops the queue in reverse, per-source contributions are
 // summed over sources in networkx node order.  One lane per (env, source);
 // per-lane BFS state lives node-major in LDS ([node][lane], conflict-free).
+// Damaged links are folded into per-env CSR slot tables (head / tail, -1 when
+// damaged) so a BFS edge step is one LDS read, not two dependent ones.
 #include <hip/hip_runtime.h>
 
 #include "obs_common.h"
@@ -29,49 +31,46 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     const int L = kObsThreads;
     const int tid = threadIdx.x;
     const int env0 = blockIdx.x * EPW;
-    // LDS: sigma[N][L] f64, delta[N][L] f64, dist[N][L] i16, queue[N][L] u8, dmg[EPW][E] f32, insub[EPW][N] u8
-    double* sigma = reinterpret_cast<double*>(smem_raw);
-    double* delta = sigma + (size_t)N * L;
-    int16_t* dist = reinterpret_cast<int16_t*>(delta + (size_t)N * L);
-    uint8_t* queue = reinterpret_cast<uint8_t*>(dist + (size_t)N * L);
-    float* dmg = reinterpret_cast<float*>(queue + (((size_t)N * L + 15) & ~size_t(15)));
-    uint8_t* insub = reinterpret_cast<uint8_t*>(dmg + (size_t)EPW * E);
-    int* nsub = reinterpret_cast<int*>(insub + (((size_t)EPW * N + 15) & ~size_t(15)));
-    float* goal_l = reinterpret_cast<float*>(nsub + 16);  // [EPW][E] staged for the per-env features
-    float* flow_l = goal_l + (size_t)EPW * E;             // [EPW][E]
-    // the graph's adjacency (read in every BFS step) staged as int16
-    int16_t* gop = reinterpret_cast<int16_t*>(flow_l + (size_t)EPW * E);  // out_ptr [N+1]
-    int16_t* gip = gop + (N + 1);                                          // in_ptr  [N+1]
-    int16_t* goe = gip + (N + 1);                                          // out_eid [E]
-    int16_t* god = goe + E;                                                // out_dst [E]
-    int16_t* gie = god + E;                                                // in_eid  [E]
-    int16_t* gis = gie + E;                                                // in_src  [E]
-    int16_t* gnx = gis + E;                                                // nx_order [N]
+    // LDS (sized so that 8 blocks of a 24-node graph share one CU):
+    //   delta[N][L] f64, sigma[N][L] u16, dist[N][L] u8 (0xff = unreached), queue[N][L] u8,
+    //   odst[EPW][E] i8 (head of CSR out-slot k, -1 when that link is damaged),
+    //   isrc[EPW][E] i8 (tail of CSR in-slot k, -1 when damaged), insub[EPW][N] u8, nsub[16] i32,
+    //   out_ptr / in_ptr [N+1] and nx_order [N] as int16.
+    // (Keeping the BFS levels as node bit masks in registers instead of dist[]
+    // measured 11% slower: 87 vs 78 us at B=4096.)
+    // sigma counts shortest paths: every one of them takes one node from each BFS
+    // level strictly between source and target, so sigma <= prod(level sizes) with
+    // sum(level sizes) <= N-2, i.e. <= 3^10 = 59049 for N <= 32 -- exact in u16 and,
+    // converted, the same float64 value networkx's float sigma holds.
+    double* delta = reinterpret_cast<double*>(smem_raw);
+    uint16_t* sigma = reinterpret_cast<uint16_t*>(delta + (size_t)N * L);
+    uint8_t* dist = reinterpret_cast<uint8_t*>(sigma + (size_t)N * L);
+    uint8_t* queue = dist + (size_t)N * L;
+    int8_t* odst = reinterpret_cast<int8_t*>(queue + (size_t)N * L);
+    int8_t* isrc = odst + (size_t)EPW * E;
+    uint8_t* insub = reinterpret_cast<uint8_t*>(isrc + (size_t)EPW * E);
+    int* nsub = reinterpret_cast<int*>(smem_raw + (((size_t)N * L * 12 + 2 * (size_t)EPW * E + EPW * N + 15) & ~size_t(15)));
+    int16_t* gop = reinterpret_cast<int16_t*>(nsub + 16);  // out_ptr [N+1]
+    int16_t* gip = gop + (N + 1);                          // in_ptr  [N+1]
+    int16_t* gnx = gip + (N + 1);                          // nx_order [N]
     for (int i = tid; i <= N; i += L) {
         gop[i] = (int16_t)g.out_ptr[i];
         gip[i] = (int16_t)g.in_ptr[i];
     }
-    for (int i = tid; i < E; i += L) {
-        goe[i] = (int16_t)g.out_eid[i];
-        god[i] = (int16_t)g.out_dst[i];
-        gie[i] = (int16_t)g.in_eid[i];
-        gis[i] = (int16_t)g.in_src[i];
-    }
     for (int i = tid; i < N; i += L) gnx[i] = (int16_t)g.nx_order[i];
-
     for (int i = tid; i < EPW * E; i += L) {
-        int el = i / E, gb = env0 + el;
-        const size_t gi = (size_t)gb * E + (i - el * E);
-        dmg[i] = gb < B ? s.damaged[gi] : 1.0f;
-        goal_l[i] = gb < B ? s.goal[gi] : 0.0f;
-        flow_l[i] = gb < B ? s.flow[gi] : 0.0f;
+        int el = i / E, k = i - el * E, gb = env0 + el;
+        const float* dm = s.damaged + (size_t)(gb < B ? gb : 0) * E;
+        bool ok = gb < B;
+        odst[i] = ok && dm[g.out_eid[k]] == 0.0f ? (int8_t)g.out_dst[k] : (int8_t)-1;
+        isrc[i] = ok && dm[g.in_eid[k]] == 0.0f ? (int8_t)g.in_src[k] : (int8_t)-1;
     }
     __syncthreads();
     for (int i = tid; i < EPW * N; i += L) {
         int el = i / N, v = i - el * N;
         int in = 0;
-        for (int j = gop[v]; j < gop[v + 1] && !in; ++j) in = dmg[el * E + goe[j]] == 0.0f;
-        for (int j = gip[v]; j < gip[v + 1] && !in; ++j) in = dmg[el * E + gie[j]] == 0.0f;
+        for (int k = gop[v]; k < gop[v + 1] && !in; ++k) in = odst[el * E + k] >= 0;
+        for (int k = gip[v]; k < gip[v + 1] && !in; ++k) in = isrc[el * E + k] >= 0;
         insub[i] = (uint8_t)in;
     }
     __syncthreads();
@@ -88,43 +87,43 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     const bool active_src = on && insub[lenv * N + src];
     if (on) {
         for (int v = 0; v < N; ++v) {
-            sigma[v * L + tid] = 0.0;
+            sigma[v * L + tid] = 0;
             delta[v * L + tid] = 0.0;
-            dist[v * L + tid] = -1;
+            dist[v * L + tid] = 0xff;
         }
     }
     if (active_src) {
-        const float* dm = dmg + lenv * E;
-        sigma[src * L + tid] = 1.0;
+        const int8_t* od = odst + lenv * E;
+        const int8_t* is = isrc + lenv * E;
+        sigma[src * L + tid] = 1;
         dist[src * L + tid] = 0;
         int qh = 0, qt = 0;
         queue[qt++ * L + tid] = (uint8_t)src;
         while (qh < qt) {
             int v = queue[qh++ * L + tid];
-            int dv = dist[v * L + tid];
-            double sv = sigma[v * L + tid];
-            for (int k = gop[v]; k < gop[v + 1]; ++k) {
-                if (dm[goe[k]] != 0.0f) continue;  // only active edges are in the subgraph
-                int w = god[k];
+            int dv1 = dist[v * L + tid] + 1;
+            uint16_t sv = sigma[v * L + tid];
+            for (int k = gop[v], ke = gop[v + 1]; k < ke; ++k) {
+                int w = od[k];
+                if (w < 0) continue;  // only active links are in the subgraph
                 int dw = dist[w * L + tid];
-                if (dw < 0) {
+                if (dw == 0xff) {
                     queue[qt++ * L + tid] = (uint8_t)w;
-                    dist[w * L + tid] = (int16_t)(dv + 1);
-                    dw = dv + 1;
+                    dist[w * L + tid] = (uint8_t)dv1;
+                    dw = dv1;
                 }
-                if (dw == dv + 1) sigma[w * L + tid] += sv;
+                if (dw == dv1) sigma[w * L + tid] += sv;
             }
         }
         // _accumulate_basic: pop in reverse BFS order
         for (int q = qt - 1; q >= 0; --q) {
             int w = queue[q * L + tid];
-            double coeff = (1.0 + delta[w * L + tid]) / sigma[w * L + tid];
-            int dw = dist[w * L + tid];
-            for (int k = gip[w]; k < gip[w + 1]; ++k) {
-                if (dm[gie[k]] != 0.0f) continue;
-                int v = gis[k];
-                if (dist[v * L + tid] >= 0 && dist[v * L + tid] == dw - 1)
-                    delta[v * L + tid] += sigma[v * L + tid] * coeff;
+            double coeff = (1.0 + delta[w * L + tid]) / (double)sigma[w * L + tid];
+            int dw1 = dist[w * L + tid] - 1;
+            for (int k = gip[w], ke = gip[w + 1]; k < ke; ++k) {
+                int v = is[k];
+                if (v < 0) continue;
+                if (dist[v * L + tid] == dw1) delta[v * L + tid] += (double)sigma[v * L + tid] * coeff;
             }
         }
     }
@@ -133,7 +132,7 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     // ---------------- per (env, node): betweenness, then per-env features
     // betweenness[w] = sum over sources s (nx order, s != w, w reached) of delta_s[w]
     float* bwv = reinterpret_cast<float*>(sigma);  // reuse after the barrier below
-    float bw_local[2] = {0.f, 0.f};
+    float bw0 = 0.f, bw1 = 0.f;  // this thread's (at most 2) nodes, kept out of scratch
     int nloc = 0;
     for (int i = tid; i < EPW * N; i += L) {
         int el = i / N, w = i - el * N;
@@ -143,7 +142,7 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
                 int s_ = gnx[jj];
                 int lane = el * N + jj;
                 if (s_ == w || !insub[el * N + s_]) continue;
-                if (dist[w * L + lane] < 0) continue;
+                if (dist[w * L + lane] == 0xff) continue;
                 bc += delta[w * L + lane];
             }
             int n = nsub[el];
@@ -152,19 +151,98 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
                 bc *= scale;
             }
         }
-        if (nloc < 2) bw_local[nloc++] = (float)bc;
+        if (nloc == 0) bw0 = (float)bc;
+        else bw1 = (float)bc;
+        ++nloc;
     }
     __syncthreads();
     nloc = 0;
     for (int i = tid; i < EPW * N; i += L) {
-        if (nloc < 2) bwv[i] = bw_local[nloc++];
+        bwv[i] = nloc == 0 ? bw0 : bw1;
+        ++nloc;
     }
     __syncthreads();
 
-    if (tid < EPW && env0 + tid < B) {
-        // feature scratch reuses delta (>= E + 8 floats per env, checked at launch)
-        obs_env_features(g, s, env0 + tid, goal_l + tid * E, dmg + tid * E, flow_l + tid * E, bwv + tid * N,
-                         reinterpret_cast<float*>(delta) + tid * (E + 8), node_x);
+    if (E > 128) {  // numpy's recursive pairwise split: one thread per env
+        if (tid < EPW && env0 + tid < B) {
+            const size_t off = (size_t)(env0 + tid) * E;
+            obs_env_features(g, s, env0 + tid, s.goal + off, s.damaged + off, s.flow + off, bwv + tid * N,
+                             reinterpret_cast<float*>(delta) + tid * (E + 8), node_x);
+        }
+    } else {
+        // The three per-env link sums in numpy's pairwise_sum order for n <= 128
+        // (8 running partials r[j] over a[j], a[j+8], ..., a tree over r, then the
+        // tail in order), the partials on 8 lanes each.  delta is free here:
+        //   cflow[EPW][E] undamaged flows compacted in link order, part[EPW][3][8],
+        //   sums[EPW][4] (rem, gtot, fsum, bmax), sc[EPW][3] scalars, nund[EPW].
+        float* cflow = reinterpret_cast<float*>(delta);
+        float* part = cflow + (size_t)EPW * E;
+        float* sums = part + (size_t)EPW * 24;
+        float* sc = sums + (size_t)EPW * 4;
+        int* nund = reinterpret_cast<int*>(sc + (size_t)EPW * 3);
+        for (int el = 0; el < EPW; ++el) {  // one wave: ballot compaction
+            const int gb = env0 + el;
+            if (gb >= B) break;
+            const float* dm = s.damaged + (size_t)gb * E;
+            const float* fl = s.flow + (size_t)gb * E;
+            int cnt = 0;
+            for (int b0 = 0; b0 < E; b0 += L) {
+                const int e = b0 + tid;
+                const bool und = e < E && dm[e] == 0.0f;
+                const unsigned long long m = __ballot(und);
+                if (und) cflow[el * E + cnt + __popcll(m & ((1ull << tid) - 1ull))] = fl[e];
+                cnt += __popcll(m);
+            }
+            if (tid == 0) nund[el] = cnt;
+        }
+        __syncthreads();
+        for (int t = tid; t < EPW * 24; t += L) {
+            const int el = t / 24, q = (t / 8) % 3, jj = t % 8, gb = env0 + el;
+            if (gb >= B) continue;
+            const int n = q == 2 ? nund[el] : E;
+            if (n < 8) continue;
+            const float* go = s.goal + (size_t)gb * E;
+            const float* dm = s.damaged + (size_t)gb * E;
+            const float* cf = cflow + el * E;
+            auto a = [&](int i) { return q == 0 ? __fmul_rn(go[i], dm[i]) : (q == 1 ? go[i] : cf[i]); };
+            float r = a(jj);
+            for (int i = 8; i < n - (n % 8); i += 8) r = __fadd_rn(r, a(i + jj));
+            part[t] = r;
+        }
+        __syncthreads();
+        for (int t = tid; t < EPW * 4; t += L) {
+            const int el = t / 4, q = t % 4, gb = env0 + el;
+            if (gb >= B) continue;
+            float res = 0.0f;
+            if (q == 3) {
+                for (int v = 0; v < N; ++v) res = fmaxf(res, bwv[el * N + v]);
+            } else {
+                const int n = q == 2 ? nund[el] : E;
+                const float* go = s.goal + (size_t)gb * E;
+                const float* dm = s.damaged + (size_t)gb * E;
+                const float* cf = cflow + el * E;
+                auto a = [&](int i) { return q == 0 ? __fmul_rn(go[i], dm[i]) : (q == 1 ? go[i] : cf[i]); };
+                int i = 0;
+                if (n >= 8) {
+                    const float* r = part + el * 24 + q * 8;
+                    res = __fadd_rn(__fadd_rn(__fadd_rn(r[0], r[1]), __fadd_rn(r[2], r[3])),
+                                    __fadd_rn(__fadd_rn(r[4], r[5]), __fadd_rn(r[6], r[7])));
+                    i = n - (n % 8);
+                }
+                for (; i < n; ++i) res = __fadd_rn(res, a(i));
+            }
+            sums[t] = res;
+        }
+        __syncthreads();
+        if (tid < EPW && env0 + tid < B) {
+            const float* sm = sums + tid * 4;
+            obs_env_scalars(g, s, env0 + tid, sm[0], sm[1], sm[2], nund[tid], sc + tid * 3);
+        }
+        __syncthreads();
+        for (int i = tid; i < EPW * N; i += L) {
+            const int el = i / N, v = i - el * N, gb = env0 + el;
+            if (gb < B) obs_node_features(N, gb, v, bwv[i], sums[el * 4 + 3], sc + el * 3, node_x);
+        }
     }
     for (int i = tid; i < EPW * E; i += L) {
         int el = i / E, e = i - el * E, gb = env0 + el;
@@ -173,13 +251,10 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
 }
 
 static size_t observe_smem(const DevGraph& g, int epw) {
-    size_t n = (size_t)g.N * kObsThreads;
-    size_t b = n * 8 * 2 + n * 2 + ((n + 15) & ~size_t(15));
-    b += (size_t)epw * g.E * 4;
-    b += (((size_t)epw * g.N + 15) & ~size_t(15)) + 16 * 4;
-    b += (size_t)epw * g.E * 4 * 2;  // goal / flow staged for the per-env features
-    b += ((size_t)2 * (g.N + 1) + 4 * (size_t)g.E + g.N) * 2 + 16;  // int16 adjacency
-    // the feature scratch reuses delta: needs epw*(E+8) floats <= N*L doubles
+    size_t b = (((size_t)g.N * kObsThreads * 12 + 2 * (size_t)epw * g.E + (size_t)epw * g.N + 15) & ~size_t(15));
+    b += 16 * 4 + ((size_t)3 * g.N + 2) * 2;
+    // bwv reuses sigma (epw*N floats <= N*L u16) and the feature scratch reuses
+    // delta (epw*(E+8) floats <= N*L doubles), both checked at launch
     return b;
 }
 
@@ -187,8 +262,10 @@ hipError_t launch_observe_kernel(const DevGraph& g, int B, const trx_state& s, f
                                  float* mask, hipStream_t stream) {
     int epw = kObsThreads / g.N;
     if (epw < 1) return hipErrorInvalidValue;
-    if ((size_t)epw * (g.E + 8) > (size_t)g.N * kObsThreads * 2) return hipErrorInvalidValue;
-    if (epw * g.N > 2 * kObsThreads) return hipErrorInvalidValue;  // bw_local holds 2 entries per thread
+    // feature scratch in delta: epw*(E+8) floats (E > 128) or epw*(E+32)+epw floats (E <= 128)
+    if ((size_t)epw * (g.E + 33) > (size_t)g.N * kObsThreads * 2) return hipErrorInvalidValue;
+    // bw0 / bw1 hold 2 entries per thread; i8 CSR heads / tails; the u16 sigma bound needs N <= 32
+    if (epw * g.N > 2 * kObsThreads || g.N > kSmallMaxNodes || g.N > 127) return hipErrorInvalidValue;
     int blocks = (B + epw - 1) / epw;
     hipLaunchKernelGGL(observe_kernel, dim3(blocks), dim3(kObsThreads), observe_smem(g, epw), stream, g, s, B, epw,
                        node_x, edge_x, mask);

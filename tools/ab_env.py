@@ -1,5 +1,6 @@
 """A/B timing of the env kernel from two builds of libtrafficrl.so in one
-process each: python tools/ab_env.py <lib.so> [B] [reps] [scipy|torch]."""
+process each: python tools/ab_env.py <lib.so> [B] [reps] [scipy|torch|obs]
+("obs" times trx_observe after one step instead of the step kernel)."""
 import os
 import sys
 
@@ -15,11 +16,24 @@ from trafficrl.env import VecRepairEnv  # noqa: E402
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
 sp = sys.argv[4] if len(sys.argv) > 4 else "scipy"
-env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=True, fixed_damage_seed=42, sp_backend=sp)
+env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=True, fixed_damage_seed=42,
+                   sp_backend="scipy" if sp == "obs" else sp)
 gen = torch.Generator(device="cuda").manual_seed(0)
 acts = [(torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32) for _ in range(2)]
 flow0, cap0, dmg0 = env.flow.clone(), env.capacity.clone(), env.damaged.clone()
 ms = []
+if sp == "obs":
+    env.step(acts[0], observe=False, check=False)
+    for r in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        env.observe()
+        e.record()
+        torch.cuda.synchronize()
+        ms.append(s.elapsed_time(e))
+    ms = sorted(ms)[2:-2]
+    print(f"{os.path.basename(sys.argv[1])}: observe {sum(ms) / len(ms) * 1e3:.1f} us (B={B})")
+    sys.exit(0)
 for r in range(reps):
     env.flow.copy_(flow0); env.capacity.copy_(cap0); env.damaged.copy_(dmg0)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -31,6 +31,7 @@ for s in "$@"; do
         opprobe) step op_probe 300 python tools/op_probe.py ;;
         castprobe) step cast_probe 300 python tools/cast_probe.py ;;
         perbench) step per_bench 200 rocprofv3 --kernel-trace --stats -d gpurun_out/perb -o run --output-format csv -- python3 tools/per_bench.py 50 ;;
+        obstests) step obs_tests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_oracle_observe.py tests/test_gpu_gp.py tests/test_rewards.py tests/test_torch_sp.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
         pertests) step per_tests 300 python -u -m pytest tests/test_per_tree.py tests/test_replay_train.py -x -v --timeout 120 --timeout-method thread ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 44 --warmup 22 --no-cpu ;;
         profenv) step profenv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profenv -o run --output-format csv -- python3 bench.py --workload env --steps 44 --warmup 22 --no-cpu ;;
@@ -54,6 +55,7 @@ for s in "$@"; do
                TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         abk) step ab_quad 200 env TRX_KERNEL=quad python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 && step ab_packed 200 python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
         abt) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step abt_$n 200 python tools/ab_env.py $f 4096 20 torch || exit 1; done ;;
+        abo) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step abo_$n 200 python tools/ab_env.py $f 4096 30 obs || exit 1; done ;;
         abx) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step ab_$n 200 python tools/ab_env.py $f 4096 30 || exit 1; done ;;
         pmcab) for k in quad packed; do
                  step pmc_${k}_1 200 env TRX_KERNEL=$k rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d gpurun_out/pmc_${k}_1 -o run --output-format csv -- python3 tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 6 || exit 1
