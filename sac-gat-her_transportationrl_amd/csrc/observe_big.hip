@@ -29,9 +29,8 @@ namespace trx {
 namespace {
 
 struct SmemO {
-    uint32_t dmg;                       // [E] f32
     uint32_t optr, iptr;                // [N+1] i16
-    uint32_t odst, oeid, isrc, ieid;    // [E] i16
+    uint32_t odst, isrc;                // [E] i16: head of CSR out-slot / tail of in-slot, -1 when damaged
     uint32_t insub;                     // [N] u8
     uint32_t srcs;                      // [N] i16 active sources in networkx order
     uint32_t misc;                      // [4] i32
@@ -53,13 +52,10 @@ __host__ __device__ inline SmemO smemo_layout(int N, int E, int W) {
         off = a16(off + b);
         return r;
     };
-    o.dmg = take(E * 4);
     o.optr = take((N + 1) * 2);
     o.iptr = take((N + 1) * 2);
     o.odst = take(E * 2);
-    o.oeid = take(E * 2);
     o.isrc = take(E * 2);
-    o.ieid = take(E * 2);
     o.insub = take(N);
     o.srcs = take(N * 2);
     o.misc = take(16);
@@ -102,13 +98,10 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
     const int tid = threadIdx.x, L = blockDim.x, W = L / 64, wave = tid >> 6, lane = tid & 63;
     const int gb = blockIdx.x;
     const SmemO O = smemo_layout(N, E, W);
-    float* dmg = (float*)(smem_raw + O.dmg);
     int16_t* optr = (int16_t*)(smem_raw + O.optr);
     int16_t* iptr = (int16_t*)(smem_raw + O.iptr);
     int16_t* odst = (int16_t*)(smem_raw + O.odst);
-    int16_t* oeid = (int16_t*)(smem_raw + O.oeid);
     int16_t* isrc = (int16_t*)(smem_raw + O.isrc);
-    int16_t* ieid = (int16_t*)(smem_raw + O.ieid);
     uint8_t* insub = smem_raw + O.insub;
     int16_t* srcs = (int16_t*)(smem_raw + O.srcs);
     int* misc = (int*)(smem_raw + O.misc);
@@ -124,12 +117,12 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
     int16_t* lvl = (int16_t*)(smem_raw + O.lvl) + (size_t)wave * (N + 1);
     int* claim = (int*)(smem_raw + O.claim) + (size_t)wave * N;
 
-    for (int e = tid; e < E; e += L) {
-        dmg[e] = s.damaged[(size_t)gb * E + e];
-        odst[e] = (int16_t)g.out_dst[e];
-        oeid[e] = (int16_t)g.out_eid[e];
-        isrc[e] = (int16_t)g.in_src[e];
-        ieid[e] = (int16_t)g.in_eid[e];
+    // damaged links folded into the CSR slot tables: every adjacency step below
+    // is one LDS read instead of two dependent ones
+    const float* dm = s.damaged + (size_t)gb * E;
+    for (int k = tid; k < E; k += L) {
+        odst[k] = dm[g.out_eid[k]] == 0.0f ? (int16_t)g.out_dst[k] : (int16_t)-1;
+        isrc[k] = dm[g.in_eid[k]] == 0.0f ? (int16_t)g.in_src[k] : (int16_t)-1;
     }
     for (int v = tid; v <= N; v += L) {
         optr[v] = (int16_t)g.out_ptr[v];
@@ -140,8 +133,8 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
     // edge_subgraph(active): nodes incident to an active link
     for (int v = tid; v < N; v += L) {
         int in = 0;
-        for (int k = optr[v]; k < optr[v + 1] && !in; ++k) in = dmg[oeid[k]] == 0.0f;
-        for (int k = iptr[v]; k < iptr[v + 1] && !in; ++k) in = dmg[ieid[k]] == 0.0f;
+        for (int k = optr[v]; k < optr[v + 1] && !in; ++k) in = odst[k] >= 0;
+        for (int k = iptr[v]; k < iptr[v + 1] && !in; ++k) in = isrc[k] >= 0;
         insub[v] = (uint8_t)in;
     }
     __syncthreads();
@@ -180,10 +173,9 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
                     const int i = base + lane;
                     if (i < le) {
                         const int v = queue[i], k0 = optr[v];
-                        for (int k = k0; k < optr[v + 1]; ++k) {
-                            if (dmg[oeid[k]] != 0.0f) continue;
+                        for (int k = k0, k1 = optr[v + 1]; k < k1; ++k) {
                             const int w = odst[k];
-                            if (dist[w] < 0) atomicMin(&claim[w], i * 64 + (k - k0));
+                            if (w >= 0 && dist[w] < 0) atomicMin(&claim[w], i * 64 + (k - k0));
                         }
                     }
                 }
@@ -196,14 +188,18 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
                         v = queue[i];
                         k0 = optr[v];
                         k1 = optr[v + 1];
-                        for (int k = k0; k < k1; ++k)
-                            if (dmg[oeid[k]] == 0.0f && claim[odst[k]] == i * 64 + (k - k0)) ++c;
+                        for (int k = k0; k < k1; ++k) {
+                            const int w = odst[k];
+                            if (w >= 0 && claim[w] == i * 64 + (k - k0)) ++c;
+                        }
                     }
                     int tot;
                     int pos = le + added + wave_excl_scan(c, lane, tot);
                     if (i < le)
-                        for (int k = k0; k < k1; ++k)
-                            if (dmg[oeid[k]] == 0.0f && claim[odst[k]] == i * 64 + (k - k0)) queue[pos++] = odst[k];
+                        for (int k = k0; k < k1; ++k) {
+                            const int w = odst[k];
+                            if (w >= 0 && claim[w] == i * 64 + (k - k0)) queue[pos++] = (int16_t)w;
+                        }
                     added += tot;
                 }
                 wsync();
@@ -216,10 +212,9 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
                 for (int q = le + lane; q < le + added; q += 64) {  // sigma[w] = sum of parents' sigma (exact)
                     const int w = queue[q];
                     double sg = 0.0;
-                    for (int k = iptr[w]; k < iptr[w + 1]; ++k) {
-                        if (dmg[ieid[k]] != 0.0f) continue;
+                    for (int k = iptr[w], k1 = iptr[w + 1]; k < k1; ++k) {
                         const int v = isrc[k];
-                        if (dist[v] == lev) sg += sigma[v];
+                        if (v >= 0 && dist[v] == lev) sg += sigma[v];
                     }
                     sigma[w] = sg;
                 }
@@ -240,10 +235,9 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
                     int prev = INT_MAX;
                     for (;;) {  // children in reverse queue order (networkx's stack pops)
                         int bp = -1, bwn = -1;
-                        for (int k = optr[v]; k < optr[v + 1]; ++k) {
-                            if (dmg[oeid[k]] != 0.0f) continue;
+                        for (int k = optr[v], k1 = optr[v + 1]; k < k1; ++k) {
                             const int w = odst[k];
-                            if (dist[w] != lv + 1) continue;
+                            if (w < 0 || dist[w] != lv + 1) continue;
                             const int p = claim[w];
                             if (p < prev && p > bp) {
                                 bp = p;
@@ -286,12 +280,17 @@ __global__ void __launch_bounds__(512) observe_big_kernel(const DevGraph g, cons
     for (int e = tid; e < E; e += L) obs_edge_features(g, s, gb, e, edge_x, mask);
 }
 
+// waves per workgroup (one source per wave): the most resident waves per CU
+// under the 160 KB LDS, ties to the wider workgroup (fewer source rounds per env)
 static int observe_big_waves(const DevGraph& g) {
-    for (int w : {8, 4, 2, 1})
-        if (smemo_layout(g.N, g.E, w).total <= 80 * 1024) return w;  // two workgroups per CU
-    for (int w : {4, 2, 1})
-        if (smemo_layout(g.N, g.E, w).total <= 160 * 1024) return w;
-    return 0;
+    int best = 0, best_res = 0;
+    for (int w = 1; w <= 8; ++w) {
+        const uint32_t t = smemo_layout(g.N, g.E, w).total;
+        if (t > 160u * 1024u) break;
+        const int res = w * (int)((160u * 1024u) / t);
+        if (res >= best_res) best = w, best_res = res;
+    }
+    return best;
 }
 
 hipError_t launch_observe_big(const DevGraph& g, int B, const trx_state& s, float* node_x, float* edge_x, float* mask,
