@@ -1,0 +1,644 @@
+// assign_sparse.hip -- fused batched static traffic assignment, gfx950, v4
+// ("sparse-relaxation" kernel).  Same contract and the same exact-label
+// packed keys as assign_packed.hip (src/env/repair_env.py:167-205 reset,
+// 207-237 step, 299-345 assignment, scipy branch of _all_or_nothing 481-503 +
+// 707-722, compute_tstt 724-735); the Dijkstra is reorganised around where
+// the packed kernel spent its VALU issue:
+//
+//  * the keys (bits(label) | node id, scanned = sign bit) live in LDS, one
+//    [NP] u64 row per shortest-path tree.  Each step the tree's quad reads
+//    the row (NP/4 keys per lane, ds_read_b128), takes the (label, id)
+//    minimum and relaxes ONLY the extracted node's out-links: lane j of the
+//    quad takes out-link slots j, j+4, .. of u from a per-env sparse cost
+//    table [NP][DS] and applies a signed 64-bit LDS atomic min (scanned keys
+//    are negative: never improved; scipy's strict `>`: an equal key is the
+//    same key).  The packed kernel relaxed all NP/4 slots of every lane
+//    against a dense [NP][NP] cost matrix (~3 of 24 entries finite).
+//  * predecessors come from the atomic's returned old key: a strict
+//    improvement makes u the predecessor (scipy's `>`).  Labels are exact
+//    sums, so an EQUAL returned key means v already holds this label from the
+//    tail pl[v]; scipy scans that tail first unless both tails have the same
+//    label -- then its heap order, which our (label, id) order does not
+//    follow, decides, and the tree is replayed with the exact Fibonacci heap
+//    (device_common.h exact_sssp).  This replaces the packed kernel's
+//    tie-candidate link pairs (their per-iteration masks, one barrier).
+//  * predecessors are stored as tail node ids (no parallel links), so the
+//    link-load gather compares pred(v) with src(e); the subtree-sum rows,
+//    the replay heap and the link-position scratch alias the key rows.
+// Barriers per MSA/FW iteration: 2 (trees | gather + flow update + BPR +
+// cost table).  Exactness preconditions: packed_ok() plus out/in-degree <= 16.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "device_common.h"
+#include "trx_internal.h"
+
+#ifdef TRX_PHASE_STAMPS
+// Diagnostic build only (make stamps): per-phase cycle totals of thread 0 of
+// each workgroup.  Never compiled into the shipped library.
+__device__ unsigned long long trx_phase_cycles_s[8];
+#define TRX_SSTAMP(slot)                                                    \
+    do {                                                                    \
+        if (threadIdx.x == 0) {                                             \
+            unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
+            atomicAdd(&trx_phase_cycles_s[slot], now_ - stamp_prev_);        \
+            stamp_prev_ = now_;                                             \
+        }                                                                   \
+    } while (0)
+extern "C" int trx_debug_phase_cycles_s(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_phase_cycles_s), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -2;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(trx_phase_cycles_s), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#else
+#define TRX_SSTAMP(slot) \
+    do {                 \
+    } while (0)
+#endif
+
+#ifndef TRX_SPARSE_WAVES
+#define TRX_SPARSE_WAVES 6  // waves/SIMD the register budget targets (LDS allows 6 at EPW = 2)
+#endif
+
+namespace trx {
+
+namespace {
+
+constexpr int kQs = 4;
+constexpr uint64_t kInfKeyS = 0x7FF0000000000000ull;  // bits(+inf): unreached
+constexpr uint64_t kLabelMask = 0x7FFFFFFFFFFFFFE0ull;  // strip scanned bit and node id
+constexpr uint32_t kSignS = 0x80000000u;
+constexpr int kMaxDeg = 16;   // out-degree (out-slot rounds of 4: 1, 2, 4)
+constexpr int kInSlots = 8;   // in-slots per node: one 16-byte LDS row of u16 entries
+
+struct SmemS {
+    uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [EPW*E] f32 (dprev: CFW only)
+    uint32_t ocost;  // [EPW][NP][DS] f32 cost of out-link slot s of u (+inf: none)
+    uint32_t ov;     // [NP][DS] u8 head node of out-link slot s of u (empty: u itself)
+    uint32_t keys;   // [rows][NP] u64 keys per tree; aliased: subtree sums (f32, first NP of each row),
+                     // per-wave replay heap, link-position scratch at start-up
+    uint32_t pred;   // [EPW*Z][NP] u8 predecessor node per tree (0xFF: none)
+    uint32_t ord;    // [EPW*Z][NP] u8 scan order per tree
+    uint32_t iadj;   // [NP][8] u16 in-links of v: tail | link id << 5 (empty: v itself, link 0)
+    uint32_t dem;    // [Z*N] f32
+    uint32_t t0;     // [E] f32
+    uint32_t lsrc;   // [E] u8 tail node of each link
+    uint32_t ldst;   // [E] u8 head node of each link
+    uint32_t unas;   // [EPW] f32
+    uint32_t act;    // [EPW] i32
+    uint32_t red;    // [EPW*2] f64
+    uint32_t total;
+};
+
+__host__ __device__ inline uint32_t al16s(uint32_t x) { return (x + 15u) & ~15u; }
+
+__host__ __device__ inline SmemS smems_layout(int E, int N, int Z, int NP, int EPW, int L, int DS,
+                                             bool cfw) {
+    SmemS o{};
+    uint32_t off = 0;
+    auto take = [&off](uint32_t bytes) {
+        uint32_t r = off;
+        off = al16s(off + bytes);
+        return r;
+    };
+    const uint32_t el = (uint32_t)(EPW * E * 4);
+    const int rows = ((L + 63) / 64) * 16;  // 16 trees per wave: every wave's heap lies in its own rows
+    o.flow = take(el);
+    o.cap = take(el);
+    o.dmg = take(el);
+    o.goal = take(el);
+    o.t = take(el);
+    o.aux = take(el);
+    o.dprev = take(cfw ? el : 0u);
+    o.ocost = take((uint32_t)(EPW * NP * DS * 4));
+    o.ov = take((uint32_t)(NP * DS));
+    o.keys = take((uint32_t)(rows * NP * 8));
+    o.pred = take((uint32_t)(EPW * Z * NP));
+    o.ord = take((uint32_t)(EPW * Z * NP));
+    o.iadj = take((uint32_t)(NP * kInSlots * 2));
+    o.dem = take((uint32_t)(Z * N * 4));
+    o.t0 = take((uint32_t)(E * 4));
+    o.lsrc = take((uint32_t)E);
+    o.ldst = take((uint32_t)E);
+    o.unas = take((uint32_t)(EPW * 4));
+    o.act = take((uint32_t)(EPW * 4));
+    o.red = take((uint32_t)(EPW * 2 * 8));
+    o.total = off;
+    return o;
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t qps(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t qps64(uint64_t x) {
+    return ((uint64_t)qps<CTRL>((uint32_t)(x >> 32)) << 32) | qps<CTRL>((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t dbits_s(double d) { return (uint64_t)__double_as_longlong(d); }
+__device__ __forceinline__ double bitsd_s(uint64_t b) { return __longlong_as_double((long long)b); }
+
+__device__ __forceinline__ void wave_sync_s() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The lane's NPL consecutive keys of a tree row (16-byte LDS reads).
+template <int NPL>
+__device__ __forceinline__ void read_keys(const uint64_t* row, uint64_t (&m)[NPL]) {
+    const uint4* r4 = reinterpret_cast<const uint4*>(row);
+#pragma unroll
+    for (int q = 0; q < NPL / 2; ++q) {
+        const uint4 w = r4[q];
+        m[2 * q] = ((uint64_t)w.y << 32) | w.x;
+        m[2 * q + 1] = ((uint64_t)w.w << 32) | w.z;
+    }
+}
+
+// The exact scipy-heap replay of one ambiguous tree (rare: out of line so the
+// Dijkstra loop's registers are not sized for it); writes scan order and preds.
+template <int NP>
+__device__ __noinline__ void replay_tree_s(int N, const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                                           const int16_t* __restrict__ eid_of, const float* stl, int origin, FibLane* h,
+                                           uint8_t* ol, uint8_t* pl) {
+    exact_sssp(N, indptr, indices, [stl, eid_of](int a_, int b_) { return stl[eid_of[a_ * NP + b_]]; }, origin, h, ol,
+               pl, 1, 0);
+}
+
+// out-slot rounds of 4 (the kernel is instantiated for 1, 2 and 4)
+int sparse_rounds(const DevGraph& g) {
+    const int r = (g.max_out_deg + kQs - 1) / kQs;
+    return r <= 1 ? 1 : (r == 2 ? 2 : 4);
+}
+
+}  // namespace
+
+bool sparse_ok(const DevGraph& g, const trx_params& p) {
+    return packed_ok(g, p) && g.max_out_deg <= kMaxDeg && g.max_in_deg <= kInSlots && g.NP % 8 == 0;
+}
+
+template <int NP, int R>  // R = out-slot rounds per extracted node (DS = 4R slots)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRX_SPARSE_WAVES)))
+env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int EPW, int mode,
+             const int32_t* __restrict__ action, double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
+             uint8_t* __restrict__ valid_out, const uint8_t* __restrict__ env_mask) {
+    constexpr int NPL = NP / kQs;
+    constexpr int DS = R * kQs;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    const int E = g.E, N = g.N, Z = g.Z;
+    const int L = blockDim.x;
+    const int tid = threadIdx.x;
+    const int EL = EPW * E;
+    const int env0 = blockIdx.x * EPW;
+    const bool cfw = p.method == TRX_METHOD_CFW;
+    const SmemS O = smems_layout(E, N, Z, NP, EPW, L, DS, cfw);
+    float* const sflow = (float*)(smem_raw + O.flow);
+    float* const scap = (float*)(smem_raw + O.cap);
+    float* const sdmg = (float*)(smem_raw + O.dmg);
+    float* const sgoal = (float*)(smem_raw + O.goal);
+    float* const st = (float*)(smem_raw + O.t);
+    float* const saux = (float*)(smem_raw + O.aux);
+    float* const sdprev = (float*)(smem_raw + O.dprev);
+    float* const socost = (float*)(smem_raw + O.ocost);
+    uint8_t* const sov = smem_raw + O.ov;
+    uint64_t* const skeys = (uint64_t*)(smem_raw + O.keys);
+    uint8_t* const spred = smem_raw + O.pred;
+    uint8_t* const sord = smem_raw + O.ord;
+    uint16_t* const siadj = (uint16_t*)(smem_raw + O.iadj);
+    float* const sdem = (float*)(smem_raw + O.dem);
+    float* const st0 = (float*)(smem_raw + O.t0);
+    uint8_t* const slsrc = smem_raw + O.lsrc;
+    uint8_t* const sldst = smem_raw + O.ldst;
+    float* const sunas = (float*)(smem_raw + O.unas);
+    int* const sact = (int*)(smem_raw + O.act);
+    double* const sred = (double*)(smem_raw + O.red);
+    const int NDS = NP * DS;
+#ifdef TRX_PHASE_STAMPS
+    unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
+
+    // ------------------------------------------------ per-env activation
+    if (tid < EPW) {
+        const int gb = env0 + tid;
+        int active = 0;
+        if (gb < B) {
+            if (mode == kModeStep) {
+                const int a = action[gb];
+                // out-of-range ids (check=False) are memory-safe no-ops, like an
+                // already-repaired link (repair_env.py:208-212)
+                active = (unsigned)a < (unsigned)E && s.damaged[(size_t)gb * E + a] != 0.0f;
+                if (!active) {
+                    reward_out[gb] = -1.0;
+                    done_out[gb] = 0;
+                    valid_out[gb] = 0;
+                }
+            } else {
+                active = env_mask ? (env_mask[gb] != 0) : 1;
+            }
+        }
+        sact[tid] = active;
+        sunas[tid] = 0.0f;
+    }
+    // static tables: sparse out-adjacency (scipy CSR order), in-adjacency
+    int16_t* const opos_tmp = reinterpret_cast<int16_t*>(skeys);  // [E] scratch in the key rows
+    // padding entries are harmless no-ops, so the loops below need no validity
+    // tests: an empty out-slot of u targets u itself (scanned before its
+    // relaxation: never improved) at cost +inf; an empty in-slot of v names v
+    // itself as tail over link 0 (label(v) + cost > label(v): never achieving)
+    for (int i = tid; i < NDS; i += L) sov[i] = (uint8_t)(i / DS);
+    for (int i = tid; i < NP * kInSlots; i += L) siadj[i] = (uint16_t)(i / kInSlots);
+    for (int i = tid; i < EPW * NDS; i += L) socost[i] = kInfF;
+    for (int i = tid; i < Z * N; i += L) sdem[i] = g.dem[i];
+    for (int i = tid; i < E; i += L) {
+        st0[i] = g.t0[i];
+        slsrc[i] = (uint8_t)g.src[i];
+        sldst[i] = (uint8_t)g.dst[i];
+    }
+    __syncthreads();
+    for (int u = tid; u < N; u += L) {
+        const int a0 = g.indptr[u], a1 = g.indptr[u + 1];
+        for (int a = a0; a < a1; ++a) {
+            sov[u * DS + (a - a0)] = (uint8_t)g.indices[a];
+            opos_tmp[g.csr_eid[a]] = (int16_t)(u * DS + (a - a0));
+        }
+        const int b0 = g.in_ptr[u], b1 = g.in_ptr[u + 1];
+        for (int b = b0; b < b1; ++b) siadj[u * kInSlots + (b - b0)] = (uint16_t)(g.in_src[b] | (g.in_eid[b] << 5));
+    }
+    __syncthreads();
+    const bool opos_reg = EL <= L;  // one (env, link) per thread: its cost-table slot in a register
+    int my_opos = -1;
+    if (opos_reg && tid < EL) {
+        const int el = tid / E, e = tid - el * E;
+        my_opos = el * NDS + opos_tmp[e];
+    }
+    __syncthreads();  // the scratch is overwritten by the key rows below
+
+    // ------------------------------------------------------- load state
+    for (int i = tid; i < EL; i += L) {
+        const int el = i / E, e = i - el * E;
+        const int gb = env0 + el;
+        float fl = 0.f, cp = 0.f, dm = 0.f, gl = 0.f;
+        if (sact[el]) {
+            const size_t gi = (size_t)gb * E + e;
+            if (mode == kModeReset) {
+                dm = s.damaged[gi];  // repair_env.py:193-198
+                cp = dm != 0.0f ? p.capacity_damage : g.cap0[e];
+                gl = dm;
+            } else {
+                fl = s.flow[gi];
+                cp = s.capacity[gi];
+                dm = s.damaged[gi];
+                gl = s.goal[gi];
+                if (mode == kModeStep && e == action[gb]) {  // repair_env.py:215-216
+                    dm = 0.0f;
+                    cp = g.cap0[e];
+                }
+            }
+        }
+        sflow[i] = fl;
+        scap[i] = cp;
+        sdmg[i] = dm;
+        sgoal[i] = gl;
+        saux[i] = 0.0f;
+        if (cfw) sdprev[i] = 0.0f;
+        const float tv = sact[el] ? bpr_cost(fl, cp, st0[e], dm, p.bpr_alpha, p.bpr_beta) : 0.0f;
+        st[i] = tv;
+        if (my_opos >= 0) socost[my_opos] = tv;  // opos_reg: i == tid
+    }
+    __syncthreads();
+    if (!opos_reg) {  // generic path: cost-table entries from the static out-adjacency
+        for (int x = tid; x < EPW * NDS; x += L) {
+            const int el = x / NDS, r = x - el * NDS;
+            const int u = r / DS, v = sov[r];
+            socost[x] = v != 0xFF ? st[el * E + g.eid_of[u * NP + v]] : kInfF;
+        }
+    }
+    __syncthreads();
+
+    // thread -> (tree = (env, origin zone), lane j of its quad)
+    const int tree = tid / kQs;
+    const int j = tid & (kQs - 1);
+    const int lenv = tree / Z;
+    const int zi = tree - lenv * Z;
+    const bool tree_on = (lenv < EPW) && sact[lenv];
+    const int origin = tree_on ? g.origins[zi] : 0;
+    float unassigned_lane = 0.0f;
+    TRX_SSTAMP(0);
+
+    for (int it = 0; it < p.iters; ++it) {
+        // ---------------- shortest-path tree per quad (Dijkstra, sparse relaxation)
+        if (tree_on) {
+            uint64_t* const kt = skeys + tree * NP;
+            uint32_t* const kt32 = reinterpret_cast<uint32_t*>(kt);
+            const float* const oc = socost + lenv * NDS;
+            uint8_t* const ol = sord + tree * NP;
+            uint8_t* const pl = spred + tree * NP;
+            int jo = j;
+            asm volatile("" : "+v"(jo));  // keep the key set-up inside the loop (no hoist + spill)
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int v = NPL * jo + i;
+                kt[NPL * j + i] = v >= N ? ~0ull : (v == origin ? (uint64_t)v : (kInfKeyS | (uint64_t)v));
+                pl[NPL * j + i] = kNoPred;
+            }
+            wave_sync_s();
+            int nscan = 0;
+            int amb = 0;
+            uint64_t m[NPL];
+            read_keys<NPL>(kt + NPL * j, m);
+            for (int k = 0; k < N; ++k) {
+                // argmin over the lane's keys (pairwise), then over the quad (DPP)
+#pragma unroll
+                for (int w = 1; w < NPL; w *= 2)
+#pragma unroll
+                    for (int i = 0; i + w < NPL; i += 2 * w) m[i] = m[i + w] < m[i] ? m[i + w] : m[i];
+                uint64_t best = m[0];
+                uint64_t o = qps64<0xB1>(best);
+                best = o < best ? o : best;
+                o = qps64<0x4E>(best);
+                best = o < best ? o : best;
+                if (best >= kInfKeyS) break;  // quad-uniform: the rest is unreachable
+                const uint32_t u = (uint32_t)best & 31u;
+                // the quad's 4 lanes store the same values: scan order, scanned bit
+                ol[k] = (uint8_t)u;
+                kt32[2 * u + 1] = (uint32_t)(best >> 32) | kSignS;
+                nscan = k + 1;
+                const uint64_t lb = best & ~31ull;
+                const double bl = bitsd_s(lb);
+                uint32_t v[R];
+                float c[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {  // all reads in flight before the first use
+                    const int sl = (int)u * (R * kQs) + r * kQs + j;
+                    v[r] = sov[sl];
+                    c[r] = oc[sl];
+                }
+                long long nk[R], was[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {  // the atomics back to back
+                    nk[r] = (long long)(dbits_s(__dadd_rn(bl, (double)c[r])) | v[r]);
+                    was[r] = __hip_atomic_fetch_min(reinterpret_cast<long long*>(kt + v[r]), nk[r], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                // next step's keys: issued behind the mark and the atomics (a wave's LDS
+                // operations complete in order), before waiting on the atomics' results
+                read_keys<NPL>(kt + NPL * j, m);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    // scipy's strict improvement: u becomes v's predecessor.  An equal key
+                    // means v already holds this label from the tail pl[v]; scipy's order
+                    // between the two is its heap's iff the tails' labels are equal.
+                    if (nk[r] < was[r]) pl[v[r]] = (uint8_t)u;
+                    if (nk[r] == was[r]) amb |= (kt[pl[v[r]]] & kLabelMask) == lb;
+                }
+            }
+            wave_sync_s();
+            TRX_SSTAMP(1);
+            amb |= (int)qps<0xB1>((uint32_t)amb);
+            amb |= (int)qps<0x4E>((uint32_t)amb);
+            const uint64_t need = __ballot(amb != 0 && j == 0);
+            wave_sync_s();
+            TRX_SSTAMP(2);
+            if (need) {  // wave-uniform, rare: exact scipy-heap replays, one tree at a time
+                const float* const stl = st + lenv * E;
+                FibLane* const h = reinterpret_cast<FibLane*>(smem_raw + O.keys + (uint32_t)((tid >> 6) * 16 * NP * 8));
+                uint64_t pending = need;
+                while (pending) {
+                    const int leader = __ffsll((unsigned long long)pending) - 1;
+                    if ((tid & 63) == leader) replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
+                    pending &= pending - 1;
+                }
+                wave_sync_s();
+            }
+            // ---------------- all-or-nothing (repair_env.py:490-502, 707-722), part 1:
+            // subtree demand sums S(v) per tree in reverse scan order (one lane per
+            // tree, plain LDS read-modify-write); integral demands: exact in any order.
+            const float* dm = sdem + zi * N;
+            float* const sa = reinterpret_cast<float*>(kt);
+            float un = 0.0f;
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int v = NPL * j + i;
+                const float dv = v < N ? dm[v] : 0.0f;
+                const bool load = v < N && pl[v] != kNoPred;  // reached, not the origin
+                un += (dv > 0.0f && !load) ? dv : 0.0f;      // intrazonal or unreachable (708)
+                sa[v] = load ? dv : 0.0f;
+            }
+            wave_sync_s();
+            if (j == 0) {
+                uint32_t ow[NP / 4];  // the scan order in registers
+#pragma unroll
+                for (int q = 0; q < NP / 4; ++q) ow[q] = reinterpret_cast<const uint32_t*>(ol)[q];
+                uint32_t pw[NP / 4];  // and the predecessor of each scanned node
+#pragma unroll
+                for (int q = 0; q < NP / 4; ++q) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+                        w |= (4 * q + b < nscan ? (uint32_t)pl[(ow[q] >> (8 * b)) & 0xFF] : 0u) << (8 * b);
+                    pw[q] = w;
+                }
+#pragma unroll
+                for (int k = NP - 1; k >= 1; --k) {
+                    if (k < nscan) {  // quad-uniform
+                        const int v = (ow[k >> 2] >> (8 * (k & 3))) & 0xFF;
+                        const int pv = (pw[k >> 2] >> (8 * (k & 3))) & 0xFF;
+                        sa[pv] = sa[pv] + sa[v];
+                    }
+                }
+            }
+            unassigned_lane = un;
+            TRX_SSTAMP(3);
+        }
+        __syncthreads();
+        TRX_SSTAMP(4);
+
+        // ---------------- all-or-nothing, part 2 + flow update + BPR + next cost
+        // table (repair_env.py:317-342): link load of e = the sum over the env's
+        // trees whose predecessor of dst(e) is src(e) of S(dst(e))
+        const double stepd = (p.method == TRX_METHOD_MSA) ? 1.0 / (it + 1.0) : 2.0 / (it + 2.0);
+        const float s32 = (float)stepd, om32 = (float)(1.0 - stepd);
+        if (cfw) {
+            for (int i = tid; i < EL; i += L) {
+                const int el = i / E, e = i - el * E;
+                if (!sact[el]) continue;
+                const int v = sldst[e];
+                const uint32_t u = slsrc[e];
+                float ax = 0.0f;
+                for (int z = 0; z < Z; ++z) {
+                    const int tr = el * Z + z;
+                    ax += spred[tr * NP + v] == u ? reinterpret_cast<const float*>(skeys + tr * NP)[v] : 0.0f;
+                }
+                saux[i] = ax;
+            }
+            __syncthreads();
+            if (tid < EPW && sact[tid]) {
+                double num = 0.0, den = 0.0;
+                const float* fl = sflow + tid * E;
+                const float* ax = saux + tid * E;
+                const float* dp = sdprev + tid * E;
+                for (int e = 0; e < E; ++e) {
+                    const float dfw = __fsub_rn(ax[e], fl[e]);
+                    num += (double)__fmul_rn(dfw, __fsub_rn(dfw, dp[e]));
+                    den += (double)__fmul_rn(dp[e], dp[e]);
+                }
+                sred[2 * tid] = num;
+                sred[2 * tid + 1] = den;
+            }
+            __syncthreads();
+        }
+        for (int i = tid; i < EL; i += L) {
+            const int el = i / E, e = i - el * E;
+            if (!sact[el]) continue;
+            const float fl = sflow[i];
+            float ax;
+            if (cfw) {
+                ax = saux[i];
+            } else {
+                const int v = sldst[e];
+                const uint32_t u = slsrc[e];
+                ax = 0.0f;
+                for (int z = 0; z < Z; ++z) {
+                    const int tr = el * Z + z;
+                    ax += spred[tr * NP + v] == u ? reinterpret_cast<const float*>(skeys + tr * NP)[v] : 0.0f;
+                }
+            }
+            float nf;
+            if (cfw) {
+                const float dfw = __fsub_rn(ax, fl);
+                float dir;
+                if (it == 0) {
+                    dir = dfw;
+                } else {
+                    const float num = (float)sred[2 * el];
+                    const double den = (double)(float)sred[2 * el + 1] + 1e-12;
+                    double b = (double)num / den;
+                    b = b < 0.0 ? 0.0 : b;
+                    dir = __fadd_rn(dfw, __fmul_rn((float)b, sdprev[i]));
+                }
+                nf = __fadd_rn(fl, __fmul_rn(s32, dir));
+                nf = nf > 0.0f ? nf : 0.0f;
+                sdprev[i] = dir;
+            } else {
+                nf = __fadd_rn(__fmul_rn(om32, fl), __fmul_rn(s32, ax));
+            }
+            if (nf != nf) nf = 0.0f;  // nan_to_num guard (repair_env.py:338-340)
+            sflow[i] = nf;
+            const float tv = bpr_cost(nf, scap[i], st0[e], sdmg[i], p.bpr_alpha, p.bpr_beta);
+            st[i] = tv;
+            if (my_opos >= 0) socost[my_opos] = tv;
+        }
+        __syncthreads();
+        if (!opos_reg) {
+            for (int x = tid; x < EPW * NDS; x += L) {
+                const int el = x / NDS, r = x - el * NDS;
+                const int u = r / DS, v = sov[r];
+                if (v != 0xFF) socost[x] = st[el * E + g.eid_of[u * NP + v]];
+            }
+            __syncthreads();
+        }
+    }
+
+    TRX_SSTAMP(5);
+    // ---------------- per-env unassigned (last iteration; exact integers)
+    if (tree_on) atomicAdd(&sunas[lenv], unassigned_lane);
+    for (int i = tid; i < EL; i += L) saux[i] = __fmul_rn(sflow[i], st[i]);
+    __syncthreads();
+
+    if (tid < EPW && sact[tid]) {
+        const int gb = env0 + tid;
+        const double un = (double)sunas[tid];
+        const double base = (double)pairwise_sum(saux + tid * E, E);
+        const double td = g.total_demand > 1.0 ? g.total_demand : 1.0;
+        const double tstt = base / td + (un > 0 ? p.unassigned_penalty * (un / td) : 0.0);  // repair_env.py:724-735
+        const double prev = s.tstt[gb];
+        s.tstt[gb] = tstt;
+        s.unassigned[gb] = un;
+        if (mode == kModeReset) s.initial_tstt[gb] = tstt;
+        if (mode == kModeStep) {
+            float rem = 0.0f;
+            for (int e = 0; e < E; ++e) rem += __fmul_rn(sgoal[tid * E + e], sdmg[tid * E + e]);
+            const bool complete = rem == 0.0f;  // is_goal_complete (293-294)
+            reward_out[gb] = reward_fn(p, prev, tstt, s.initial_tstt[gb], complete);
+            done_out[gb] = complete ? 1 : 0;
+            valid_out[gb] = 1;
+        }
+    }
+    for (int i = tid; i < EL; i += L) {
+        const int el = i / E;
+        if (!sact[el]) continue;
+        const size_t gi = (size_t)(env0 + el) * E + (i - el * E);
+        s.flow[gi] = sflow[i];
+        if (s.t) s.t[gi] = st[i];
+        if (mode != kModeAssign) {
+            s.capacity[gi] = scap[i];
+            s.damaged[gi] = sdmg[i];
+            s.goal[gi] = sgoal[i];
+        }
+    }
+    TRX_SSTAMP(6);
+}
+
+LaunchCfg sparse_launch_cfg(const DevGraph& g, int num_envs, int method) {
+    LaunchCfg c{};
+    c.np = g.NP;
+    const int per_env = g.Z * kQs;
+    static const int epw_env = [] {
+        const char* e = getenv("TRX_EPW");  // tuning knob (A/B runs)
+        return e ? atoi(e) : 0;
+    }();
+    int epw = epw_env > 0 ? epw_env : 2;
+    while (epw > 1 && epw * per_env > 256) --epw;
+    c.epw = epw;
+    c.threads = ((epw * per_env + 63) / 64) * 64;
+    c.smem = smems_layout(g.E, g.N, g.Z, c.np, c.epw, c.threads, sparse_rounds(g) * kQs,
+                          method == TRX_METHOD_CFW).total;
+    c.blocks = (num_envs + c.epw - 1) / c.epw;
+    return c;
+}
+
+hipError_t launch_env_kernel_sparse(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs,
+                                    int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                                    const uint8_t* env_mask, hipStream_t stream) {
+    const LaunchCfg c = sparse_launch_cfg(g, num_envs, p.method);
+    if (c.blocks == 0) return hipSuccess;
+    if (c.threads > 256 || c.smem > 64 * 1024) return hipErrorInvalidConfiguration;
+    const int R = sparse_rounds(g);
+    const dim3 grid(c.blocks), block(c.threads);
+#define TRX_SPARSE_LAUNCH(NPV, RV)                                                                              \
+    hipLaunchKernelGGL((env_kernel_s<NPV, RV>), grid, block, c.smem, stream, g, p, s, num_envs, c.epw, mode, \
+                       action, reward, done, valid, env_mask)
+#define TRX_SPARSE_NP(NPV)             \
+    if (R == 1)                        \
+        TRX_SPARSE_LAUNCH(NPV, 1);     \
+    else if (R == 2)                   \
+        TRX_SPARSE_LAUNCH(NPV, 2);     \
+    else                               \
+        TRX_SPARSE_LAUNCH(NPV, 4)
+    switch (c.np) {
+        case 8:
+            TRX_SPARSE_NP(8);
+            break;
+        case 16:
+            TRX_SPARSE_NP(16);
+            break;
+        case 24:
+            TRX_SPARSE_NP(24);
+            break;
+        default:
+            TRX_SPARSE_NP(32);
+            break;
+    }
+#undef TRX_SPARSE_NP
+#undef TRX_SPARSE_LAUNCH
+    return hipGetLastError();
+}
+
+}  // namespace trx

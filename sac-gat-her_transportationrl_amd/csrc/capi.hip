@@ -90,15 +90,19 @@ int check_state(const trx_state* s, bool need_initial) {
     return TRX_OK;
 }
 
-// TRX_KERNEL=quad selects the previous small-graph kernels (A/B runs): env_kernel_q
-// for both shortest-path rules instead of env_kernel_p (scipy) / env_kernel_t (torch)
-bool use_packed() {
-    static const bool on = [] {
+// TRX_KERNEL selects earlier small-graph kernels for A/B runs: "quad" = env_kernel_q
+// for both shortest-path rules (instead of env_kernel_s / env_kernel_p for scipy and
+// env_kernel_t for torch), "packed" = env_kernel_p for the scipy rule.
+int kernel_choice() {  // 0 = current, 1 = packed, 2 = quad
+    static const int c = [] {
         const char* e = getenv("TRX_KERNEL");
-        return !(e && std::string(e) == "quad");
+        if (e && std::string(e) == "quad") return 2;
+        if (e && std::string(e) == "packed") return 1;
+        return 0;
     }();
-    return on;
+    return c;
 }
+bool use_packed() { return kernel_choice() != 2; }
 
 int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mode, const int32_t* action,
         double* reward, uint8_t* done, uint8_t* valid, const uint8_t* env_mask, void* ws, void* stream) {
@@ -123,6 +127,10 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
     } else if (p->sp_rule == TRX_SP_TORCH && use_packed() && trx::torch_kernel_ok(g->dg)) {
         e = trx::launch_env_kernel_torch(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
                                          static_cast<hipStream_t>(stream));
+    } else if (g->dg.N <= trx::kSmallMaxNodes && p->sp_rule == TRX_SP_SCIPY && kernel_choice() == 0 &&
+               trx::sparse_ok(g->dg, *p)) {
+        e = trx::launch_env_kernel_sparse(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
+                                          static_cast<hipStream_t>(stream));
     } else if (g->dg.N <= trx::kSmallMaxNodes && p->sp_rule == TRX_SP_SCIPY && use_packed() &&
                trx::packed_ok(g->dg, *p))
         e = trx::launch_env_kernel_packed(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
@@ -400,6 +408,11 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
                     tie_pairs.push_back(e1 | (e2 << 16));
                 }
     d.npairs = (int)tie_pairs.size();
+    d.max_out_deg = d.max_in_deg = 0;
+    for (int u = 0; u < N; ++u) {
+        d.max_out_deg = std::max(d.max_out_deg, out_ptr[u + 1] - out_ptr[u]);
+        d.max_in_deg = std::max(d.max_in_deg, in_ptr[u + 1] - in_ptr[u]);
+    }
     if (tie_pairs.empty()) tie_pairs.push_back(0u);
     int rc = TRX_OK;
     std::vector<int32_t> vsrc(src, src + E), vdst(dst, dst + E);

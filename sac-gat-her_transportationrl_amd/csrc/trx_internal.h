@@ -61,6 +61,7 @@ struct DevGraph {
     float min_t0;               // smallest free-flow time (exact-label headroom, assign_packed.hip)
     int npairs;                 // in-link pairs of a common head (tie candidates), N <= kSmallMaxNodes
     const uint32_t* tie_pairs;  // [npairs] e1 | e2 << 16, e1 < e2, dst[e1] == dst[e2]
+    int max_out_deg, max_in_deg;  // largest out-/in-degree (sparse-relaxation kernel tables)
 };
 
 // Largest tie-candidate pair list of the packed-key kernel (LDS budget).
@@ -124,6 +125,11 @@ struct LaunchCfg {
 LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs, int sp_rule);
 bool packed_ok(const DevGraph& g, const trx_params& p);
 LaunchCfg packed_launch_cfg(const DevGraph& g, int num_envs, int method);
+bool sparse_ok(const DevGraph& g, const trx_params& p);
+LaunchCfg sparse_launch_cfg(const DevGraph& g, int num_envs, int method);
+hipError_t launch_env_kernel_sparse(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs,
+                                    int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                                    const uint8_t* env_mask, hipStream_t stream);
 hipError_t launch_env_kernel_packed(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs,
                                    int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                    const uint8_t* env_mask, hipStream_t stream);

@@ -15,10 +15,13 @@ from trafficrl import _lib  # noqa: E402
 
 _lib.LIB_PATH = os.path.join(ROOT, "sac-gat-her_transportationrl_amd", "trafficrl", "libtrafficrl_stamps.so")
 L = _lib.load()
-# the packed-key kernel (assign_packed.hip) has its own counters
-PACKED = os.environ.get("TRX_KERNEL", "packed") != "quad"
-if PACKED:
+# each small-graph kernel has its own counters: sparse (default), packed, quad
+KIND = os.environ.get("TRX_KERNEL", "sparse")
+PACKED = KIND != "quad"
+if KIND == "packed":
     L.trx_debug_phase_cycles = L.trx_debug_phase_cycles_p
+elif KIND == "sparse":
+    L.trx_debug_phase_cycles = L.trx_debug_phase_cycles_s
 L.trx_debug_phase_cycles.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 from trafficrl.data import sioux_falls  # noqa: E402
 from trafficrl.env import VecRepairEnv  # noqa: E402
@@ -32,7 +35,9 @@ for _ in range(5):
     a = (torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32)
     env.step(a, observe=False)
 L.trx_debug_phase_cycles(buf, 1)
-names = (["load", "dijkstra", "tie check+replay", "aon walk", "barrier wait", "update+bpr", "tie candidates"]
+names = (["load", "dijkstra", "pred pass", "replay+subtree", "barrier wait", "gather+update+bpr", "tstt+store"]
+         if KIND == "sparse" else
+         ["load", "dijkstra", "tie check+replay", "aon walk", "barrier wait", "update+bpr", "tie candidates"]
          if PACKED else ["load", "cost build", "dijkstra", "tie check+replay", "aon", "update+bpr", "tstt+store"])
 tot = sum(buf[i] for i in range(7))
 for i, n in enumerate(names):
