@@ -29,6 +29,7 @@
 // cost table).  Exactness preconditions: packed_ok() plus out/in-degree <= 16.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 
 #include "device_common.h"
@@ -265,8 +266,10 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     for (int u = tid; u < N; u += L) {
         const int a0 = g.indptr[u], a1 = g.indptr[u + 1];
         for (int a = a0; a < a1; ++a) {
-            sov[u * DS + (a - a0)] = (uint8_t)g.indices[a];
-            opos_tmp[g.csr_eid[a]] = (int16_t)(u * DS + (a - a0));
+            // out-link k of u -> lane k % 4, round k / 4: each lane's R slots are contiguous
+            const int pos = u * DS + ((a - a0) & (kQs - 1)) * R + (a - a0) / kQs;
+            sov[pos] = (uint8_t)g.indices[a];
+            opos_tmp[g.csr_eid[a]] = (int16_t)pos;
         }
         const int b0 = g.in_ptr[u], b1 = g.in_ptr[u + 1];
         for (int b = b0; b < b1; ++b) siadj[u * kInSlots + (b - b0)] = (uint16_t)(g.in_src[b] | (g.in_eid[b] << 5));
@@ -317,7 +320,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
         for (int x = tid; x < EPW * NDS; x += L) {
             const int el = x / NDS, r = x - el * NDS;
             const int u = r / DS, v = sov[r];
-            socost[x] = v != 0xFF ? st[el * E + g.eid_of[u * NP + v]] : kInfF;
+            socost[x] = v != u ? st[el * E + g.eid_of[u * NP + v]] : kInfF;
         }
     }
     __syncthreads();
@@ -366,26 +369,47 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 best = o < best ? o : best;
                 if (best >= kInfKeyS) break;  // quad-uniform: the rest is unreachable
                 const uint32_t u = (uint32_t)best & 31u;
-                // the quad's 4 lanes store the same values: scan order, scanned bit
-                ol[k] = (uint8_t)u;
-                kt32[2 * u + 1] = (uint32_t)(best >> 32) | kSignS;
+                // one lane of the quad stores the scan order and the scanned bit
+                if (j == 0) {
+                    ol[k] = (uint8_t)u;
+                    kt32[2 * u + 1] = (uint32_t)(best >> 32) | kSignS;
+                }
                 nscan = k + 1;
                 const uint64_t lb = best & ~31ull;
                 const double bl = bitsd_s(lb);
                 uint32_t v[R];
                 float c[R];
+                {  // lane j's R slots of u: one read each for heads and costs
+                    const int sl = (int)u * DS + j * R;
+                    if constexpr (R == 1) {
+                        v[0] = sov[sl];
+                        c[0] = oc[sl];
+                    } else if constexpr (R == 2) {
+                        const uint32_t hv = *reinterpret_cast<const uint16_t*>(sov + sl);
+                        const float2 cv = *reinterpret_cast<const float2*>(oc + sl);
+                        v[0] = hv & 0xFFu;
+                        v[1] = hv >> 8;
+                        c[0] = cv.x;
+                        c[1] = cv.y;
+                    } else {
+                        const uint32_t hv = *reinterpret_cast<const uint32_t*>(sov + sl);
+                        const float4 cv = *reinterpret_cast<const float4*>(oc + sl);
 #pragma unroll
-                for (int r = 0; r < R; ++r) {  // all reads in flight before the first use
-                    const int sl = (int)u * (R * kQs) + r * kQs + j;
-                    v[r] = sov[sl];
-                    c[r] = oc[sl];
+                        for (int r = 0; r < 4; ++r) v[r] = (hv >> (8 * r)) & 0xFFu;
+                        c[0] = cv.x;
+                        c[1] = cv.y;
+                        c[2] = cv.z;
+                        c[3] = cv.w;
+                    }
                 }
                 long long nk[R], was[R];
 #pragma unroll
-                for (int r = 0; r < R; ++r) {  // the atomics back to back
+                for (int r = 0; r < R; ++r) {  // the atomics back to back; empty slots (v == u) skip theirs
                     nk[r] = (long long)(dbits_s(__dadd_rn(bl, (double)c[r])) | v[r]);
-                    was[r] = __hip_atomic_fetch_min(reinterpret_cast<long long*>(kt + v[r]), nk[r], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+                    was[r] = LLONG_MIN;
+                    if (v[r] != u)
+                        was[r] = __hip_atomic_fetch_min(reinterpret_cast<long long*>(kt + v[r]), nk[r],
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 // next step's keys: issued behind the mark and the atomics (a wave's LDS
                 // operations complete in order), before waiting on the atomics' results
@@ -540,7 +564,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             for (int x = tid; x < EPW * NDS; x += L) {
                 const int el = x / NDS, r = x - el * NDS;
                 const int u = r / DS, v = sov[r];
-                if (v != 0xFF) socost[x] = st[el * E + g.eid_of[u * NP + v]];
+                if (v != u) socost[x] = st[el * E + g.eid_of[u * NP + v]];
             }
             __syncthreads();
         }
