@@ -186,13 +186,14 @@ def measured_traffic(network):
     of this workload (profiles/r02_sf_pmc.json for Sioux Falls,
     profiles/r01_ana_pmc.json for the Anaheim-size network; separate
     FETCH_SIZE / WRITE_SIZE passes, see tools/pmc_summary.py)."""
-    name = {"sf": "r02_sf_pmc.json", "anaheim": "r01_ana_pmc.json"}[network]
+    name = {"sf": "r02_sf_sparse_pmc.json", "anaheim": "r01_ana_pmc.json"}[network]
     path = os.path.join(ROOT, "profiles", name)
     try:
         d = json.load(open(path))
-        return d.get("hbm_bytes_per_launch_raw"), os.path.relpath(path, ROOT), d.get("valu_busy_frac")
+        return (d.get("hbm_bytes_per_launch_raw"), os.path.relpath(path, ROOT), d.get("valu_busy_frac"),
+                d.get("lds_bank_conflict_frac"))
     except (OSError, ValueError):
-        return None, None, None
+        return None, None, None, None
 
 
 def env_kernel_name(big, sp):
@@ -201,8 +202,10 @@ def env_kernel_name(big, sp):
         return "trx::env_kernel_big"
     if os.environ.get("TRX_KERNEL", "") == "quad":
         return "trx::env_kernel_q<24>"     # the round-1 quad kernel (A/B runs)
+    if sp == "scipy" and os.environ.get("TRX_KERNEL", "") == "packed":
+        return "trx::env_kernel_p<24>"     # packed-key Dijkstra (assign_packed.hip, A/B runs)
     if sp == "scipy":
-        return "trx::env_kernel_p<24>"     # packed-key Dijkstra (assign_packed.hip)
+        return "trx::env_kernel_s<24, 2>"  # sparse-relaxation Dijkstra (assign_sparse.hip; SF: max out-degree 5)
     return "trx::env_kernel_t<24>"         # torch rule: per-wave Floyd-Warshall (assign_torch.hip)
 
 
@@ -381,11 +384,11 @@ def main():
     P = len(env.graph.od_o)
     bpa = bytes_per_assign(N, E, Z, P, args.iters)
     achieved = bpa * B / mean_kernel_s
-    traffic, traffic_src, valu_frac = measured_traffic(args.network)
+    traffic, traffic_src, valu_frac, lds_conf = measured_traffic(args.network)
     kname = env_kernel_name(big, args.sp)
     if (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")) or \
-            (not big and kname != "trx::env_kernel_p<24>"):
-        traffic, traffic_src, valu_frac = None, None, None  # the committed PMC passes are for the default workloads
+            (not big and kname != "trx::env_kernel_s<24, 2>"):
+        traffic, traffic_src, valu_frac, lds_conf = None, None, None, None  # committed PMC passes: default workloads
     mfma = gemm_mfma(B * N, B) if (args.workload == "train" and rank == 0) else None
     if rank == 0:
         cpu = None
@@ -427,9 +430,10 @@ def main():
                                  "(raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic else None,
                 "kernel": kname, "kernel_mean_ms": mean_kernel_s * 1e3,
                 "valu_busy_frac": valu_frac,
+                "lds_bank_conflict_frac": lds_conf,
                 "valu_note": ("SIMD VALU issue share of the same kernel from the committed PMC passes "
                               "(4 x SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs)); the kernel is issue-bound, "
-                              "not HBM-bound") if valu_frac else None,
+                              "not HBM-bound; lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS") if valu_frac else None,
                 "bytes_per_assign": bpa, "assigns_per_launch": B,
                 "mfma": mfma,
             },

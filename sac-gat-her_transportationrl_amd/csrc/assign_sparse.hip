@@ -72,9 +72,16 @@ namespace trx {
 namespace {
 
 constexpr int kQs = 4;
-constexpr uint64_t kInfKeyS = 0x7FF0000000000000ull;  // bits(+inf): unreached
-constexpr uint64_t kLabelMask = 0x7FFFFFFFFFFFFFE0ull;  // strip scanned bit and node id
-constexpr uint32_t kSignS = 0x80000000u;
+// Key encoding (64 bits, read as a double by the argmin and as a signed integer by
+// the relaxation's atomic min):
+//   reached, unscanned: bits(label) | id -- a positive double, ordered by (label, id)
+//   unreached:          0x7FF8000000000000 | id -- a quiet NaN, the largest positive integer
+//   scanned:            high word 0xFFF80000, low word kept -- a quiet NaN, a negative integer
+//   padding node:       all ones -- a quiet NaN, a negative integer
+// v_min_f64 (IEEE minNum) ignores quiet NaNs, so the argmin sees only reached,
+// unscanned nodes; the signed min never improves a scanned key.
+constexpr uint64_t kUnreached = 0x7FF8000000000000ull;
+constexpr uint32_t kScannedHi = 0xFFF80000u;
 constexpr int kMaxDeg = 16;   // out-degree (out-slot rounds of 4: 1, 2, 4)
 constexpr int kInSlots = 8;   // in-slots per node: one 16-byte LDS row of u16 entries
 
@@ -144,6 +151,14 @@ __device__ __forceinline__ uint64_t qps64(uint64_t x) {
 }
 __device__ __forceinline__ uint64_t dbits_s(double d) { return (uint64_t)__double_as_longlong(d); }
 __device__ __forceinline__ double bitsd_s(uint64_t b) { return __longlong_as_double((long long)b); }
+
+// v_min_f64 without the compiler's sNaN canonicalisation of the inputs (all NaN
+// keys are quiet by construction)
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 __device__ __forceinline__ void wave_sync_s() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -348,7 +363,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
 #pragma unroll
             for (int i = 0; i < NPL; ++i) {
                 const int v = NPL * jo + i;
-                kt[NPL * j + i] = v >= N ? ~0ull : (v == origin ? (uint64_t)v : (kInfKeyS | (uint64_t)v));
+                kt[NPL * j + i] = v >= N ? ~0ull : (v == origin ? (uint64_t)v : (kUnreached | (uint64_t)v));
                 pl[NPL * j + i] = kNoPred;
             }
             wave_sync_s();
@@ -357,22 +372,23 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             uint64_t m[NPL];
             read_keys<NPL>(kt + NPL * j, m);
             for (int k = 0; k < N; ++k) {
-                // argmin over the lane's keys (pairwise), then over the quad (DPP)
+                // argmin over the lane's keys (pairwise v_min_f64), then over the quad (DPP)
+                double d[NPL];
+#pragma unroll
+                for (int i = 0; i < NPL; ++i) d[i] = bitsd_s(m[i]);
 #pragma unroll
                 for (int w = 1; w < NPL; w *= 2)
 #pragma unroll
-                    for (int i = 0; i + w < NPL; i += 2 * w) m[i] = m[i + w] < m[i] ? m[i + w] : m[i];
-                uint64_t best = m[0];
-                uint64_t o = qps64<0xB1>(best);
-                best = o < best ? o : best;
-                o = qps64<0x4E>(best);
-                best = o < best ? o : best;
-                if (best >= kInfKeyS) break;  // quad-uniform: the rest is unreachable
+                    for (int i = 0; i + w < NPL; i += 2 * w) d[i] = vmin_f64(d[i], d[i + w]);
+                double bd = vmin_f64(d[0], bitsd_s(qps64<0xB1>(dbits_s(d[0]))));
+                bd = vmin_f64(bd, bitsd_s(qps64<0x4E>(dbits_s(bd))));
+                if (!(bd < kInfD)) break;  // quad-uniform: the rest is unreachable (NaN or +inf: all ignored)
+                const uint64_t best = dbits_s(bd);
                 const uint32_t u = (uint32_t)best & 31u;
-                // one lane of the quad stores the scan order and the scanned bit
+                // one lane of the quad stores the scan order and the scanned mark
                 if (j == 0) {
                     ol[k] = (uint8_t)u;
-                    kt32[2 * u + 1] = (uint32_t)(best >> 32) | kSignS;
+                    kt32[2 * u + 1] = kScannedHi;
                 }
                 nscan = k + 1;
                 const uint64_t lb = best & ~31ull;
@@ -420,7 +436,9 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                     // means v already holds this label from the tail pl[v]; scipy's order
                     // between the two is its heap's iff the tails' labels are equal.
                     if (nk[r] < was[r]) pl[v[r]] = (uint8_t)u;
-                    if (nk[r] == was[r]) amb |= (kt[pl[v[r]]] & kLabelMask) == lb;
+                    // (scanned keys keep their low word: equal low label bits = maybe equal
+                    // labels; a false positive costs one exact replay, never a wrong tree)
+                    if (nk[r] == was[r]) amb |= ((kt32[2 * pl[v[r]]] ^ (uint32_t)lb) & ~31u) == 0u;
                 }
             }
             wave_sync_s();

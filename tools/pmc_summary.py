@@ -33,6 +33,8 @@ if "SQ_INSTS_VALU" in mean and "GRBM_GUI_ACTIVE" in mean:
     # is summed over the 8 XCDs; 256 CUs x 4 SIMDs
     cyc = mean["GRBM_GUI_ACTIVE"] / 8
     out["valu_busy_frac"] = 4 * mean["SQ_INSTS_VALU"] / (cyc * 1024)
+if "SQ_LDS_BANK_CONFLICT" in mean and mean.get("SQ_ACTIVE_INST_LDS"):
+    out["lds_bank_conflict_frac"] = mean["SQ_LDS_BANK_CONFLICT"] / mean["SQ_ACTIVE_INST_LDS"]
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     raw = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024
     out["hbm_bytes_per_launch_raw"] = raw
