@@ -22,9 +22,11 @@
 //    follow, decides, and the tree is replayed with the exact Fibonacci heap
 //    (device_common.h exact_sssp).  This replaces the packed kernel's
 //    tie-candidate link pairs (their per-iteration masks, one barrier).
-//  * predecessors are stored as tail node ids (no parallel links), so the
-//    link-load gather compares pred(v) with src(e); the subtree-sum rows,
-//    the replay heap and the link-position scratch alias the key rows.
+//  * the all-or-nothing loads come straight out of the subtree-demand pass
+//    (reverse scan order): each final S(v) is added to v's predecessor link
+//    with a u32 LDS atomic (integral demands: exact), so there is no pass
+//    over (link, tree) pairs; subtree sums, the replay heap and the
+//    link-position scratch alias the key rows.
 // Barriers per MSA/FW iteration: 2 (trees | gather + flow update + BPR +
 // cost table).  Exactness preconditions: packed_ok() plus out/in-degree <= 16.
 #include <hip/hip_runtime.h>
@@ -83,21 +85,19 @@ constexpr int kQs = 4;
 constexpr uint64_t kUnreached = 0x7FF8000000000000ull;
 constexpr uint32_t kScannedHi = 0xFFF80000u;
 constexpr int kMaxDeg = 16;   // out-degree (out-slot rounds of 4: 1, 2, 4)
-constexpr int kInSlots = 8;   // in-slots per node: one 16-byte LDS row of u16 entries
 
 struct SmemS {
-    uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [EPW*E] f32 (dprev: CFW only)
+    uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [EPW*E] f32 (dprev: CFW only); aux: u32 AON link
+                                                   // loads while an iteration runs, f32 after
     uint32_t ocost;  // [EPW][NP][DS] f32 cost of out-link slot s of u (+inf: none)
     uint32_t ov;     // [NP][DS] u8 head node of out-link slot s of u (empty: u itself)
     uint32_t keys;   // [rows][NP] u64 keys per tree; aliased: subtree sums (f32, first NP of each row),
                      // per-wave replay heap, link-position scratch at start-up
     uint32_t pred;   // [EPW*Z][NP] u8 predecessor node per tree (0xFF: none)
     uint32_t ord;    // [EPW*Z][NP] u8 scan order per tree
-    uint32_t iadj;   // [NP][8] u16 in-links of v: tail | link id << 5 (empty: v itself, link 0)
+    uint32_t eid;    // [NP*NP] u8 link id of (u, v) (0xFF: none; the kernel takes E <= 255)
     uint32_t dem;    // [Z*N] f32
     uint32_t t0;     // [E] f32
-    uint32_t lsrc;   // [E] u8 tail node of each link
-    uint32_t ldst;   // [E] u8 head node of each link
     uint32_t unas;   // [EPW] f32
     uint32_t act;    // [EPW] i32
     uint32_t red;    // [EPW*2] f64
@@ -129,11 +129,9 @@ __host__ __device__ inline SmemS smems_layout(int E, int N, int Z, int NP, int E
     o.keys = take((uint32_t)(rows * NP * 8));
     o.pred = take((uint32_t)(EPW * Z * NP));
     o.ord = take((uint32_t)(EPW * Z * NP));
-    o.iadj = take((uint32_t)(NP * kInSlots * 2));
+    o.eid = take((uint32_t)(NP * NP));
     o.dem = take((uint32_t)(Z * N * 4));
     o.t0 = take((uint32_t)(E * 4));
-    o.lsrc = take((uint32_t)E);
-    o.ldst = take((uint32_t)E);
     o.unas = take((uint32_t)(EPW * 4));
     o.act = take((uint32_t)(EPW * 4));
     o.red = take((uint32_t)(EPW * 2 * 8));
@@ -197,7 +195,7 @@ int sparse_rounds(const DevGraph& g) {
 }  // namespace
 
 bool sparse_ok(const DevGraph& g, const trx_params& p) {
-    return packed_ok(g, p) && g.max_out_deg <= kMaxDeg && g.max_in_deg <= kInSlots && g.NP % 8 == 0;
+    return packed_ok(g, p) && g.max_out_deg <= kMaxDeg && g.NP % 8 == 0;
 }
 
 template <int NP, int R>  // R = out-slot rounds per extracted node (DS = 4R slots)
@@ -227,11 +225,10 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     uint64_t* const skeys = (uint64_t*)(smem_raw + O.keys);
     uint8_t* const spred = smem_raw + O.pred;
     uint8_t* const sord = smem_raw + O.ord;
-    uint16_t* const siadj = (uint16_t*)(smem_raw + O.iadj);
+    uint8_t* const seid = smem_raw + O.eid;
+    uint32_t* const sload = reinterpret_cast<uint32_t*>(saux);  // AON link loads (integral demands)
     float* const sdem = (float*)(smem_raw + O.dem);
     float* const st0 = (float*)(smem_raw + O.t0);
-    uint8_t* const slsrc = smem_raw + O.lsrc;
-    uint8_t* const sldst = smem_raw + O.ldst;
     float* const sunas = (float*)(smem_raw + O.unas);
     int* const sact = (int*)(smem_raw + O.act);
     double* const sred = (double*)(smem_raw + O.red);
@@ -269,13 +266,11 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     // relaxation: never improved) at cost +inf; an empty in-slot of v names v
     // itself as tail over link 0 (label(v) + cost > label(v): never achieving)
     for (int i = tid; i < NDS; i += L) sov[i] = (uint8_t)(i / DS);
-    for (int i = tid; i < NP * kInSlots; i += L) siadj[i] = (uint16_t)(i / kInSlots);
+    for (int i = tid; i < NP * NP; i += L) seid[i] = (uint8_t)g.eid_of[i];
     for (int i = tid; i < EPW * NDS; i += L) socost[i] = kInfF;
     for (int i = tid; i < Z * N; i += L) sdem[i] = g.dem[i];
     for (int i = tid; i < E; i += L) {
         st0[i] = g.t0[i];
-        slsrc[i] = (uint8_t)g.src[i];
-        sldst[i] = (uint8_t)g.dst[i];
     }
     __syncthreads();
     for (int u = tid; u < N; u += L) {
@@ -286,8 +281,6 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             sov[pos] = (uint8_t)g.indices[a];
             opos_tmp[g.csr_eid[a]] = (int16_t)pos;
         }
-        const int b0 = g.in_ptr[u], b1 = g.in_ptr[u + 1];
-        for (int b = b0; b < b1; ++b) siadj[u * kInSlots + (b - b0)] = (uint16_t)(g.in_src[b] | (g.in_eid[b] << 5));
     }
     __syncthreads();
     const bool opos_reg = EL <= L;  // one (env, link) per thread: its cost-table slot in a register
@@ -459,9 +452,10 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 }
                 wave_sync_s();
             }
-            // ---------------- all-or-nothing (repair_env.py:490-502, 707-722), part 1:
-            // subtree demand sums S(v) per tree in reverse scan order (one lane per
-            // tree, plain LDS read-modify-write); integral demands: exact in any order.
+            // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree
+            // demand sums S(v) per tree in reverse scan order (one lane per tree, plain
+            // LDS read-modify-write); once S(v) is final it is added to the load of
+            // v's predecessor link (u32 LDS atomics).  Integral demands: exact in any order.
             const float* dm = sdem + zi * N;
             float* const sa = reinterpret_cast<float*>(kt);
             float un = 0.0f;
@@ -487,12 +481,16 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                         w |= (4 * q + b < nscan ? (uint32_t)pl[(ow[q] >> (8 * b)) & 0xFF] : 0u) << (8 * b);
                     pw[q] = w;
                 }
+                uint32_t* const ll = sload + lenv * E;
 #pragma unroll
                 for (int k = NP - 1; k >= 1; --k) {
                     if (k < nscan) {  // quad-uniform
                         const int v = (ow[k >> 2] >> (8 * (k & 3))) & 0xFF;
                         const int pv = (pw[k >> 2] >> (8 * (k & 3))) & 0xFF;
-                        sa[pv] = sa[pv] + sa[v];
+                        const int e = seid[pv * NP + v];  // read beside the sums, off the chain
+                        const float sv = sa[v];
+                        sa[pv] = sa[pv] + sv;
+                        atomicAdd(ll + e, (uint32_t)sv);
                     }
                 }
             }
@@ -502,24 +500,11 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
         __syncthreads();
         TRX_SSTAMP(4);
 
-        // ---------------- all-or-nothing, part 2 + flow update + BPR + next cost
-        // table (repair_env.py:317-342): link load of e = the sum over the env's
-        // trees whose predecessor of dst(e) is src(e) of S(dst(e))
+        // ---------------- flow update + BPR + next cost table (repair_env.py:317-342)
         const double stepd = (p.method == TRX_METHOD_MSA) ? 1.0 / (it + 1.0) : 2.0 / (it + 2.0);
         const float s32 = (float)stepd, om32 = (float)(1.0 - stepd);
-        if (cfw) {
-            for (int i = tid; i < EL; i += L) {
-                const int el = i / E, e = i - el * E;
-                if (!sact[el]) continue;
-                const int v = sldst[e];
-                const uint32_t u = slsrc[e];
-                float ax = 0.0f;
-                for (int z = 0; z < Z; ++z) {
-                    const int tr = el * Z + z;
-                    ax += spred[tr * NP + v] == u ? reinterpret_cast<const float*>(skeys + tr * NP)[v] : 0.0f;
-                }
-                saux[i] = ax;
-            }
+        if (cfw) {  // the conjugate direction needs every link's load of the env
+            for (int i = tid; i < EL; i += L) saux[i] = (float)sload[i];  // exact: < 2^24
             __syncthreads();
             if (tid < EPW && sact[tid]) {
                 double num = 0.0, den = 0.0;
@@ -540,18 +525,8 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             const int el = i / E, e = i - el * E;
             if (!sact[el]) continue;
             const float fl = sflow[i];
-            float ax;
-            if (cfw) {
-                ax = saux[i];
-            } else {
-                const int v = sldst[e];
-                const uint32_t u = slsrc[e];
-                ax = 0.0f;
-                for (int z = 0; z < Z; ++z) {
-                    const int tr = el * Z + z;
-                    ax += spred[tr * NP + v] == u ? reinterpret_cast<const float*>(skeys + tr * NP)[v] : 0.0f;
-                }
-            }
+            const float ax = cfw ? saux[i] : (float)sload[i];  // exact: integral, < 2^24
+            sload[i] = 0u;                                       // the next iteration's loads
             float nf;
             if (cfw) {
                 const float dfw = __fsub_rn(ax, fl);
