@@ -441,6 +441,9 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             const uint64_t need = __ballot(amb != 0 && j == 0);
             wave_sync_s();
             TRX_SSTAMP(2);
+#ifdef TRX_PHASE_STAMPS
+            if (tid == 0) atomicAdd(&trx_phase_cycles_s[7], (unsigned long long)__popcll(need));  // replayed trees (wave 0)
+#endif
             if (need) {  // wave-uniform, rare: exact scipy-heap replays, one tree at a time
                 const float* const stl = st + lenv * E;
                 FibLane* const h = reinterpret_cast<FibLane*>(smem_raw + O.keys + (uint32_t)((tid >> 6) * 16 * NP * 8));

@@ -40,5 +40,8 @@ names = (["load", "dijkstra", "pred pass", "replay+subtree", "barrier wait", "ga
          ["load", "dijkstra", "tie check+replay", "aon walk", "barrier wait", "update+bpr", "tie candidates"]
          if PACKED else ["load", "cost build", "dijkstra", "tie check+replay", "aon", "update+bpr", "tstt+store"])
 tot = sum(buf[i] for i in range(7))
+if KIND == "sparse":
+    print(f"replayed trees (wave 0 of each workgroup): {buf[7]} over 5 steps x {B // 2} workgroups x 30 iterations "
+          f"x 16 trees = {buf[7] / (5 * (B // 2) * 30 * 16) * 100:.3f} %")
 for i, n in enumerate(names):
     print(f"{n:>14}: {buf[i] / tot * 100:6.2f} %  ({buf[i] / 5 / (B / 4) / 30:.0f} cycles/WG/iter)")
