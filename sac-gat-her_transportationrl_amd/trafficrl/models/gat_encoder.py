@@ -33,7 +33,7 @@ from torch import nn
 import torch.nn.functional as F
 
 from .. import _lib
-from .skinny import perm_gather, skinny_linear
+from .skinny import perm_gather, skinny_linear, splitk_linear
 
 # in-feature widths up to which a projection's weight gradient takes the
 # split-K path (trafficrl/models/skinny.py)
@@ -324,7 +324,7 @@ class _Lin(nn.Module):
         _glorot_(self.weight)
 
     def forward(self, x):
-        return F.linear(x, self.weight)
+        return splitk_linear(x, self.weight)
 
 
 class GATConv(nn.Module):

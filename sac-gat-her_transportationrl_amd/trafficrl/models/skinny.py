@@ -65,6 +65,47 @@ class _SkinnyMM(torch.autograd.Function):
         return dx, dw, db
 
 
+class _SplitKLinear(torch.autograd.Function):
+    """y = bf16(x) @ bf16(w)^T (autocast's product, bf16 output) whose weight
+    gradient is `splits` bf16 partial products over K/splits batch rows summed
+    in float32 and returned as the float32 master weight's gradient: no
+    bf16 -> float32 cast of dW, and hipBLASLt's single-tile walk over K = 6144
+    (~11 % of the MFMA peak) becomes a batched product (tools/wgrad_probe.py:
+    44 -> 29 us for 6144 x 1024 x 1024)."""
+
+    @staticmethod
+    def forward(ctx, x, w, splits: int):
+        xb, wb = x.to(torch.bfloat16), w.to(torch.bfloat16)
+        ctx.save_for_backward(xb, wb)
+        ctx.splits = splits
+        return xb @ wb.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wb = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16)
+        dx = dy @ wb if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            S = ctx.splits
+            K = dy.shape[0]
+            part = torch.bmm(dy.reshape(S, K // S, -1).transpose(1, 2), xb.reshape(S, K // S, -1))
+            dw = part.sum(0, dtype=torch.float32)
+        return dx, dw, None
+
+
+def splitk_linear(x: torch.Tensor, w: torch.Tensor, splits: int = 4) -> torch.Tensor:
+    """F.linear(x, w) under bf16 autocast with a split-K float32 weight
+    gradient (large square products of the SAC update); plain F.linear
+    otherwise (other dtypes, no autograd, batch rows not divisible)."""
+    if (torch.is_grad_enabled() and w.requires_grad and w.dtype == torch.float32 and x.dim() == 2
+            and x.shape[0] % splits == 0 and x.shape[0] >= 1024 and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        with torch.autocast("cuda", enabled=False):
+            return _SplitKLinear.apply(x, w, splits)
+    return torch.nn.functional.linear(x, w)
+
+
 def skinny_linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None) -> torch.Tensor:
     """F.linear(x, w, b) (autocast-aware) whose weight gradient is a split-K
     float32 reduction; for products with a tiny in- or out-feature side."""

@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 from ..models import fused
 from ..models.gat_encoder import GATEncoder, is_regular_batch
-from ..models.skinny import regular_gather, skinny_linear
+from ..models.skinny import regular_gather, skinny_linear, splitk_linear
 
 
 @dataclass
@@ -232,7 +232,7 @@ class _EdgeHead(nn.Module):
         # torch.split: the backward is one cat, not a zero-fill + add per slice
         w_src, w_dst, w_e, w_ctx = torch.split(W1, [d, d, k, W1.shape[1] - 2 * d - k], dim=1)
         w_nodes = torch.cat([w_src, w_dst], 0)                        # [2H, embed]
-        p = node_emb @ w_nodes.t()                                    # per-node projections
+        p = splitk_linear(node_emb, w_nodes)                          # per-node projections
         hdim = W1.shape[0]
         c = global_ctx @ w_ctx.t() + b1                               # [B, H] per-graph context
         W2, b2 = self.edge_mlp[2].weight, self.edge_mlp[2].bias
