@@ -50,6 +50,7 @@ for s in "$@"; do
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         hostprobe) step hostprobe 300 python tools/cpu_bound_probe.py 4096 ;;
         mm) step mm 200 python tools/mm_probe.py ;;
+        actmm) step actmm 200 python tools/act_gemm_probe.py ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
         copies) step copies 300 python tools/update_profile.py 60 copies ;;
         istamps) step istamps 300 python tools/infer_stamps.py 4096 ;;
