@@ -35,16 +35,19 @@ struct SmemT {
     uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [E] f32
     uint32_t cold, rowd, colh;                     // [NP] f32, f32, u32: column k, row k, next_hop[:, k]
     uint32_t he;                                   // [NP*NP] u16: next hop | link id << 8 (0xFFFF: none)
-    uint32_t eid;                                  // [NP*NP] u8 link id of (u, v), 0xFF: none
     uint32_t red;                                  // [2] f64 (CFW)
-    uint32_t od, odd;                              // [P] u32 origin | destination << 8, f32 demand
+    uint32_t od;                                   // [P] u16 origin | destination << 8 (demands: global)
     uint32_t rep;                                  // [kRep][E | 1] u32 link-load copies (integral demands)
     uint32_t total;
 };
 
 __host__ __device__ inline uint32_t al16t(uint32_t x) { return (x + 15u) & ~15u; }
 
-__host__ __device__ inline SmemT smemt_layout(int E, int NP, int P) {
+// LDS per env is what limits residency (one wave per workgroup): the link-id
+// table and the OD demands are read from the graph in global memory (cached;
+// once per iteration / walk), OD entries are u16, the CFW direction is
+// allocated only for CFW.
+__host__ __device__ inline SmemT smemt_layout(int E, int NP, int P, bool cfw) {
     SmemT o{};
     uint32_t off = 0;
     auto take = [&off](uint32_t bytes) {
@@ -59,15 +62,13 @@ __host__ __device__ inline SmemT smemt_layout(int E, int NP, int P) {
     o.goal = take(el);
     o.t = take(el);
     o.aux = take(el);
-    o.dprev = take(el);
+    o.dprev = take(cfw ? el : 0u);
     o.cold = take((uint32_t)NP * 4u);
     o.rowd = take((uint32_t)NP * 4u);
     o.colh = take((uint32_t)NP * 4u);
     o.he = take((uint32_t)(NP * NP * 2));
-    o.eid = take((uint32_t)(NP * NP));
     o.red = take(16u);
-    o.od = take((uint32_t)P * 4u);
-    o.odd = take((uint32_t)P * 4u);
+    o.od = take((uint32_t)P * 2u);
     o.rep = take((uint32_t)(kRep * (E | 1)) * 4u);
     o.total = off;
     return o;
@@ -82,7 +83,7 @@ __device__ __forceinline__ void wave_sync() {
 }  // namespace
 
 bool torch_kernel_ok(const DevGraph& g) {
-    return g.N <= kSmallMaxNodes && g.E <= 255 && g.NP % 8 == 0 && smemt_layout(g.E, g.NP, g.P).total <= 64 * 1024;
+    return g.N <= kSmallMaxNodes && g.E <= 255 && g.NP % 8 == 0 && smemt_layout(g.E, g.NP, g.P, true).total <= 64 * 1024;
 }
 
 template <int NP>
@@ -97,7 +98,8 @@ __global__ void __launch_bounds__(64) env_kernel_t(const DevGraph g, const trx_p
     const int lane = threadIdx.x;
     const int gb = blockIdx.x;
     if (gb >= B) return;
-    const SmemT O = smemt_layout(E, NP, P);
+    const bool cfw = p.method == TRX_METHOD_CFW;
+    const SmemT O = smemt_layout(E, NP, P, cfw);
     float* const sflow = (float*)(smem_raw + O.flow);
     float* const scap = (float*)(smem_raw + O.cap);
     float* const sdmg = (float*)(smem_raw + O.dmg);
@@ -109,13 +111,11 @@ __global__ void __launch_bounds__(64) env_kernel_t(const DevGraph g, const trx_p
     float* const rowd = (float*)(smem_raw + O.rowd);
     uint32_t* const colh = (uint32_t*)(smem_raw + O.colh);
     uint16_t* const she = (uint16_t*)(smem_raw + O.he);
-    uint8_t* const seid = smem_raw + O.eid;
+    const int16_t* const geid = g.eid_of;  // [NP*NP] link id of (u, v), -1: none (global, cached)
     double* const sred = (double*)(smem_raw + O.red);
-    uint32_t* const sod = (uint32_t*)(smem_raw + O.od);
-    float* const sodd = (float*)(smem_raw + O.odd);
+    uint16_t* const sod = (uint16_t*)(smem_raw + O.od);
     uint32_t* const srep = (uint32_t*)(smem_raw + O.rep);
     const int EP = E | 1;  // odd row stride: a link's copies sit in different banks
-    const bool cfw = p.method == TRX_METHOD_CFW;
 
     // ------------------------------------------------ activation (wave-uniform)
     int active;
@@ -137,7 +137,6 @@ __global__ void __launch_bounds__(64) env_kernel_t(const DevGraph g, const trx_p
     }
 
     // ------------------------------------------------------- load state
-    for (int i = lane; i < NP * NP; i += 64) seid[i] = (uint8_t)g.eid_of[i];
     const int act_e = mode == kModeStep ? action[gb] : -1;
     for (int e = lane; e < E; e += 64) {
         const size_t gi = (size_t)gb * E + e;
@@ -161,15 +160,14 @@ __global__ void __launch_bounds__(64) env_kernel_t(const DevGraph g, const trx_p
         sdmg[e] = dm;
         sgoal[e] = gl;
         saux[e] = 0.0f;
-        sdprev[e] = 0.0f;
+        if (cfw) sdprev[e] = 0.0f;
         st[e] = bpr_cost(fl, cp, g.t0[e], dm, p.bpr_alpha, p.bpr_beta);
     }
     // OD entries (origin | destination << 8, demand), zone-major (od_ptr)
     for (int zi = 0; zi < g.Z; ++zi) {
         const int q0 = g.od_ptr[zi], q1 = g.od_ptr[zi + 1], o = g.origins[zi];
         for (int q = q0 + lane; q < q1; q += 64) {
-            sod[q] = (uint32_t)o | ((uint32_t)g.od_dst[q] << 8);
-            sodd[q] = g.od_dem[q];
+            sod[q] = (uint16_t)(o | (g.od_dst[q] << 8));
         }
     }
     wave_sync();
@@ -185,10 +183,10 @@ __global__ void __launch_bounds__(64) env_kernel_t(const DevGraph g, const trx_p
 #pragma unroll
             for (int b = 0; b < BS; ++b) {
                 const int i = BS * r + a, j = BS * c + b;
-                const int e = seid[i * NP + j];
+                const int e = geid[i * NP + j];
                 // dist = 1e12, diag 0, then dist[row, col] = t per link (524-535); padding never improves
-                d[a][b] = e != 0xFF ? st[e] : (i == j ? 0.0f : 1e12f);
-                h[a][b] = e != 0xFF ? (uint32_t)j : 0xFFu;
+                d[a][b] = e >= 0 ? st[e] : (i == j ? 0.0f : 1e12f);
+                h[a][b] = e >= 0 ? (uint32_t)j : 0xFFu;
             }
         for (int k = 0; k < N; ++k) {
             const int kb = k / BS, ks = k - kb * BS;
@@ -240,7 +238,7 @@ __global__ void __launch_bounds__(64) env_kernel_t(const DevGraph g, const trx_p
             for (int b = 0; b < BS; ++b) {
                 const int i = BS * r + a, j = BS * c + b;
                 const uint32_t hv = h[a][b];
-                she[i * NP + j] = hv == 0xFFu ? (uint16_t)0xFFFF : (uint16_t)(hv | ((uint32_t)seid[i * NP + hv] << 8));
+                she[i * NP + j] = hv == 0xFFu ? (uint16_t)0xFFFF : (uint16_t)(hv | ((uint32_t)geid[i * NP + hv] << 8));
             }
         wave_sync();
         // ---------------- next_hop walks (repair_env.py:548-568)
@@ -259,14 +257,14 @@ __global__ void __launch_bounds__(64) env_kernel_t(const DevGraph g, const trx_p
                 const uint32_t odm = sod[q];
                 oA = odm & 0xFF;
                 dA = (odm >> 8) & 0xFF;
-                mA = (uint32_t)sodd[q];
+                mA = (uint32_t)g.od_dem[q];  // zone-major like sod (global, cached)
             }
             const bool hasB = q + 64 < P;
             if (hasB) {
                 const uint32_t odm = sod[q + 64];
                 oB = odm & 0xFF;
                 dB = (odm >> 8) & 0xFF;
-                mB = (uint32_t)sodd[q + 64];
+                mB = (uint32_t)g.od_dem[q + 64];
             }
             const bool liveA = oA != dA, liveB = hasB && oB != dB;  // origin == dest: skipped (551-552)
             int cA = oA, hA = 0, cB = oB, hB = 0;
@@ -410,7 +408,7 @@ hipError_t launch_env_kernel_torch(const DevGraph& g, const trx_params& p, const
                                    const uint8_t* env_mask, hipStream_t stream) {
     if (num_envs <= 0) return hipSuccess;
     const int num_od = g.P;
-    const size_t smem = smemt_layout(g.E, g.NP, num_od).total;
+    const size_t smem = smemt_layout(g.E, g.NP, num_od, p.method == TRX_METHOD_CFW).total;
     const dim3 grid(num_envs), block(64);
     switch (g.NP) {
         case 8:
