@@ -66,7 +66,10 @@ extern "C" int trx_debug_phase_cycles_s(unsigned long long* out, int reset) {
 #endif
 
 #ifndef TRX_SPARSE_WAVES
-#define TRX_SPARSE_WAVES 6  // waves/SIMD the register budget targets (LDS allows 6 at EPW = 2)
+// waves/SIMD the register budget targets (72 VGPRs; some spills outside the Dijkstra
+// loop).  LDS then allows 9 workgroups (27 waves) per CU for Sioux Falls: 0.92 ->
+// 0.84 ms per 4096-env step against the 6-wave (80 VGPR, 24 waves) build.
+#define TRX_SPARSE_WAVES 7
 #endif
 
 namespace trx {
@@ -96,8 +99,6 @@ struct SmemS {
     uint32_t pred;   // [EPW*Z][NP] u8 predecessor node per tree (0xFF: none)
     uint32_t ord;    // [EPW*Z][NP] u8 scan order per tree
     uint32_t eid;    // [NP*NP] u8 link id of (u, v) (0xFF: none; the kernel takes E <= 255)
-    uint32_t dem;    // [Z*N] f32
-    uint32_t t0;     // [E] f32
     uint32_t unas;   // [EPW] f32
     uint32_t act;    // [EPW] i32
     uint32_t red;    // [EPW*2] f64
@@ -130,8 +131,6 @@ __host__ __device__ inline SmemS smems_layout(int E, int N, int Z, int NP, int E
     o.pred = take((uint32_t)(EPW * Z * NP));
     o.ord = take((uint32_t)(EPW * Z * NP));
     o.eid = take((uint32_t)(NP * NP));
-    o.dem = take((uint32_t)(Z * N * 4));
-    o.t0 = take((uint32_t)(E * 4));
     o.unas = take((uint32_t)(EPW * 4));
     o.act = take((uint32_t)(EPW * 4));
     o.red = take((uint32_t)(EPW * 2 * 8));
@@ -227,8 +226,8 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     uint8_t* const sord = smem_raw + O.ord;
     uint8_t* const seid = smem_raw + O.eid;
     uint32_t* const sload = reinterpret_cast<uint32_t*>(saux);  // AON link loads (integral demands)
-    float* const sdem = (float*)(smem_raw + O.dem);
-    float* const st0 = (float*)(smem_raw + O.t0);
+    const float* const gdem = g.dem;  // [Z*N] demands and [E] free-flow times: read from the graph
+    const float* const gt0 = g.t0;    // (global, cached) -- LDS per workgroup bounds residency
     float* const sunas = (float*)(smem_raw + O.unas);
     int* const sact = (int*)(smem_raw + O.act);
     double* const sred = (double*)(smem_raw + O.red);
@@ -268,11 +267,6 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     for (int i = tid; i < NDS; i += L) sov[i] = (uint8_t)(i / DS);
     for (int i = tid; i < NP * NP; i += L) seid[i] = (uint8_t)g.eid_of[i];
     for (int i = tid; i < EPW * NDS; i += L) socost[i] = kInfF;
-    for (int i = tid; i < Z * N; i += L) sdem[i] = g.dem[i];
-    for (int i = tid; i < E; i += L) {
-        st0[i] = g.t0[i];
-    }
-    __syncthreads();
     for (int u = tid; u < N; u += L) {
         const int a0 = g.indptr[u], a1 = g.indptr[u + 1];
         for (int a = a0; a < a1; ++a) {
@@ -319,7 +313,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
         sgoal[i] = gl;
         saux[i] = 0.0f;
         if (cfw) sdprev[i] = 0.0f;
-        const float tv = sact[el] ? bpr_cost(fl, cp, st0[e], dm, p.bpr_alpha, p.bpr_beta) : 0.0f;
+        const float tv = sact[el] ? bpr_cost(fl, cp, gt0[e], dm, p.bpr_alpha, p.bpr_beta) : 0.0f;
         st[i] = tv;
         if (my_opos >= 0) socost[my_opos] = tv;  // opos_reg: i == tid
     }
@@ -459,7 +453,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             // demand sums S(v) per tree in reverse scan order (one lane per tree, plain
             // LDS read-modify-write); once S(v) is final it is added to the load of
             // v's predecessor link (u32 LDS atomics).  Integral demands: exact in any order.
-            const float* dm = sdem + zi * N;
+            const float* dm = gdem + zi * N;
             float* const sa = reinterpret_cast<float*>(kt);
             float un = 0.0f;
 #pragma unroll
@@ -551,7 +545,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             }
             if (nf != nf) nf = 0.0f;  // nan_to_num guard (repair_env.py:338-340)
             sflow[i] = nf;
-            const float tv = bpr_cost(nf, scap[i], st0[e], sdmg[i], p.bpr_alpha, p.bpr_beta);
+            const float tv = bpr_cost(nf, scap[i], gt0[e], sdmg[i], p.bpr_alpha, p.bpr_beta);
             st[i] = tv;
             if (my_opos >= 0) socost[my_opos] = tv;
         }
