@@ -466,28 +466,33 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             }
             wave_sync_s();
             if (j == 0) {
-                uint32_t ow[NP / 4];  // the scan order in registers
-#pragma unroll
-                for (int q = 0; q < NP / 4; ++q) ow[q] = reinterpret_cast<const uint32_t*>(ol)[q];
-                uint32_t pw[NP / 4];  // and the predecessor of each scanned node
-#pragma unroll
-                for (int q = 0; q < NP / 4; ++q) {
-                    uint32_t w = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b)
-                        w |= (4 * q + b < nscan ? (uint32_t)pl[(ow[q] >> (8 * b)) & 0xFF] : 0u) << (8 * b);
-                    pw[q] = w;
-                }
                 uint32_t* const ll = sload + lenv * E;
+                constexpr int QH = NP / 8;  // scan-order words per half: two halves keep 2*QH VGPRs live
 #pragma unroll
-                for (int k = NP - 1; k >= 1; --k) {
-                    if (k < nscan) {  // quad-uniform
-                        const int v = (ow[k >> 2] >> (8 * (k & 3))) & 0xFF;
-                        const int pv = (pw[k >> 2] >> (8 * (k & 3))) & 0xFF;
-                        const int e = seid[pv * NP + v];  // read beside the sums, off the chain
-                        const float sv = sa[v];
-                        sa[pv] = sa[pv] + sv;
-                        atomicAdd(ll + e, (uint32_t)sv);
+                for (int half = 1; half >= 0; --half) {
+                    uint32_t ow[QH], pw[QH];  // scan order and predecessors of this half, in registers
+#pragma unroll
+                    for (int q = 0; q < QH; ++q) ow[q] = reinterpret_cast<const uint32_t*>(ol)[half * QH + q];
+#pragma unroll
+                    for (int q = 0; q < QH; ++q) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            w |= (4 * (half * QH + q) + b < nscan ? (uint32_t)pl[(ow[q] >> (8 * b)) & 0xFF] : 0u)
+                                 << (8 * b);
+                        pw[q] = w;
+                    }
+#pragma unroll
+                    for (int kk = 4 * QH - 1; kk >= 0; --kk) {
+                        const int k = half * 4 * QH + kk;
+                        if (k >= 1 && k < nscan) {  // quad-uniform
+                            const int v = (ow[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
+                            const int pv = (pw[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
+                            const int e = seid[pv * NP + v];  // read beside the sums, off the chain
+                            const float sv = sa[v];
+                            sa[pv] = sa[pv] + sv;
+                            atomicAdd(ll + e, (uint32_t)sv);
+                        }
                     }
                 }
             }
