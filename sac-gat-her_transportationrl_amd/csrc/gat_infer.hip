@@ -237,7 +237,50 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
     //    wave at a time, one per 16-lane row; a lane owns channels 4*sl + 64*m
     //    (conflict-free LDS reads) and the row sums by DPP (no readlane chain).
     //    Pairs t = h*n + i, groups of four dealt round-robin to the waves.
-    {
+    //    When heads and waves nest (H | waves or waves | H) and C <= 256, a wave
+    //    keeps one head: its lanes hold that head's att_src/att_dst slices in
+    //    registers (loaded once) and loop over the nodes four at a time, so the
+    //    loop reads only LDS (the per-pair global att loads were its latency).
+    //    Same per-lane summation order either way.
+    const bool head_waves = C <= 256 && C % 64 == 0 && (kInferWaves % H == 0 || H % kInferWaves == 0);
+    if (head_waves) {
+        const int sub = lane >> 4, sl = lane & 15;
+        const int hstep = H >= kInferWaves ? kInferWaves : H;
+        const int wph = H >= kInferWaves ? 1 : kInferWaves / H;  // waves sharing one head
+        const int wi = H >= kInferWaves ? 0 : wave / H;
+        const int CM = C / 64;
+        for (int h = H >= kInferWaves ? wave : wave % H; h < H; h += hstep) {
+            float4 sa[4], da[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                if (m < CM) {
+                    sa[m] = *reinterpret_cast<const float4*>(a.att_src + h * C + 4 * sl + 64 * m);
+                    da[m] = *reinterpret_cast<const float4*>(a.att_dst + h * C + 4 * sl + 64 * m);
+                }
+            for (int i0 = 4 * wi; i0 < n; i0 += 4 * wph) {
+                const int i = i0 + sub;
+                const bool ok = i < n;
+                float s1 = 0.0f, s2 = 0.0f;
+                if (ok) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        if (m < CM) {
+                            const uint2 u = *reinterpret_cast<const uint2*>(xs + i * HC + h * C + 4 * sl + 64 * m);
+                            const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
+                            const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
+                            s1 += (v0 * sa[m].x + v1 * sa[m].y) + (v2 * sa[m].z + v3 * sa[m].w);
+                            s2 += (v0 * da[m].x + v1 * da[m].y) + (v2 * da[m].z + v3 * da[m].w);
+                        }
+                }
+                s1 = row_sum16_f(s1);
+                s2 = row_sum16_f(s2);
+                if (ok && sl == 0) {
+                    as_[i * H + h] = s1;
+                    ad_[i * H + h] = s2;
+                }
+            }
+        }
+    } else {
         const int P = n * H, groups = (P + 3) / 4;
         const int sub = lane >> 4, sl = lane & 15;
         for (int gi = wave; gi < groups; gi += kInferWaves) {
