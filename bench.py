@@ -181,32 +181,41 @@ def gemm_mfma(rows, graphs, hidden=256, heads=4, embed=256, reps=20):
             "peak": MFMA_PEAK_BF16 / 1e12, "unit": "TFLOP/s", "frac": flops / sec / MFMA_PEAK_BF16}
 
 
-def measured_traffic(network):
-    """HBM bytes per env-kernel launch from the committed rocprofv3 PMC summary
-    of this workload (profiles/r02_sf_pmc.json for Sioux Falls,
-    profiles/r01_ana_pmc.json for the Anaheim-size network; separate
-    FETCH_SIZE / WRITE_SIZE passes, see tools/pmc_summary.py)."""
-    name = {"sf": "r02_sf_sparse_pmc.json", "anaheim": "r01_ana_pmc.json"}[network]
+def lib_sha16():
+    """First 16 hex digits of sha256(libtrafficrl.so) -- the binary this process loads."""
+    import hashlib
+    from trafficrl import _lib
+    with open(_lib.LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def measured_traffic(network, sha):
+    """HBM bytes per env-kernel launch and the VALU / LDS-conflict shares from
+    the committed rocprofv3 PMC summary of this workload (tools/pmc_summary.py:
+    separate FETCH_SIZE / WRITE_SIZE / SQ passes).  Used only when the summary
+    was captured on the library this process loaded (lib_sha16 match);
+    otherwise (None, reason)."""
+    name = {"sf": "r03_sf_pmc.json", "anaheim": "r03_ana_pmc.json"}[network]
     path = os.path.join(ROOT, "profiles", name)
     try:
         d = json.load(open(path))
-        return (d.get("hbm_bytes_per_launch_raw"), os.path.relpath(path, ROOT), d.get("valu_busy_frac"),
-                d.get("lds_bank_conflict_frac"))
     except (OSError, ValueError):
-        return None, None, None, None
+        return None, f"no PMC summary {os.path.relpath(path, ROOT)}"
+    if d.get("lib_sha16") != sha:
+        return None, (f"{os.path.relpath(path, ROOT)} was captured on libtrafficrl.so {d.get('lib_sha16')}, "
+                      f"this run loaded {sha}: counters omitted")
+    return d, os.path.relpath(path, ROOT)
 
 
-def env_kernel_name(big, sp):
-    """The env kernel trx_step launches for this workload (capi.hip run())."""
-    if big:
-        return "trx::env_kernel_big"
-    if os.environ.get("TRX_KERNEL", "") == "quad":
-        return "trx::env_kernel_q<24>"     # the round-1 quad kernel (A/B runs)
-    if sp == "scipy" and os.environ.get("TRX_KERNEL", "") == "packed":
-        return "trx::env_kernel_p<24>"     # packed-key Dijkstra (assign_packed.hip, A/B runs)
-    if sp == "scipy":
-        return "trx::env_kernel_s<24, 2>"  # sparse-relaxation Dijkstra (assign_sparse.hip; SF: max out-degree 5)
-    return "trx::env_kernel_t<24>"         # torch rule: per-wave Floyd-Warshall (assign_torch.hip)
+def env_kernel_name(env, big):
+    """The env kernel trx_step launches for this workload (trx_env_kernel_name),
+    with the template arguments of the Sioux Falls instantiation."""
+    k = env.kernel_name
+    if k == "env_kernel_s" and env.num_nodes == 24:
+        return "trx::env_kernel_s<24, 2>"   # sparse-relaxation Dijkstra (SF: max out-degree 5)
+    if k in ("env_kernel_t", "env_kernel_q") and env.num_nodes == 24:
+        return f"trx::{k}<24>"
+    return f"trx::{k}"
 
 
 def main():
@@ -384,11 +393,15 @@ def main():
     P = len(env.graph.od_o)
     bpa = bytes_per_assign(N, E, Z, P, args.iters)
     achieved = bpa * B / mean_kernel_s
-    traffic, traffic_src, valu_frac, lds_conf = measured_traffic(args.network)
-    kname = env_kernel_name(big, args.sp)
-    if (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")) or \
-            (not big and kname != "trx::env_kernel_s<24, 2>"):
-        traffic, traffic_src, valu_frac, lds_conf = None, None, None, None  # committed PMC passes: default workloads
+    kname = env_kernel_name(env, big)
+    sha = lib_sha16()
+    pmc, pmc_src = measured_traffic(args.network, sha)
+    if pmc is not None and (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")) \
+            or pmc is not None and pmc.get("kernel", "").split("(")[0] != kname:
+        pmc, pmc_src = None, "committed PMC passes cover the default workloads only"
+    traffic = pmc.get("hbm_bytes_per_launch_raw") if pmc else None
+    valu_frac = pmc.get("valu_busy_frac") if pmc else None
+    lds_conf = pmc.get("lds_bank_conflict_frac") if pmc else None
     mfma = gemm_mfma(B * N, B) if (args.workload == "train" and rank == 0) else None
     if rank == 0:
         cpu = None
@@ -426,8 +439,10 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": traffic,
-                "traffic_note": (f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {traffic_src} "
-                                 "(raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic else None,
+                "traffic_note": (f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {pmc_src} (same libtrafficrl.so "
+                                 f"{sha}; raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic
+                else pmc_src,
+                "lib_sha16": sha,
                 "kernel": kname, "kernel_mean_ms": mean_kernel_s * 1e3,
                 "valu_busy_frac": valu_frac,
                 "lds_bank_conflict_frac": lds_conf,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 4
+#define TRX_ABI_VERSION 5
 
 /* error codes */
 #define TRX_OK 0
@@ -129,6 +129,14 @@ int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs);
  * (envs are contiguous rows of equal size: row b starts at b * bytes(1)).
  * GP needs N <= 32, E <= 128 and 1 <= keep_paths <= 3 (else TRX_EUNSUP). */
 int64_t trx_gp_state_bytes(const trx_graph* g, int32_t num_envs, int32_t keep_paths);
+
+/* Which env kernel trx_assign/trx_reset/trx_step launch for this graph and
+ * params: "env_kernel_s" (scipy rule, N <= 32, within the exact-label and
+ * out-degree <= 16 preconditions), "env_kernel_q" (the general N <= 32 kernel,
+ * both rules), "env_kernel_t" (torch rule), "env_kernel_big" (N > 32),
+ * "gp_kernel", or "" when no kernel takes the pair (the calls then fail with
+ * TRX_EUNSUP).  No device work; the string is static. */
+const char* trx_env_kernel_name(const trx_graph* g, const trx_params* p);
 
 /* ----------------------------------------------------------- hot path
  * trx_assign: RepairEnv.compute_flow_assignment (repair_env.py:299-345) for

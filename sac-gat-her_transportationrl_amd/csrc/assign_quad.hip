@@ -1,7 +1,10 @@
 // assign_quad.hip -- fused batched static traffic assignment, gfx950, v2.
 //
-// Same contract as assign_kernel.hip (src/env/repair_env.py:299-345, 207-237,
-// 167-205), different mapping: each (env, origin) shortest-path tree is owned
+// The general small-graph (N <= 32) env kernel for both shortest-path rules:
+// the dispatcher (capi.hip select_env_kernel) runs it for graphs outside the
+// sparse kernel's exact-label / out-degree preconditions (scipy rule) and the
+// torch-rule kernel's LDS budget (torch rule), and on TRX_KERNEL=quad.
+// Contract: src/env/repair_env.py:299-345, 207-237, 167-205.  Mapping: each (env, origin) shortest-path tree is owned
 // by a QUAD of lanes instead of one lane.  Lane j of the quad owns nodes
 // v = 4i + j (i < NP/4), keeping their float64 labels and predecessor info in
 // VGPRs.  One Dijkstra extraction is:
@@ -638,12 +641,18 @@ LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs, int sp_rule) {
     return c;
 }
 
+bool quad_ok(const DevGraph& g, int sp_rule) {
+    if (g.N > kSmallMaxNodes) return false;
+    const LaunchCfg c = quad_launch_cfg(g, 1, sp_rule);
+    return c.threads <= 512 && c.smem <= 64 * 1024;
+}
+
 hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream) {
     LaunchCfg c = quad_launch_cfg(g, num_envs, p.sp_rule);
     if (c.blocks == 0) return hipSuccess;
-    if (c.threads > 512) return hipErrorInvalidConfiguration;
+    if (c.threads > 512 || c.smem > 64 * 1024) return hipErrorInvalidConfiguration;
     dim3 grid(c.blocks), block(c.threads);
     if (p.sp_rule == TRX_SP_TORCH) {
         switch (c.np) {

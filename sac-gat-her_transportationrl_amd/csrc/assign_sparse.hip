@@ -1,6 +1,6 @@
 // assign_sparse.hip -- fused batched static traffic assignment, gfx950, v4
 // ("sparse-relaxation" kernel).  Same contract and the same exact-label
-// packed keys as assign_packed.hip (src/env/repair_env.py:167-205 reset,
+// packed keys as the round-2 packed kernel (src/env/repair_env.py:167-205 reset,
 // 207-237 step, 299-345 assignment, scipy branch of _all_or_nothing 481-503 +
 // 707-722, compute_tstt 724-735); the Dijkstra is reorganised around where
 // the packed kernel spent its VALU issue:
@@ -28,7 +28,8 @@
 //    over (link, tree) pairs; subtree sums, the replay heap and the
 //    link-position scratch alias the key rows.
 // Barriers per MSA/FW iteration: 2 (trees | gather + flow update + BPR +
-// cost table).  Exactness preconditions: packed_ok() plus out/in-degree <= 16.
+// cost table).  Exactness preconditions: exact_label_ok() plus out-degree <= 16
+// (sparse_ok(); graphs outside them run env_kernel_q, assign_quad.hip).
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -193,15 +194,34 @@ int sparse_rounds(const DevGraph& g) {
 
 }  // namespace
 
+// Exact-label headroom: every path label is an exact float64 sum of float32
+// link costs, each a multiple of g = ulp(smallest float32 cost); when
+// (N-1) * t_max < 2^48 g the label's mantissa ends in >= 5 zero bits, which
+// carry the node id of the key.  t_max bounds the BPR cost at the v/c clip
+// (10) and the damaged-link cost 1e6 (repair_env.py:667-677).
+bool exact_label_ok(const DevGraph& g, const trx_params& p) {
+    if (!(g.min_t0 > 0.0f) || p.bpr_alpha < 0.0f || g.E > 255) return false;
+    int ex = 0;
+    std::frexp((double)g.min_t0, &ex);                 // min_t0 = m * 2^ex, m in [0.5, 1)
+    const double gran = std::ldexp(1.0, ex - 1 - 23);  // ulp of the smallest float32 cost
+    const double tmax = std::fmax(1e6, (double)g.max_t0 * (1.0 + (double)p.bpr_alpha * std::pow(10.0, p.bpr_beta)));
+    const double bound = (double)(g.N - 1) * tmax * 1.0001;
+    return bound < std::ldexp(gran, 48);
+}
+
 bool sparse_ok(const DevGraph& g, const trx_params& p) {
-    return packed_ok(g, p) && g.max_out_deg <= kMaxDeg && g.NP % 8 == 0;
+    if (g.N > kSmallMaxNodes || !exact_label_ok(g, p) || g.max_out_deg > kMaxDeg || g.NP % 8 != 0) return false;
+    // the launch budget launch_env_kernel_sparse enforces, checked here so that
+    // selection falls through to env_kernel_q instead of failing the step
+    const LaunchCfg c = sparse_launch_cfg(g, 1, p.method);
+    return c.threads <= 256 && c.smem <= 64 * 1024;
 }
 
 template <int NP, int R>  // R = out-slot rounds per extracted node (DS = 4R slots)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TRX_SPARSE_WAVES)))
 env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int EPW, int mode,
              const int32_t* __restrict__ action, double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
-             uint8_t* __restrict__ valid_out, const uint8_t* __restrict__ env_mask) {
+             uint8_t* __restrict__ valid_out, const uint8_t* __restrict__ env_mask, unsigned char* __restrict__ ws) {
     constexpr int NPL = NP / kQs;
     constexpr int DS = R * kQs;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -373,10 +393,18 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 const uint64_t best = dbits_s(bd);
                 const uint32_t u = (uint32_t)best & 31u;
                 // one lane of the quad stores the scan order and the scanned mark
+#ifdef TRX_AON_ANC
+                // scanned mark: the high word keeps 19 label bits (bits 5..23 of the
+                // low word) for the tie check; the low word receives the node's
+                // ancestor mask at the end of the step
+                if (j == 0) kt32[2 * u + 1] = kScannedHi | (((uint32_t)best >> 5) & 0x7FFFFu);
+                const uint32_t pu = pl[u];
+#else
                 if (j == 0) {
                     ol[k] = (uint8_t)u;
                     kt32[2 * u + 1] = kScannedHi;
                 }
+#endif
                 nscan = k + 1;
                 const uint64_t lb = best & ~31ull;
                 const double bl = bitsd_s(lb);
@@ -414,6 +442,10 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                         was[r] = __hip_atomic_fetch_min(reinterpret_cast<long long*>(kt + v[r]), nk[r],
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+#ifdef TRX_AON_ANC
+                // ancestor mask of u's predecessor (scanned earlier: its low word is final)
+                const uint32_t ap = kt32[2 * (pu < (uint32_t)NP ? pu : 0u)];
+#endif
                 // next step's keys: issued behind the mark and the atomics (a wave's LDS
                 // operations complete in order), before waiting on the atomics' results
                 read_keys<NPL>(kt + NPL * j, m);
@@ -425,8 +457,16 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                     if (nk[r] < was[r]) pl[v[r]] = (uint8_t)u;
                     // (scanned keys keep their low word: equal low label bits = maybe equal
                     // labels; a false positive costs one exact replay, never a wrong tree)
+#ifdef TRX_AON_ANC
+                    if (nk[r] == was[r])
+                        amb |= ((kt32[2 * pl[v[r]] + 1] ^ ((uint32_t)lb >> 5)) & 0x7FFFFu) == 0u;
+#else
                     if (nk[r] == was[r]) amb |= ((kt32[2 * pl[v[r]]] ^ (uint32_t)lb) & ~31u) == 0u;
+#endif
                 }
+#ifdef TRX_AON_ANC
+                if (j == 0) kt32[2 * u] = (pu < (uint32_t)NP ? ap : 0u) | (1u << u);
+#endif
             }
             wave_sync_s();
             TRX_SSTAMP(1);
@@ -440,15 +480,74 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
 #endif
             if (need) {  // wave-uniform, rare: exact scipy-heap replays, one tree at a time
                 const float* const stl = st + lenv * E;
-                FibLane* const h = reinterpret_cast<FibLane*>(smem_raw + O.keys + (uint32_t)((tid >> 6) * 16 * NP * 8));
+                // the exact heap lives in the caller's workspace (global memory, one
+                // FibLane per wave): the key rows stay intact for the AON phase
+                FibLane* const h = reinterpret_cast<FibLane*>(
+                    ws + ((size_t)blockIdx.x * (size_t)(L >> 6) + (size_t)(tid >> 6)) * sizeof(FibLane));
                 uint64_t pending = need;
                 while (pending) {
                     const int leader = __ffsll((unsigned long long)pending) - 1;
-                    if ((tid & 63) == leader) replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
+                    if ((tid & 63) == leader) {
+                        replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
+#ifdef TRX_AON_ANC
+                        // the replayed tree's ancestor masks, in its scan order, into the
+                        // low words of its (scanned) keys
+                        for (int kk = 0; kk < nscan; ++kk) {
+                            const int uu = ol[kk];
+                            const int pp = pl[uu];
+                            kt32[2 * uu] = (pp != kNoPred ? kt32[2 * pp] : 0u) | (1u << uu);
+                        }
+#endif
+                    }
                     pending &= pending - 1;
                 }
                 wave_sync_s();
             }
+#ifdef TRX_AON_ANC
+            // ---------------- all-or-nothing (repair_env.py:490-502, 707-722) from the
+            // ancestor masks: the load of v's predecessor link is S(v) = the demands of
+            // every reached destination d whose path passes v (v in anc(d)); integral
+            // demands, exact.  Each lane sums S for its NPL nodes over all NP
+            // destinations (masks and demands broadcast within the quad by DPP), then
+            // adds them to the links with u32 LDS atomics: no sequential pass.
+            {
+                const float* dm = gdem + zi * N;
+                float un = 0.0f;
+                uint32_t ancv[NPL], dme[NPL], S[NPL];
+                read_keys<NPL>(kt + NPL * j, m);  // low words: ancestor masks of scanned nodes
+#pragma unroll
+                for (int i = 0; i < NPL; ++i) ancv[i] = (uint32_t)m[i];
+#pragma unroll
+                for (int i = 0; i < NPL; ++i) {
+                    const int v = NPL * j + i;
+                    const float dv = v < N ? dm[v] : 0.0f;
+                    const bool load = v < N && pl[v] != kNoPred;  // reached, not the origin
+                    un += (dv > 0.0f && !load) ? dv : 0.0f;      // intrazonal or unreachable (708)
+                    dme[i] = load ? (uint32_t)dv : 0u;
+                    S[i] = 0u;
+                }
+                const uint32_t sh = (uint32_t)(NPL * j);
+#define TRX_ANC_SRC(JJ)                                                              \
+    _Pragma("unroll") for (int ii = 0; ii < NPL; ++ii) {                             \
+        const uint32_t a_ = qps<(JJ) * 0x55>(ancv[ii]) >> sh;                        \
+        const uint32_t w_ = qps<(JJ) * 0x55>(dme[ii]);                               \
+        _Pragma("unroll") for (int i = 0; i < NPL; ++i) S[i] += ((a_ >> i) & 1u) * w_; \
+    }
+                TRX_ANC_SRC(0)
+                TRX_ANC_SRC(1)
+                TRX_ANC_SRC(2)
+                TRX_ANC_SRC(3)
+#undef TRX_ANC_SRC
+                uint32_t* const ll = sload + lenv * E;
+#pragma unroll
+                for (int i = 0; i < NPL; ++i) {
+                    const int v = NPL * j + i;
+                    const int pv = v < N ? pl[v] : kNoPred;
+                    if (pv != kNoPred) atomicAdd(ll + seid[pv * NP + v], S[i]);
+                }
+                unassigned_lane = un;
+            }
+#else
             // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree
             // demand sums S(v) per tree in reverse scan order (one lane per tree, plain
             // LDS read-modify-write); once S(v) is final it is added to the load of
@@ -497,6 +596,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 }
             }
             unassigned_lane = un;
+#endif
             TRX_SSTAMP(3);
         }
         __syncthreads();
@@ -605,6 +705,11 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     TRX_SSTAMP(6);
 }
 
+size_t sparse_workspace_bytes(const DevGraph& g, int num_envs) {
+    const LaunchCfg c = sparse_launch_cfg(g, num_envs, TRX_METHOD_MSA);
+    return (size_t)c.blocks * (size_t)(c.threads / 64) * sizeof(FibLane);
+}
+
 LaunchCfg sparse_launch_cfg(const DevGraph& g, int num_envs, int method) {
     LaunchCfg c{};
     c.np = g.NP;
@@ -625,7 +730,7 @@ LaunchCfg sparse_launch_cfg(const DevGraph& g, int num_envs, int method) {
 
 hipError_t launch_env_kernel_sparse(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs,
                                     int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
-                                    const uint8_t* env_mask, hipStream_t stream) {
+                                    const uint8_t* env_mask, void* ws, hipStream_t stream) {
     const LaunchCfg c = sparse_launch_cfg(g, num_envs, p.method);
     if (c.blocks == 0) return hipSuccess;
     if (c.threads > 256 || c.smem > 64 * 1024) return hipErrorInvalidConfiguration;
@@ -633,7 +738,7 @@ hipError_t launch_env_kernel_sparse(const DevGraph& g, const trx_params& p, cons
     const dim3 grid(c.blocks), block(c.threads);
 #define TRX_SPARSE_LAUNCH(NPV, RV)                                                                              \
     hipLaunchKernelGGL((env_kernel_s<NPV, RV>), grid, block, c.smem, stream, g, p, s, num_envs, c.epw, mode, \
-                       action, reward, done, valid, env_mask)
+                       action, reward, done, valid, env_mask, static_cast<unsigned char*>(ws))
 #define TRX_SPARSE_NP(NPV)             \
     if (R == 1)                        \
         TRX_SPARSE_LAUNCH(NPV, 1);     \

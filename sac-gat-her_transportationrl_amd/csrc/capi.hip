@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <string>
 #include <vector>
 
 #include "trx_internal.h"
@@ -90,19 +91,39 @@ int check_state(const trx_state* s, bool need_initial) {
     return TRX_OK;
 }
 
-// TRX_KERNEL selects earlier small-graph kernels for A/B runs: "quad" = env_kernel_q
-// for both shortest-path rules (instead of env_kernel_s / env_kernel_p for scipy and
-// env_kernel_t for torch), "packed" = env_kernel_p for the scipy rule.
-int kernel_choice() {  // 0 = current, 1 = packed, 2 = quad
-    static const int c = [] {
+// The env kernel a (graph, params) pair runs.  TRX_KERNEL=quad forces the
+// general quad kernel for both rules (A/B runs).
+enum EnvKernel { kEnvNone = 0, kEnvSparse, kEnvQuad, kEnvTorch, kEnvBig, kEnvGp };
+
+bool force_quad() {
+    static const bool q = [] {
         const char* e = getenv("TRX_KERNEL");
-        if (e && std::string(e) == "quad") return 2;
-        if (e && std::string(e) == "packed") return 1;
-        return 0;
+        return e && std::string(e) == "quad";
     }();
-    return c;
+    return q;
 }
-bool use_packed() { return kernel_choice() != 2; }
+
+EnvKernel select_env_kernel(const trx::DevGraph& g, const trx_params& p) {
+    const bool small = g.N <= trx::kSmallMaxNodes;
+    if (p.method == TRX_METHOD_GP) return small && g.E <= 128 && g.Z <= 256 ? kEnvGp : kEnvNone;
+    if (!small) return p.sp_rule == TRX_SP_SCIPY ? kEnvBig : kEnvNone;  // torch rule: N <= 32 only
+    if (!force_quad()) {
+        if (p.sp_rule == TRX_SP_TORCH && trx::torch_kernel_ok(g)) return kEnvTorch;
+        if (p.sp_rule == TRX_SP_SCIPY && trx::sparse_ok(g, p)) return kEnvSparse;
+    }
+    return trx::quad_ok(g, p.sp_rule) ? kEnvQuad : kEnvNone;
+}
+
+const char* env_kernel_label(EnvKernel k) {
+    switch (k) {
+        case kEnvSparse: return "env_kernel_s";
+        case kEnvQuad: return "env_kernel_q";
+        case kEnvTorch: return "env_kernel_t";
+        case kEnvBig: return "env_kernel_big";
+        case kEnvGp: return "gp_kernel";
+        default: return "";
+    }
+}
 
 int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mode, const int32_t* action,
         double* reward, uint8_t* done, uint8_t* valid, const uint8_t* env_mask, void* ws, void* stream) {
@@ -114,33 +135,34 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
     if (!ws) return fail(TRX_EINVAL, "workspace is NULL (size it with trx_workspace_bytes)");
     hipError_t e = hipSetDevice(g->device);
     if (e != hipSuccess) return fail(TRX_EHIP, "hipSetDevice: %s", hipGetErrorString(e));
-    if (p->method == TRX_METHOD_GP) {
-        if (g->dg.N > trx::kSmallMaxNodes || g->dg.E > 128 || g->dg.Z > 256)
-            return fail(TRX_EUNSUP, "GP assignment supports N <= %d, E <= 128 (got N=%d E=%d)",
-                        trx::kSmallMaxNodes, g->dg.N, g->dg.E);
-        if (!s->gp) return fail(TRX_EINVAL, "state.gp is NULL (size it with trx_gp_state_bytes)");
-        e = trx::launch_gp_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
-                                  static_cast<hipStream_t>(stream));
-    } else if (p->sp_rule == TRX_SP_TORCH && g->dg.N > trx::kSmallMaxNodes) {
-        return fail(TRX_EUNSUP, "sp_rule TORCH (all-pairs Floyd-Warshall) supports N <= %d (got N=%d)",
-                    trx::kSmallMaxNodes, g->dg.N);
-    } else if (p->sp_rule == TRX_SP_TORCH && use_packed() && trx::torch_kernel_ok(g->dg)) {
-        e = trx::launch_env_kernel_torch(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
-                                         static_cast<hipStream_t>(stream));
-    } else if (g->dg.N <= trx::kSmallMaxNodes && p->sp_rule == TRX_SP_SCIPY && kernel_choice() == 0 &&
-               trx::sparse_ok(g->dg, *p)) {
-        e = trx::launch_env_kernel_sparse(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
-                                          static_cast<hipStream_t>(stream));
-    } else if (g->dg.N <= trx::kSmallMaxNodes && p->sp_rule == TRX_SP_SCIPY && use_packed() &&
-               trx::packed_ok(g->dg, *p))
-        e = trx::launch_env_kernel_packed(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
-                                          static_cast<hipStream_t>(stream));
-    else if (g->dg.N <= trx::kSmallMaxNodes)
-        e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask,
-                                        static_cast<hipStream_t>(stream));
-    else
-        e = trx::launch_env_kernel_big(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws,
-                                       static_cast<hipStream_t>(stream));
+    const EnvKernel k = select_env_kernel(g->dg, *p);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    switch (k) {
+        case kEnvGp:
+            if (!s->gp) return fail(TRX_EINVAL, "state.gp is NULL (size it with trx_gp_state_bytes)");
+            e = trx::launch_gp_kernel(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, st);
+            break;
+        case kEnvTorch:
+            e = trx::launch_env_kernel_torch(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, st);
+            break;
+        case kEnvSparse:
+            e = trx::launch_env_kernel_sparse(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws, st);
+            break;
+        case kEnvQuad:
+            e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, st);
+            break;
+        case kEnvBig:
+            e = trx::launch_env_kernel_big(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws, st);
+            break;
+        default:
+            if (p->method == TRX_METHOD_GP)
+                return fail(TRX_EUNSUP, "GP assignment supports N <= %d, E <= 128 (got N=%d E=%d)",
+                            trx::kSmallMaxNodes, g->dg.N, g->dg.E);
+            if (p->sp_rule == TRX_SP_TORCH && g->dg.N > trx::kSmallMaxNodes)
+                return fail(TRX_EUNSUP, "sp_rule TORCH (all-pairs Floyd-Warshall) supports N <= %d (got N=%d)",
+                            trx::kSmallMaxNodes, g->dg.N);
+            return fail(TRX_EUNSUP, "graph (N=%d, E=%d) exceeds every env kernel's LDS budget", g->dg.N, g->dg.E);
+    }
     if (e != hipSuccess) return fail(TRX_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
@@ -397,23 +419,11 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     d.max_t0 = E > 0 ? mt : 1.0f;
     d.max_cap = E > 0 ? mc : 1.0f;
     d.min_t0 = mn;
-    // tie candidates of the packed-key kernel: every pair of in-links of a node
-    std::vector<uint32_t> tie_pairs;
-    if (small)
-        for (int v = 0; v < N; ++v)
-            for (int a = in_ptr[v]; a < in_ptr[v + 1]; ++a)
-                for (int b = a + 1; b < in_ptr[v + 1]; ++b) {
-                    const uint32_t e1 = (uint32_t)std::min(in_eid[a], in_eid[b]);
-                    const uint32_t e2 = (uint32_t)std::max(in_eid[a], in_eid[b]);
-                    tie_pairs.push_back(e1 | (e2 << 16));
-                }
-    d.npairs = (int)tie_pairs.size();
     d.max_out_deg = d.max_in_deg = 0;
     for (int u = 0; u < N; ++u) {
         d.max_out_deg = std::max(d.max_out_deg, out_ptr[u + 1] - out_ptr[u]);
         d.max_in_deg = std::max(d.max_in_deg, in_ptr[u + 1] - in_ptr[u]);
     }
-    if (tie_pairs.empty()) tie_pairs.push_back(0u);
     int rc = TRX_OK;
     std::vector<int32_t> vsrc(src, src + E), vdst(dst, dst + E);
     std::vector<float> vt0(t0, t0 + E), vcap(cap0, cap0 + E);
@@ -430,7 +440,7 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
         (rc = upload(g, od_dem, &d.od_dem)) || (rc = upload(g, b_origin, &d.b_origin)) ||
         (rc = upload(g, b_od_dst, &d.b_od_dst)) || (rc = upload(g, b_lsrc, &d.b_lsrc)) ||
         (rc = upload(g, b_indptr, &d.b_indptr)) || (rc = upload(g, b_indices, &d.b_indices)) ||
-        (rc = upload(g, b_csr_eid, &d.b_csr_eid)) || (rc = upload(g, tie_pairs, &d.tie_pairs))) {
+        (rc = upload(g, b_csr_eid, &d.b_csr_eid))) {
         trx_graph_destroy(g);
         return rc;
     }
@@ -462,7 +472,10 @@ int trx_graph_info(const trx_graph* g, int32_t* num_nodes, int32_t* num_edges, i
 
 int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs) {
     if (!g || num_envs < 0) return fail(TRX_EINVAL, "bad arguments");
-    if (g->dg.N <= trx::kSmallMaxNodes) return 256;  // all per-env work lives in LDS
+    // small graphs: per-env work lives in LDS; the sparse kernel's rare exact-heap
+    // replays use one FibLane per wave here
+    if (g->dg.N <= trx::kSmallMaxNodes)
+        return (int64_t)std::max<size_t>(256, trx::sparse_workspace_bytes(g->dg, num_envs));
     // large graphs: one exact-heap scratch slot per wave (rarely touched)
     return (int64_t)std::max<size_t>(256, trx::big_workspace_bytes(g->dg, num_envs));
 }
@@ -474,6 +487,11 @@ int64_t trx_gp_state_bytes(const trx_graph* g, int32_t num_envs, int32_t keep_pa
     if (g->dg.N > trx::kSmallMaxNodes || g->dg.E > 128)
         return fail(TRX_EUNSUP, "GP assignment supports N <= %d, E <= 128", trx::kSmallMaxNodes);
     return (int64_t)num_envs * (int64_t)trx::gp_layout(g->dg.P, keep_paths).total;
+}
+
+const char* trx_env_kernel_name(const trx_graph* g, const trx_params* p) {
+    if (!g || check_params(p)) return "";
+    return env_kernel_label(select_env_kernel(g->dg, *p));
 }
 
 int trx_assign(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, const uint8_t* env_mask, void* ws,

@@ -58,14 +58,9 @@ struct DevGraph {
     const float* od_dem;        // [P]
     double total_demand;        // float(np.sum(list(od_demand.values())))
     float max_t0, max_cap;      // RepairEnv.max_t0 / max_capacity
-    float min_t0;               // smallest free-flow time (exact-label headroom, assign_packed.hip)
-    int npairs;                 // in-link pairs of a common head (tie candidates), N <= kSmallMaxNodes
-    const uint32_t* tie_pairs;  // [npairs] e1 | e2 << 16, e1 < e2, dst[e1] == dst[e2]
+    float min_t0;               // smallest free-flow time (exact-label headroom, assign_sparse.hip)
     int max_out_deg, max_in_deg;  // largest out-/in-degree (sparse-relaxation kernel tables)
 };
-
-// Largest tie-candidate pair list of the packed-key kernel (LDS budget).
-constexpr int kMaxTiePairs = 2048;
 
 // Per-lane Fibonacci-heap state for the exact (scipy-order) SSSP fallback.
 struct FibLane {
@@ -122,17 +117,21 @@ struct LaunchCfg {
     int blocks;    // grid
 };
 
+// Small-graph (N <= kSmallMaxNodes) env kernels, selected per graph and
+// parameters by capi.hip select_env_kernel():
+//   scipy rule: env_kernel_s (assign_sparse.hip) when sparse_ok(), else
+//               env_kernel_q (assign_quad.hip, no exact-label / degree limits);
+//   torch rule: env_kernel_t (assign_torch.hip) when torch_kernel_ok(), else
+//               env_kernel_q's torch-rule instantiation.
 LaunchCfg quad_launch_cfg(const DevGraph& g, int num_envs, int sp_rule);
-bool packed_ok(const DevGraph& g, const trx_params& p);
-LaunchCfg packed_launch_cfg(const DevGraph& g, int num_envs, int method);
+bool quad_ok(const DevGraph& g, int sp_rule);  // LDS / block-size budget of env_kernel_q
+bool exact_label_ok(const DevGraph& g, const trx_params& p);
 bool sparse_ok(const DevGraph& g, const trx_params& p);
 LaunchCfg sparse_launch_cfg(const DevGraph& g, int num_envs, int method);
 hipError_t launch_env_kernel_sparse(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs,
                                     int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
-                                    const uint8_t* env_mask, hipStream_t stream);
-hipError_t launch_env_kernel_packed(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs,
-                                   int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
-                                   const uint8_t* env_mask, hipStream_t stream);
+                                    const uint8_t* env_mask, void* workspace, hipStream_t stream);
+size_t sparse_workspace_bytes(const DevGraph& g, int num_envs);  // exact-heap scratch, one FibLane per wave
 hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream);

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 4
+ABI_VERSION = 5
 SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
@@ -29,7 +29,7 @@ EXPORTS = (
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
-    "trx_damage_sample", "trx_multi_gather", "trx_episode_step",
+    "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
 )
 
 
@@ -181,6 +181,8 @@ def load():
     L = ctypes.CDLL(LIB_PATH)
     L.trx_abi_version.restype = ctypes.c_int32
     L.trx_last_error.restype = ctypes.c_char_p
+    L.trx_env_kernel_name.argtypes = [_vp, ctypes.POINTER(TrxParams)]
+    L.trx_env_kernel_name.restype = ctypes.c_char_p
     L.trx_graph_create.argtypes = [ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp,
                                    ctypes.POINTER(_vp)]
     L.trx_graph_destroy.argtypes = [_vp]

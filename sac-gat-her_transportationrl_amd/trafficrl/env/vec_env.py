@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from .. import _lib
-from ..graph import DamageSampler, TrafficGraph, damage_sample_batch, pcg_states
+from ..graph import DamageSampler, TrafficGraph, damage_sample_batch, pcg_states, set_generator_state
 
 
 def resolve_sp_rule(sp_backend: Optional[str], num_nodes: int, force_gpu_sp: bool = False) -> int:
@@ -151,10 +151,24 @@ class VecRepairEnv:
 
     @property
     def samplers(self):
+        """Per-env DamageSampler objects.  Built lazily; when native batch draws
+        have already advanced the envs' generators (_rng_states), the samplers
+        continue from those states and become the only RNG record, so no reset
+        ever repeats a damage set already drawn."""
         if self._samplers is None:
             fd, fds = self._fixed
             self._samplers = [DamageSampler(self.graph, int(s), fd, fds) for s in self._seeds]
+            if self._rng_states is not None:
+                for smp, rec in zip(self._samplers, self._rng_states):
+                    set_generator_state(smp.rng, rec)
+                self._rng_states = None
         return self._samplers
+
+    @property
+    def kernel_name(self) -> str:
+        """The env kernel trx_step / trx_reset / trx_assign launch for this
+        graph and parameters (trx_env_kernel_name)."""
+        return _lib.load().trx_env_kernel_name(self.graph.handle, ctypes.byref(self.params)).decode()
 
     def _obs_buffers(self):
         if self._obs_bufs is None:

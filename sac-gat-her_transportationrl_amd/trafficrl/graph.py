@@ -123,6 +123,8 @@ def damage_sample_batch(num_nodes: int, src: np.ndarray, dst: np.ndarray, states
     in place exactly as each env's numpy Generator would."""
     E = len(src)
     count = max(1, int(E * damaged_ratio))
+    if E > 10000:   # numpy's choice leaves its Floyd branch above 10000 (not restated natively)
+        raise ValueError(f"damage draws support num_edges <= 10000 (numpy Generator.choice Floyd branch); got {E}")
     if not (isinstance(states, np.ndarray) and states.dtype == PCG64_DTYPE and states.flags.c_contiguous):
         raise TypeError("states must be a C-contiguous PCG64_DTYPE array (pcg_states)")
     src = np.ascontiguousarray(src, np.int32)

@@ -5,6 +5,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so
+sha256sum $LIB | cut -c1-16 > gpurun_out/lib_sha16.txt
 step() {  # step <name> <timeout-seconds> <cmd...>
     local name=$1 secs=$2; shift 2
     echo "=== $name ($(date +%T))"
@@ -56,15 +58,11 @@ for s in "$@"; do
         istamps) step istamps 300 python tools/infer_stamps.py 4096 ;;
         abact) TRX_LIB=${TRX_LIB_A:-} step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act
                TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
-        abs) step ab_sparse 200 python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 && step ab_packed 200 env TRX_KERNEL=packed python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
-        abk) step ab_quad 200 env TRX_KERNEL=quad python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 && step ab_packed 200 python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
+        abk) step ab_quad 200 env TRX_KERNEL=quad python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
+        fallback) step fallback_tests 400 python -u -m pytest tests/test_gpu_fallback.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         abt) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step abt_$n 200 python tools/ab_env.py $f 4096 20 torch || exit 1; done ;;
         abo) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step abo_$n 200 python tools/ab_env.py $f 4096 30 obs || exit 1; done ;;
         abx) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step ab_$n 200 python tools/ab_env.py $f 4096 30 || exit 1; done ;;
-        pmcab) for k in sparse packed; do
-                 step pmc_${k}_1 200 env TRX_KERNEL=$k rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d gpurun_out/pmc_${k}_1 -o run --output-format csv -- python3 tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 6 || exit 1
-                 step pmc_${k}_2 200 env TRX_KERNEL=$k rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_${k}_2 -o run --output-format csv -- python3 tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 6 || exit 1
-               done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -44,6 +44,11 @@ if "SQ_WAVE_CYCLES" in mean:
     out["wait_any_frac"] = mean.get("SQ_WAIT_ANY", 0) / w
     out["active_inst_any_frac"] = mean.get("SQ_ACTIVE_INST_ANY", 0) / w
     out["wait_inst_any_frac"] = mean.get("SQ_WAIT_INST_ANY", 0) / w
+# the library the passes ran (tools/gpu_session.sh writes its hash on the box);
+# bench.py attaches these counters only to runs of the same binary
+sha_file = os.path.join(root, "gpurun_out", "lib_sha16.txt")
+if os.path.exists(sha_file):
+    out["lib_sha16"] = open(sha_file).read().split()[0]
 path = os.path.join(root, "profiles", f"{tag}_pmc.json")
 json.dump(out, open(path, "w"), indent=1)
 print(json.dumps(out, indent=1))
