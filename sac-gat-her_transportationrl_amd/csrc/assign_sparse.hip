@@ -393,18 +393,10 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 const uint64_t best = dbits_s(bd);
                 const uint32_t u = (uint32_t)best & 31u;
                 // one lane of the quad stores the scan order and the scanned mark
-#ifdef TRX_AON_ANC
-                // scanned mark: the high word keeps 19 label bits (bits 5..23 of the
-                // low word) for the tie check; the low word receives the node's
-                // ancestor mask at the end of the step
-                if (j == 0) kt32[2 * u + 1] = kScannedHi | (((uint32_t)best >> 5) & 0x7FFFFu);
-                const uint32_t pu = pl[u];
-#else
                 if (j == 0) {
                     ol[k] = (uint8_t)u;
                     kt32[2 * u + 1] = kScannedHi;
                 }
-#endif
                 nscan = k + 1;
                 const uint64_t lb = best & ~31ull;
                 const double bl = bitsd_s(lb);
@@ -442,10 +434,6 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                         was[r] = __hip_atomic_fetch_min(reinterpret_cast<long long*>(kt + v[r]), nk[r],
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-#ifdef TRX_AON_ANC
-                // ancestor mask of u's predecessor (scanned earlier: its low word is final)
-                const uint32_t ap = kt32[2 * (pu < (uint32_t)NP ? pu : 0u)];
-#endif
                 // next step's keys: issued behind the mark and the atomics (a wave's LDS
                 // operations complete in order), before waiting on the atomics' results
                 read_keys<NPL>(kt + NPL * j, m);
@@ -457,16 +445,8 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                     if (nk[r] < was[r]) pl[v[r]] = (uint8_t)u;
                     // (scanned keys keep their low word: equal low label bits = maybe equal
                     // labels; a false positive costs one exact replay, never a wrong tree)
-#ifdef TRX_AON_ANC
-                    if (nk[r] == was[r])
-                        amb |= ((kt32[2 * pl[v[r]] + 1] ^ ((uint32_t)lb >> 5)) & 0x7FFFFu) == 0u;
-#else
                     if (nk[r] == was[r]) amb |= ((kt32[2 * pl[v[r]]] ^ (uint32_t)lb) & ~31u) == 0u;
-#endif
                 }
-#ifdef TRX_AON_ANC
-                if (j == 0) kt32[2 * u] = (pu < (uint32_t)NP ? ap : 0u) | (1u << u);
-#endif
             }
             wave_sync_s();
             TRX_SSTAMP(1);
@@ -489,65 +469,11 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                     const int leader = __ffsll((unsigned long long)pending) - 1;
                     if ((tid & 63) == leader) {
                         replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
-#ifdef TRX_AON_ANC
-                        // the replayed tree's ancestor masks, in its scan order, into the
-                        // low words of its (scanned) keys
-                        for (int kk = 0; kk < nscan; ++kk) {
-                            const int uu = ol[kk];
-                            const int pp = pl[uu];
-                            kt32[2 * uu] = (pp != kNoPred ? kt32[2 * pp] : 0u) | (1u << uu);
-                        }
-#endif
                     }
                     pending &= pending - 1;
                 }
                 wave_sync_s();
             }
-#ifdef TRX_AON_ANC
-            // ---------------- all-or-nothing (repair_env.py:490-502, 707-722) from the
-            // ancestor masks: the load of v's predecessor link is S(v) = the demands of
-            // every reached destination d whose path passes v (v in anc(d)); integral
-            // demands, exact.  Each lane sums S for its NPL nodes over all NP
-            // destinations (masks and demands broadcast within the quad by DPP), then
-            // adds them to the links with u32 LDS atomics: no sequential pass.
-            {
-                const float* dm = gdem + zi * N;
-                float un = 0.0f;
-                uint32_t ancv[NPL], dme[NPL], S[NPL];
-                read_keys<NPL>(kt + NPL * j, m);  // low words: ancestor masks of scanned nodes
-#pragma unroll
-                for (int i = 0; i < NPL; ++i) ancv[i] = (uint32_t)m[i];
-#pragma unroll
-                for (int i = 0; i < NPL; ++i) {
-                    const int v = NPL * j + i;
-                    const float dv = v < N ? dm[v] : 0.0f;
-                    const bool load = v < N && pl[v] != kNoPred;  // reached, not the origin
-                    un += (dv > 0.0f && !load) ? dv : 0.0f;      // intrazonal or unreachable (708)
-                    dme[i] = load ? (uint32_t)dv : 0u;
-                    S[i] = 0u;
-                }
-                const uint32_t sh = (uint32_t)(NPL * j);
-#define TRX_ANC_SRC(JJ)                                                              \
-    _Pragma("unroll") for (int ii = 0; ii < NPL; ++ii) {                             \
-        const uint32_t a_ = qps<(JJ) * 0x55>(ancv[ii]) >> sh;                        \
-        const uint32_t w_ = qps<(JJ) * 0x55>(dme[ii]);                               \
-        _Pragma("unroll") for (int i = 0; i < NPL; ++i) S[i] += ((a_ >> i) & 1u) * w_; \
-    }
-                TRX_ANC_SRC(0)
-                TRX_ANC_SRC(1)
-                TRX_ANC_SRC(2)
-                TRX_ANC_SRC(3)
-#undef TRX_ANC_SRC
-                uint32_t* const ll = sload + lenv * E;
-#pragma unroll
-                for (int i = 0; i < NPL; ++i) {
-                    const int v = NPL * j + i;
-                    const int pv = v < N ? pl[v] : kNoPred;
-                    if (pv != kNoPred) atomicAdd(ll + seid[pv * NP + v], S[i]);
-                }
-                unassigned_lane = un;
-            }
-#else
             // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree
             // demand sums S(v) per tree in reverse scan order (one lane per tree, plain
             // LDS read-modify-write); once S(v) is final it is added to the load of
@@ -596,7 +522,6 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 }
             }
             unassigned_lane = un;
-#endif
             TRX_SSTAMP(3);
         }
         __syncthreads();

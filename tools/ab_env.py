@@ -43,4 +43,15 @@ for r in range(reps):
     torch.cuda.synchronize()
     ms.append(s.elapsed_time(e))
 ms = sorted(ms)[2:-2]
-print(f"{os.path.basename(sys.argv[1])} [{sp}]: step kernel {sum(ms) / len(ms):.4f} ms (B={B})")
+# result checksum (variants must agree bit for bit): the timed step's state, then a
+# cold reset with per-env random damage (tie-heavy: exercises the exact-heap replays)
+import hashlib  # noqa: E402
+import numpy as np  # noqa: E402
+h = hashlib.sha1(env.flow.cpu().numpy().tobytes() + env.tstt.cpu().numpy().tobytes())
+rng = np.random.default_rng(5)
+dmg = np.zeros((B, 76), np.float32)
+for b in range(B):
+    dmg[b, rng.choice(76, 22, replace=False)] = 1.0
+env.reset(damaged=torch.from_numpy(dmg), observe=False)
+h.update(env.flow.cpu().numpy().tobytes() + env.tstt.cpu().numpy().tobytes())
+print(f"{os.path.basename(sys.argv[1])} [{sp}]: step kernel {sum(ms) / len(ms):.4f} ms (B={B}) sha {h.hexdigest()[:12]}")

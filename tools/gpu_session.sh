@@ -62,6 +62,10 @@ for s in "$@"; do
         fallback) step fallback_tests 400 python -u -m pytest tests/test_gpu_fallback.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         abt) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step abt_$n 200 python tools/ab_env.py $f 4096 20 torch || exit 1; done ;;
         abo) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step abo_$n 200 python tools/ab_env.py $f 4096 30 obs || exit 1; done ;;
+        abv) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); case $n in *stamps*) continue;; esac; step ab_$n 200 python tools/ab_env.py $f 4096 30 || exit 1; done
+             grep -h "step kernel" gpurun_out/ab_*.log ;;
+        vtest) cp sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_${VARIANT}.so $LIB && sha256sum $LIB | cut -c1-16 > gpurun_out/lib_sha16.txt
+               step vtest_$VARIANT 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sparse.py tests/test_gpu_fallback.py tests/test_torch_sp.py tests/test_gpu_large.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         abx) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step ab_$n 200 python tools/ab_env.py $f 4096 30 || exit 1; done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
