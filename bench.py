@@ -94,6 +94,17 @@ def host_cores():
     return max(1, n), vis
 
 
+def sac_update_flops(bs, N, E, hidden=256, heads=4, embed=256, edge_in=6):
+    """Dense GEMM FLOPs of one SAC update (src/rl/sac.py:157-243) at batch bs
+    with this build's per-node factoring of the edge MLP: per graph forward the
+    GAT lin layers (4 -> H*C is negligible), the edge head's node projection
+    and context product, the link-feature product; 6 forwards (next actor, 2
+    targets, 2 critics, actor) + 3 backwards at 2x their forward."""
+    hc = heads * hidden
+    per_graph = 2 * N * (hc * hc + hc * embed + embed * 2 * hidden) + 2 * (2 * embed * hidden) + 2 * E * edge_in * hidden
+    return float(bs * per_graph * (6 + 3 * 2))
+
+
 def cpu_baseline(network, method, iters, seconds=12.0, sp="scipy"):
     """Time the oracle's C restatement (same algorithm as the reference:
     scipy-order Dijkstra or the torch rule's Floyd-Warshall, predecessor /
@@ -218,6 +229,103 @@ def env_kernel_name(env, big):
     return f"trx::{k}"
 
 
+def cpu_greedy_episode(method, iters, nthreads):
+    """The greedy one-step episode (src/baselines/__init__.py:35-69 driven by
+    run_episode 72-101) on the oracle's C restatement: per decision one
+    warm-started assignment per damaged candidate (a batch over the host
+    threads), the first strict TSTT minimum, then the step's own assignment.
+    Returns (seconds, actions, tstt curve)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test/baseline infrastructure only
+
+    npz = os.path.join(ROOT, "tests", "golden", NETWORKS["sf"][1])
+    og = O.OracleGraph.from_npz(npz)
+    cap0 = np.load(npz)["cap0"].astype(np.float32)
+    dmg = fixed_damage_mask(load_network("sf"))
+    t0 = time.perf_counter()
+    cap = np.where(dmg > 0, np.float32(1e-3), cap0).astype(np.float32)
+    flow, _, _, _ = og.assign(cap, dmg, np.zeros_like(dmg), method=method, iters=iters)
+    actions, curve = [], []
+    while dmg.sum() > 0:
+        cand = np.flatnonzero(dmg)
+        C, D = np.repeat(cap[None], len(cand), 0), np.repeat(dmg[None], len(cand), 0)
+        C[np.arange(len(cand)), cand] = cap0[cand]
+        D[np.arange(len(cand)), cand] = 0.0
+        _, _, ts, _ = og.assign(C, D, np.repeat(flow[None], len(cand), 0), method=method, iters=iters,
+                                nthreads=nthreads)
+        a = int(cand[int(np.argmin(ts))])
+        cap[a], dmg[a] = cap0[a], 0.0
+        flow, _, tstt, _ = og.assign(cap, dmg, flow, method=method, iters=iters)
+        actions.append(a)
+        curve.append(float(tstt))
+    return time.perf_counter() - t0, actions, curve
+
+
+def run_greedy(args):
+    """Config #1 (configs/sioux_falls.yaml via run_greedy.py:47-121): one Sioux
+    Falls env, fixed_damage_seed=42, the greedy one-step baseline through the
+    drop-in RepairEnv facade (trafficrl/baselines: one batched trx_assign per
+    decision over the damaged candidates, then RepairEnv.step).  A step =
+    one greedy decision + the env step.  Timed: whole episodes (reset + 22
+    decisions = 276 assignments) after one warm-up episode; the actions and
+    TSTT curve are checked against the reference's own episode
+    (tests/golden/sf_greedy_<method><K>_crpow.npz)."""
+    from trafficrl.baselines import run_episode, select_greedy_one_step
+    from trafficrl.env import RepairEnv
+    method, K = args.method, args.iters
+    env = RepairEnv(load_network("sf"), assignment_iters=K, assignment_method=method, fixed_damage=True,
+                    fixed_damage_seed=42, seed=42, reward_mode="rel_improve", reward_alpha=1.0, reward_beta=0.0,
+                    reward_gamma=0.0, reward_clip=2.0, unassigned_penalty=1e4, sp_backend=args.sp)
+    acts = []
+
+    def pol(s):
+        a = select_greedy_one_step(env, s)
+        acts.append(a)
+        return a
+
+    out = run_episode(env, pol)           # warm-up episode (and the trajectory checked below)
+    torch.cuda.synchronize()
+    ref = os.path.join(ROOT, "tests", "golden", f"sf_greedy_{method}{K}_crpow.npz")
+    check = None
+    if os.path.exists(ref) and args.sp == "scipy":
+        z = np.load(ref)
+        check = bool(acts == z["actions"].tolist() and np.array_equal(np.array(out["tstt_curve"]), z["tstt"]))
+    episodes = max(1, -(-args.steps // len(acts)))
+    t0 = time.perf_counter()
+    for _ in range(episodes):
+        run_episode(env, lambda s: select_greedy_one_step(env, s))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = episodes * len(acts)
+    assigns = episodes * (1 + sum(int(env.num_edges * 0.3) - i + 1 for i in range(len(acts))))
+    cpu = None
+    if not args.no_cpu:
+        threads, visible = host_cores()
+        cs, cacts, ccurve = cpu_greedy_episode(method, K, threads)
+        cpu = {"value": len(cacts) / cs, "unit": "env steps/s", "cores": threads, "kind": "port",
+               "episode_s": cs, "decision_s": cs / len(cacts), "host_cpus_visible": visible,
+               "same_trajectory": bool(cacts == acts),
+               "sample": f"one greedy {method.upper()}-{K} episode (reset + {len(cacts)} decisions) on the C "
+                         f"restatement, candidates batched over {threads} host threads; oracle/trx_oracle.c"}
+    return {
+        "metric": METRIC, "value": steps / dt, "unit": "env steps/s", "n_gpus": 1, "steps": steps,
+        "warmup": len(acts), "ms_per_step": dt / steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32 (link flows/costs) + f64 (path labels)",
+        "data": "synthetic: Sioux Falls TNTP, fixed_damage_seed=42",
+        "config": {"workload": f"config #1: SF 1 env, greedy one-step baseline, {method.upper()}-{K} "
+                               f"({args.sp} shortest-path rule), drop-in RepairEnv facade",
+                   "workload_kind": "greedy", "envs_per_gpu": 1, "method": method, "assignment_iters": K,
+                   "network": NETWORKS["sf"][2], "parallelism": "single env"},
+        "greedy": {"episode_s": dt / episodes, "decision_s": dt / steps, "decisions_per_s": steps / dt,
+                   "assigns_per_s": assigns / dt, "assigns_per_episode": assigns // episodes,
+                   "episodes_timed": episodes, "matches_reference_episode": check,
+                   "reference_cpu_decision_s": 1.63, "reference_cpu_episode_s": 21.52,
+                   "reference_note": "SURVEY.md §6 / BASELINE.md: the reference's greedy MSA-30 episode on 1 core "
+                                     "of this container (scipy rule)"},
+        "cpu_baseline": cpu,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,7 +343,9 @@ def main():
     ap.add_argument("--no-observe", action="store_true", help="skip get_state (assignment-only steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", default=None, choices=["train", "env"], help="default train (sf) / env (anaheim)")
+    ap.add_argument("--workload", default=None, choices=["train", "env", "greedy"],
+                    help="default train (sf) / env (anaheim); greedy = config #1 (one env, greedy baseline; "
+                         "--iters 60 is configs/sioux_falls.yaml's K)")
     ap.add_argument("--damage", default="fixed", choices=["fixed", "random"],
                     help="env workload: fixed = fixed_damage_seed=42 for every env; random = per-env "
                          "default_rng(1000 + global env id) draws at every reset (host-side, repair_env.py:167-192; "
@@ -248,6 +358,11 @@ def main():
         args.method = "fw" if big else "msa"
     if args.workload is None:
         args.workload = "env" if big else "train"
+
+    if args.workload == "greedy":
+        torch.cuda.set_device(0)
+        print(json.dumps(run_greedy(args)), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -403,6 +518,21 @@ def main():
     valu_frac = pmc.get("valu_busy_frac") if pmc else None
     lds_conf = pmc.get("lds_bank_conflict_frac") if pmc else None
     mfma = gemm_mfma(B * N, B) if (args.workload == "train" and rank == 0) else None
+    upd_stats = None
+    if args.workload == "train" and phase_ev.get("update"):
+        # SAC update throughput (the timed updates are graph replays), and the env
+        # steps/s this GPU would sustain at the reference's update-to-data ratio
+        # (configs/sioux_falls.yaml:17-18 update_every 4, updates_per_step 1: one
+        # update per 4 transitions, src/train.py:954-955) instead of the bench's 1/(4B)
+        upd_ms = [s_.elapsed_time(e_) for s_, e_ in phase_ev["update"]]
+        ms_upd = float(np.mean(upd_ms))
+        ms_rest = elapsed / args.steps * 1e3 - float(np.sum(upd_ms)) / args.steps   # one iteration without updates
+        flops = sac_update_flops(int(cfg["batch_size"]), N, E)
+        upd_stats = {"ms_per_update": ms_upd, "updates_per_s": 1e3 / ms_upd, "updates_timed": len(upd_ms),
+                     "flops_per_update": flops, "mfma_frac": flops / (ms_upd / 1e3) / MFMA_PEAK_BF16,
+                     "env_steps_per_s_at_reference_utd": 1e3 / (ms_rest / B + ms_upd / 4.0),
+                     "note": "mfma_frac: GEMM FLOPs of 3 no-grad + 3 training forwards and 3 backwards "
+                             "(2x forward) at batch 256 / the update's wall time / 2.5 PF dense bf16"}
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu:
@@ -455,6 +585,8 @@ def main():
             "cpu_baseline": cpu,
             "breakdown_ms_per_step": dict(breakdown, env_kernel=mean_kernel_s * 1e3 * len(kern_ms) / args.steps),
         }
+        if args.workload == "train" and upd_stats is not None:
+            out["sac_update"] = upd_stats
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

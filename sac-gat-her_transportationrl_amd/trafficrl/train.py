@@ -363,27 +363,31 @@ class Trainer:
     def updates_due(self, it: int) -> int:
         """SAC updates to run after iteration `it` (its B transitions added).
 
-        update_unit "transitions" (default) keeps the reference's
-        update-to-data ratio: src/train.py:954-955 runs `updates_per_step`
-        updates every `update_every` env steps of its single env.  Here the
-        B transitions of an iteration count as B consecutive env steps, so
-        after the iteration that takes the transition count from T0 to T1,
-        floor(T1 / update_every) - floor(T0 / update_every) update rounds of
-        `updates_per_step` updates are due (B = 1 reproduces the reference's
-        timing).
+        update_unit "transitions" (default) follows the reference's serial
+        loop (src/train.py:915-955) per env: each env keeps its own episode
+        step counter (ep_len, reset with the episode, like `steps = 0` at
+        train.py:919); after an env's step, `updates_per_step` updates are due
+        when ep_len % update_every == 0 -- except on a step that truncates the
+        episode (max_steps reached and not done: the reference breaks out of
+        the episode before its update check, 950-952).  The iteration's count
+        is the sum over envs, so B = 1 reproduces the reference's schedule
+        (e.g. 5 updates per 22-step episode at update_every 4).
         update_unit "iterations": `updates_per_step` updates every
         `update_every` vector iterations (B transitions each) -- the bench's
         throughput workload, a UTD ratio B * update_every times lower.
         No update until the replay holds more than batch_start transitions."""
         cfg = self.cfg
         ups, every = int(cfg["updates_per_step"]), int(cfg["update_every"])
-        t0 = self._transitions
-        self._transitions = t1 = t0 + self.B
+        self._transitions += self.B
         if self.replay.size <= int(cfg["batch_start"]):
             return 0
         if str(cfg.get("update_unit", "transitions")) == "iterations":
             return ups if it % every == 0 else 0
-        return (t1 // every - t0 // every) * ups
+        due = (self.ep_len % every) == 0
+        ms = int(cfg["max_steps"])
+        if ms > 0:
+            due &= ~((self.ep_len >= ms) & ~self.env.done)
+        return int(due.sum().item()) * ups
 
     def prime_update(self):
         """Run the eager warm-up updates and the HIP-graph capture now, so that
@@ -564,7 +568,10 @@ class Trainer:
                                          f"improvement for {patience} episodes")
                     break
             if not stop and self.episodes_done >= next_eval and cfg["eval_every"] > 0:
-                next_eval += int(cfg["eval_every"])
+                # evaluations happen at iteration granularity: the next one after the
+                # next multiple of eval_every episodes (src/train.py evaluates every
+                # eval_every episodes; many envs finish episodes together here)
+                next_eval = (self.episodes_done // int(cfg["eval_every"]) + 1) * int(cfg["eval_every"])
                 ev = self.evaluate()
                 if self.rank == 0:
                     self.logger.info(f"eval {ev}")

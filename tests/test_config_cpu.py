@@ -37,20 +37,44 @@ def test_sf_config_mirrors_reference_yaml():
 
 
 def _fake(B, size, **cfg):
-    base = dict(batch_start=100, updates_per_step=1, update_every=4, update_unit="transitions")
+    import torch
+    base = dict(batch_start=100, updates_per_step=1, update_every=4, update_unit="transitions", max_steps=0)
     base.update(cfg)
-    return SimpleNamespace(cfg=base, B=B, replay=SimpleNamespace(size=size), _transitions=0)
+    return SimpleNamespace(cfg=base, B=B, replay=SimpleNamespace(size=size), _transitions=0,
+                           ep_len=torch.zeros(B, dtype=torch.int64),
+                           env=SimpleNamespace(done=torch.zeros(B, dtype=torch.bool)))
 
 
-def test_update_schedule_transitions_keeps_reference_ratio():
-    # reference: updates_per_step updates every update_every env steps (src/train.py:954-955)
-    f = _fake(B=10, size=1000)
-    n = [Trainer.updates_due(f, it) for it in range(8)]
-    assert sum(n) == 10 * 8 // 4 and n[:4] == [2, 3, 2, 3]
+def _episode(f, steps, done_at=None):
+    """Drive updates_due through one episode per env (ep_len as trx_episode_step advances it)."""
+    out = []
+    for it in range(steps):
+        f.ep_len += 1
+        if done_at is not None:
+            f.env.done = f.ep_len >= done_at
+        out.append(Trainer.updates_due(f, it))
+    return out
+
+
+def test_update_schedule_transitions_follows_reference_episode_counter():
+    # reference serial loop (src/train.py:919, 954-955): per-episode `steps`, an update
+    # whenever steps % update_every == 0 -> 5 updates in a 22-step episode at update_every 4
+    f = _fake(B=1, size=1000)
+    n = _episode(f, 22, done_at=22)
+    assert sum(n) == 5 and [i + 1 for i, k in enumerate(n) if k] == [4, 8, 12, 16, 20]
     f = _fake(B=1, size=1000, updates_per_step=2)
-    assert [Trainer.updates_due(f, it) for it in range(8)] == [0, 0, 0, 2, 0, 0, 0, 2]
+    assert _episode(f, 8) == [0, 0, 0, 2, 0, 0, 0, 2]
+    # envs at different episode offsets: the iteration's count sums over envs
+    f = _fake(B=3, size=1000)
+    f.ep_len[:] = __import__("torch").tensor([0, 1, 3])
+    assert _episode(f, 4) == [1, 0, 1, 1]   # counters 1,2,4 -> 2,3,5 -> 3,4,6 -> 4,5,7
+    # truncation (max_steps reached, not done) breaks out before the update check (950-952)
+    f = _fake(B=1, size=1000, max_steps=8)
+    assert _episode(f, 8) == [0, 0, 0, 1, 0, 0, 0, 0]
+    f = _fake(B=1, size=1000, max_steps=8)
+    assert _episode(f, 8, done_at=8) == [0, 0, 0, 1, 0, 0, 0, 1]   # done on the last step: updated
     f = _fake(B=10, size=50)      # replay not yet past batch_start
-    assert Trainer.updates_due(f, 0) == 0 and f._transitions == 10
+    assert _episode(f, 4) == [0, 0, 0, 0] and f._transitions == 40
 
 
 def test_update_schedule_iterations():
