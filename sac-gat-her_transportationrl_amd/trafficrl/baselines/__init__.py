@@ -17,23 +17,32 @@ from ..env.repair_env import EnvState, RepairEnv
 from ..env.vec_env import VecRepairEnv
 
 
+def _best_masked(score: np.ndarray, mask: np.ndarray) -> int:
+    """Index of the largest score among masked-in links (score * mask, first
+    maximum: np.argmax semantics of src/baselines/__init__.py:16-32)."""
+    return int(np.argmax(score * mask))
+
+
 def select_random(state: EnvState) -> int:
-    candidates = np.where(state.action_mask > 0)[0]
-    return int(np.random.choice(candidates))
+    """Uniform draw over the repairable links from numpy's global RNG (11-13)."""
+    return int(np.random.choice(np.flatnonzero(state.action_mask > 0)))
 
 
 def select_max_vc(state: EnvState) -> int:
-    return int(np.argmax(state.edge_features[:, 2] * state.action_mask))
+    """Largest clipped log(1 + v/c) feature (edge feature 2; 16-19)."""
+    return _best_masked(state.edge_features[:, 2], state.action_mask)
 
 
 def select_max_flow(state: EnvState) -> int:
-    return int(np.argmax(state.edge_features[:, 2] * state.edge_features[:, 1] * state.action_mask))
+    """Largest v/c feature x normalised capacity feature (a flow proxy; 22-25)."""
+    ef = state.edge_features
+    return _best_masked(ef[:, 2] * ef[:, 1], state.action_mask)
 
 
 def select_max_betweenness(state: EnvState, node_betweenness: np.ndarray, edge_index: np.ndarray) -> int:
-    src, dst = edge_index
-    edge_bw = (node_betweenness[src] + node_betweenness[dst]) / 2.0
-    return int(np.argmax(edge_bw * state.action_mask))
+    """Largest mean betweenness of the link's two end nodes (28-32)."""
+    bw = 0.5 * (node_betweenness[edge_index[0]] + node_betweenness[edge_index[1]])
+    return _best_masked(bw, state.action_mask)
 
 
 class WhatIfBatch:
@@ -135,33 +144,30 @@ def greedy_actions(venv: VecRepairEnv, batch: WhatIfBatch | None = None) -> torc
 
 def run_episode(env: RepairEnv, policy: Callable[[EnvState], int], reward_scale: float = 1.0,
                 max_steps: int = 0) -> Dict:
-    tstt_curve: List[float] = []
+    """One episode of `policy` from env.reset() (src/baselines/__init__.py:72-101):
+    the TSTT after every step, the scaled reward sum, and the curve's last /
+    mean / trapezoid area (an empty episode reports the env's TSTT)."""
     state = env.reset()
+    curve: List[float] = []
+    reward_sum = 0.0
     done = False
-    steps = 0
-    total_reward = 0.0
-    while not done:
-        action = policy(state)
-        state, reward, done, info = env.step(action)
-        total_reward += reward * reward_scale
-        tstt_curve.append(info.get("tstt", env.tstt))
-        steps += 1
-        if max_steps > 0 and steps >= max_steps and not done:
-            break
-    tstt_last = float(tstt_curve[-1]) if tstt_curve else env.tstt
-    tstt_mean = float(np.mean(tstt_curve)) if tstt_curve else env.tstt
-    tstt_auc = float(np.trapezoid(tstt_curve)) if tstt_curve else env.tstt
-    return {"tstt_curve": tstt_curve, "reward": total_reward, "tstt_last": tstt_last, "tstt_mean": tstt_mean,
-            "tstt_auc": tstt_auc, "auc": tstt_auc}
+    while not done and not (max_steps > 0 and len(curve) >= max_steps):
+        state, reward, done, info = env.step(policy(state))
+        reward_sum += reward * reward_scale
+        curve.append(info.get("tstt", env.tstt))
+    if curve:
+        last, mean, auc = float(curve[-1]), float(np.mean(curve)), float(np.trapezoid(curve))
+    else:
+        last = mean = auc = env.tstt
+    return {"tstt_curve": curve, "reward": reward_sum, "tstt_last": last, "tstt_mean": mean, "tstt_auc": auc,
+            "auc": auc}
 
 
 def get_baseline_policies(env: RepairEnv) -> Dict[str, Callable[[EnvState], int]]:
-    node_bw = env.betweenness_vec
-    edge_index = env.edge_index
-    return {
-        "random": select_random,
-        "max_vc": select_max_vc,
-        "max_flow": select_max_flow,
-        "max_betweenness": lambda s: select_max_betweenness(s, node_bw, edge_index),
-        "greedy": lambda s: select_greedy_one_step(env, s),
-    }
+    """The reference's policy table (104-113); betweenness and links are read once."""
+    bw, ei = env.betweenness_vec, env.edge_index
+    table: Dict[str, Callable[[EnvState], int]] = dict(random=select_random, max_vc=select_max_vc,
+                                                       max_flow=select_max_flow)
+    table["max_betweenness"] = lambda st: select_max_betweenness(st, bw, ei)
+    table["greedy"] = lambda st: select_greedy_one_step(env, st)
+    return table
