@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 5
+#define TRX_ABI_VERSION 6
 
 /* error codes */
 #define TRX_OK 0
@@ -239,6 +239,11 @@ typedef struct trx_gat_layer_args {
     float* out_f32;             /* [N, out] or NULL */
     void* out_bf16;             /* [N, out] bf16 or NULL */
     float* pool;                /* [num_graphs, 2*out] mean | max, or NULL */
+    /* training forward (trx_gat_layer_backward's saved tensors), each NULL = not saved: */
+    float* save_alpha;          /* [Et, heads] attention weights in CSR order             */
+    float* save_asd;            /* [N, 2*heads] a_src | a_dst                              */
+    float* save_v;              /* [N, out] aggregate + bias (LayerNorm input)             */
+    float* save_stats;          /* [N, 2] LayerNorm mean, rstd                             */
 } trx_gat_layer_args;
 int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
 
@@ -319,6 +324,126 @@ typedef struct trx_gat_prologue_args {
                                    links or nodes of another graph gets NaN rows */
 } trx_gat_prologue_args;
 int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream);
+
+/* ------------------------------------------ fused SAC-update backward
+ * The SAC update (src/rl/sac.py:157-243) runs its training forwards through
+ * the fused inference kernels above with the save_* outputs set; these
+ * kernels are their backward (csrc/gat_train.hip), one workgroup per graph.
+ *
+ * trx_gat_layer_backward: a whole GATConv layer + tail of GATEncoder
+ * (src/models/gat_encoder.py:36-49): activation (0 relu / 1 elu), residual
+ * (0 none, 1 res input [N,F] fp32 -> g_res, 2 layer 0's bf16(x0 @ wp^T + bp)),
+ * LayerNorm, bias, aggregation, edge softmax, leaky ReLU, attention dots;
+ * in_dim 4 = layer 0 (xh recomputed from x0 and w0, g_x0 written), the last
+ * layer may take the pooled-context gradient g_pool [B, 2F] (mean | max).
+ * Inputs: gy fp32 [N,F] and/or gy_bf16 bf16 [N,F] (summed), the forward's
+ * saved alpha / asd / v / stats and its output y fp32.  Outputs: g_xh bf16
+ * [N,F] (gradient of the lin output, rounded once), g_res fp32 [N,F] (always
+ * written: the gradient at the activation input; the residual's gradient for
+ * residual 1), g_a_edge [Et, a_edge_stride] at a_edge_offset, g_x0 [N,4]
+ * (in_dim 4), part [num_graphs, trx_gat_layer_backward_part_floats()]
+ * per-graph partial sums: bias, ln weight, ln bias, att_src, att_dst (F each)
+ * and, for in_dim 4, lin.weight (F x 4), input_proj weight (F x 4) and bias.
+ * F = heads*channels in {256, 512, 1024}; sptr/spos = the same graph in CSR by
+ * source (dst-CSR position of each out-edge, fixed order: deterministic).   */
+typedef struct trx_gat_layer_bwd_args {
+    int32_t num_graphs, nodes_per_graph, heads, channels, max_graph_edges, in_dim;
+    const int32_t* rowptr;      /* [N+1] CSR by destination (self loops included) */
+    const int32_t* col;         /* [Et] */
+    const int32_t* sptr;        /* [N+1] CSR by source */
+    const int32_t* spos;        /* [Et] dst-CSR position per source entry */
+    const void* xh;             /* bf16 [N, F] lin output (in_dim 0) */
+    const float* x0;            /* [N, in_dim] (in_dim 4) */
+    const float* w0;            /* [F, in_dim] bf16-rounded lin.weight (in_dim 4) */
+    const float* a_edge;        /* [Et, a_edge_stride] forward edge logits */
+    int32_t a_edge_stride, a_edge_offset;
+    const float* att_src;       /* [F] */
+    const float* att_dst;       /* [F] */
+    const float* ln_weight;     /* [F] */
+    float negative_slope;
+    int32_t activation, residual;
+    const float* wp;            /* [F, in_dim] bf16-rounded input_proj weight (residual 2) */
+    const float* alpha;         /* saved by the forward: [Et, heads] */
+    const float* asd;           /* [N, 2*heads] */
+    const float* v;             /* [N, F] */
+    const float* stats;         /* [N, 2] */
+    const float* y;             /* [N, F] forward output (fp32) */
+    const float* gy;            /* [N, F] or NULL */
+    const void* gy_bf16;        /* bf16 [N, F] or NULL */
+    const float* g_pool;        /* [B, 2F] or NULL */
+    void* g_xh;                 /* bf16 [N, F] */
+    float* g_res;               /* [N, F] */
+    float* g_x0;                /* [N, in_dim] (in_dim 4) */
+    float* g_a_edge;            /* [Et, a_edge_stride] */
+    float* part;                /* [num_graphs, part_floats] */
+} trx_gat_layer_bwd_args;
+int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream);
+int64_t trx_gat_layer_backward_part_floats(int32_t heads, int32_t channels, int32_t in_dim);
+/* out[k] = sum over r < rows (ascending) of part[r * stride + k], k < width. */
+int trx_partial_sum(const float* part, int32_t rows, int32_t width, int64_t stride, float* out, void* stream);
+
+/* trx_gat_prologue_backward: backward of trx_gat_prologue_infer (input
+ * LayerNorms, PyG mean self-loop attrs, every layer's a_edge) from g_a_edge
+ * [Et, A] (A = sum of heads), g_x0 [N, node_dim] and the edge head's link-
+ * feature gradient g_ea_head [B*e, edge_dim] (or NULL).  part [num_graphs,
+ * 8A + 32]: rows of 8 floats -- dL/dM_k (k < A, the bf16-rounded M rows of
+ * the forward's m_work), edge LN weight, edge LN bias, node LN weight, node
+ * LN bias (node_dim / edge_dim <= 8).                                       */
+typedef struct trx_gat_prologue_bwd_args {
+    int32_t num_graphs, nodes_per_graph, edges_per_graph, node_dim, edge_dim, A;
+    const float* node_x;
+    const float* edge_x;
+    const float* node_ln_w;
+    const float* node_ln_b;
+    float node_ln_eps;
+    const float* edge_ln_w;
+    const float* edge_ln_b;
+    float edge_ln_eps;
+    const int32_t* src;
+    const int32_t* dst;
+    const int32_t* rowptr;
+    const int32_t* pos_src;
+    const float* m_work;        /* [A, edge_dim] the forward's M rows */
+    const float* g_a_edge;      /* [Et, A] */
+    const float* g_x0;          /* [N, node_dim] */
+    const float* g_ea_head;     /* [B*e, edge_dim] or NULL */
+    float* part;                /* [num_graphs, 8A + 32] */
+} trx_gat_prologue_bwd_args;
+int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream);
+
+/* trx_sac_loss: DiscreteSAC.update's losses (src/rl/sac.py:184-219) for B
+ * graphs of e links (e <= 256) and their gradients: soft V target from the
+ * next-state actor probs and target critics, the PER-weighted twin-Q MSE
+ * (dL/dq1, dL/dq2 [B*e], non-zero at the taken action), the actor loss through
+ * the masked softmax of the raw logits (dL/dlogits), the alpha loss
+ * (dL/dlog_alpha).  out[8]: critic_loss, actor_loss, alpha_loss, entropy,
+ * q_taken, q_mean, logp_mean, alpha; td_error [B] = |target - q1|.
+ * target_entropy_given = 0: target entropy = ratio * mean log(valid + 1e-8). */
+typedef struct trx_sac_loss_args {
+    int32_t num_graphs, edges_per_graph;
+    const float* next_probs;    /* [B*e] */
+    const float* qt1;           /* [B*e] target critics */
+    const float* qt2;
+    const float* reward;        /* [B] */
+    const float* done;          /* [B] */
+    const float* q1;            /* [B*e] critics */
+    const float* q2;
+    const float* logits;        /* [B*e] actor raw logits */
+    const float* mask;          /* [B*e] action mask */
+    const int64_t* action;      /* [B] graph-local link */
+    const float* weights;       /* [B] PER importance weights */
+    const float* log_alpha;     /* [1] */
+    float gamma, target_entropy, target_entropy_ratio;
+    int32_t target_entropy_given;
+    float* g_q1;                /* [B*e] */
+    float* g_q2;
+    float* g_logits;
+    float* td_error;            /* [B] */
+    float* part;                /* [B, 8] scratch */
+    float* out;                 /* [8] */
+    float* g_log_alpha;         /* [1] */
+} trx_sac_loss_args;
+int trx_sac_loss(const trx_sac_loss_args* a, void* stream);
 
 /* ------------------------------------------------- prioritized replay
  * Sum tree of src/train.py:27-91 (ReplayBuffer) on the device: tree[1] is the

@@ -891,6 +891,74 @@ int trx_multi_copy(const trx_copy_list* l, void* stream) {
     return TRX_OK;
 }
 
+int64_t trx_gat_layer_backward_part_floats(int32_t heads, int32_t channels, int32_t in_dim) {
+    if (heads < 1 || channels < 1) return fail(TRX_EINVAL, "bad heads/channels");
+    return (int64_t)heads * channels * (in_dim > 0 ? 14 : 5);
+}
+
+int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_layer_backward: NULL args");
+    const int HC = a->heads * a->channels;
+    if (a->num_graphs < 0 || a->nodes_per_graph < 1 || a->nodes_per_graph > 32)
+        return fail(TRX_EUNSUP, "gat_layer_backward: nodes_per_graph must be 1..32");
+    if (a->heads < 1 || a->heads > 8 || a->channels % 4 || (HC != 256 && HC != 512 && HC != 1024) ||
+        a->channels > 256 || (a->channels < 64 ? 64 % a->channels : a->channels % 64) != 0)
+        return fail(TRX_EUNSUP, "gat_layer_backward: heads*channels 256/512/1024, channels dividing or divisible by 64");
+    if (a->max_graph_edges < 1 || a->max_graph_edges > 256)
+        return fail(TRX_EUNSUP, "gat_layer_backward: max_graph_edges must be 1..256");
+    if (a->in_dim != 0 && a->in_dim != 4) return fail(TRX_EUNSUP, "gat_layer_backward: in_dim must be 0 or 4");
+    if (a->activation != 0 && a->activation != 1) return fail(TRX_EINVAL, "gat_layer_backward: activation 0|1");
+    if (a->residual < 0 || a->residual > 2 || (a->residual == 2) != (a->in_dim == 4 && a->wp != nullptr))
+        return fail(TRX_EINVAL, "gat_layer_backward: residual 2 needs in_dim 4 and wp (and only then)");
+    if (!a->rowptr || !a->col || !a->sptr || !a->spos || (a->in_dim ? (!a->x0 || !a->w0 || !a->g_x0) : !a->xh) ||
+        !a->a_edge || !a->att_src || !a->att_dst || !a->ln_weight || !a->alpha || !a->asd || !a->v || !a->stats ||
+        !a->y || !a->g_xh || !a->g_res || !a->g_a_edge || !a->part || (!a->gy && !a->gy_bf16 && !a->g_pool))
+        return fail(TRX_EINVAL, "gat_layer_backward: NULL buffer");
+    if (a->a_edge_offset < 0 || a->a_edge_stride < a->a_edge_offset + a->heads)
+        return fail(TRX_EINVAL, "gat_layer_backward: a_edge stride/offset");
+    if (trx::gat_layer_bwd_smem(*a) > 160 * 1024) return fail(TRX_EUNSUP, "gat_layer_backward: LDS > 160 KB");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_gat_layer_bwd(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_layer_backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_partial_sum(const float* part, int32_t rows, int32_t width, int64_t stride, float* out, void* stream) {
+    if (!part || !out || rows < 0 || width < 0 || stride < width) return fail(TRX_EINVAL, "partial_sum args");
+    if (width == 0) return TRX_OK;
+    hipError_t e = trx::launch_partial_sum(part, rows, width, stride, out, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "partial_sum launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_prologue_backward: NULL args");
+    if (a->num_graphs < 0 || a->nodes_per_graph < 1 || a->nodes_per_graph > 64 || a->edges_per_graph < 0 ||
+        a->edges_per_graph > 1024 || a->node_dim < 1 || a->node_dim > 8 || a->edge_dim < 1 || a->edge_dim > 8 ||
+        a->A < 1 || a->A > 32)
+        return fail(TRX_EUNSUP, "gat_prologue_backward: sizes (nodes <= 64, links <= 1024, dims <= 8, heads <= 32)");
+    if (!a->node_x || !a->edge_x || !a->node_ln_w || !a->node_ln_b || !a->edge_ln_w || !a->edge_ln_b || !a->src ||
+        !a->dst || !a->rowptr || !a->pos_src || !a->m_work || !a->g_a_edge || !a->g_x0 || !a->part)
+        return fail(TRX_EINVAL, "gat_prologue_backward: NULL buffer");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_gat_prologue_bwd(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_prologue_backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_sac_loss(const trx_sac_loss_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "sac_loss: NULL args");
+    if (a->num_graphs < 1 || a->edges_per_graph < 1 || a->edges_per_graph > 256)
+        return fail(TRX_EUNSUP, "sac_loss: need >= 1 graph and 1..256 links per graph");
+    if (!a->next_probs || !a->qt1 || !a->qt2 || !a->reward || !a->done || !a->q1 || !a->q2 || !a->logits ||
+        !a->mask || !a->action || !a->weights || !a->log_alpha || !a->g_q1 || !a->g_q2 || !a->g_logits ||
+        !a->td_error || !a->part || !a->out || !a->g_log_alpha)
+        return fail(TRX_EINVAL, "sac_loss: NULL buffer");
+    hipError_t e = trx::launch_sac_loss(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "sac_loss launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_graph_patch_memsets(void* hip_graph, int32_t* n_patched) {
     if (!hip_graph) return fail(TRX_EINVAL, "graph_patch_memsets: NULL graph");
     int n = 0;

@@ -308,6 +308,12 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
         }
     }
     __syncthreads();
+    if (a.save_asd)
+        for (int t = tid; t < n * H; t += kInferThreads) {
+            const int i = t / H, h = t - (t / H) * H;
+            a.save_asd[(size_t)(node0 + i) * 2 * H + h] = as_[t];
+            a.save_asd[(size_t)(node0 + i) * 2 * H + H + h] = ad_[t];
+        }
     TRX_ISTAMP(2);
     TRX_ISTAMP(3);
 
@@ -326,6 +332,8 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
             al[p * H + h] = __expf(leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope) - m) / denom;
     }
     __syncthreads();
+    if (a.save_alpha)
+        for (int v = tid; v < ne * H; v += kInferThreads) a.save_alpha[(size_t)ebeg * H + v] = al[v];
     TRX_ISTAMP(4);
 
     // 4. aggregation + epilogue, one wave per node; lane owns chunks q = lane + 64k.
@@ -390,6 +398,16 @@ __global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_
                 s2 += d * d;
             }
         const float rstd = rsqrtf(wave_sum_f(s2) / (float)HC + a.ln_eps);
+        if (a.save_v) {
+#pragma unroll
+            for (int k = 0; k < KC; ++k)
+                *reinterpret_cast<float4*>(a.save_v + (size_t)node * HC + 4 * (lane + kWave * k)) =
+                    make_float4(v[k][0], v[k][1], v[k][2], v[k][3]);
+        }
+        if (a.save_stats && lane == 0) {
+            a.save_stats[2 * (size_t)node] = mean;
+            a.save_stats[2 * (size_t)node + 1] = rstd;
+        }
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
             const int f0 = 4 * (lane + kWave * k);

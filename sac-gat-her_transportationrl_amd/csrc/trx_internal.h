@@ -203,6 +203,12 @@ hipError_t launch_layer_tail_bwd(int N, int F, int act, int res_bf16, const floa
 hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t stream);
 size_t gat_prologue_smem(const trx_gat_prologue_args& a);
 hipError_t patch_graph_memsets(hipGraph_t graph, int* n_patched);
+size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a);
+hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t stream);
+hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t stride, float* out, hipStream_t stream);
+size_t gat_prologue_bwd_smem(const trx_gat_prologue_bwd_args& a);
+hipError_t launch_gat_prologue_bwd(const trx_gat_prologue_bwd_args& a, hipStream_t stream);
+hipError_t launch_sac_loss(const trx_sac_loss_args& a, hipStream_t stream);
 hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* pri, int n,
                              hipStream_t stream);
 hipError_t launch_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* pri, int n,

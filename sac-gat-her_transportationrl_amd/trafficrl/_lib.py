@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 5
+ABI_VERSION = 6
 SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
@@ -30,6 +30,8 @@ EXPORTS = (
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
     "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
+    "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_gat_prologue_backward",
+    "trx_sac_loss",
 )
 
 
@@ -85,6 +87,7 @@ class TrxGatLayerArgs(ctypes.Structure):
         ("residual", _i32), ("res", _vp), ("wp", _vp), ("bp", _vp),
         ("activation", _i32),
         ("out_f32", _vp), ("out_bf16", _vp), ("pool", _vp),
+        ("save_alpha", _vp), ("save_asd", _vp), ("save_v", _vp), ("save_stats", _vp),
     ]
 
 
@@ -112,6 +115,45 @@ class TrxGatPrologueArgs(ctypes.Structure):
         ("num_layers", _i32), ("heads", _i32 * MAX_GAT_LAYERS), ("channels", _i32 * MAX_GAT_LAYERS),
         ("lin_edge_w", _vp * MAX_GAT_LAYERS), ("att_edge", _vp * MAX_GAT_LAYERS),
         ("m_work", _vp), ("x0", _vp), ("ea", _vp), ("a_edge", _vp),
+    ]
+
+
+class TrxGatLayerBwdArgs(ctypes.Structure):
+    """trx_gat_layer_bwd_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("nodes_per_graph", _i32), ("heads", _i32), ("channels", _i32),
+        ("max_graph_edges", _i32), ("in_dim", _i32),
+        ("rowptr", _vp), ("col", _vp), ("sptr", _vp), ("spos", _vp), ("xh", _vp), ("x0", _vp), ("w0", _vp),
+        ("a_edge", _vp), ("a_edge_stride", _i32), ("a_edge_offset", _i32),
+        ("att_src", _vp), ("att_dst", _vp), ("ln_weight", _vp), ("negative_slope", _f32),
+        ("activation", _i32), ("residual", _i32), ("wp", _vp),
+        ("alpha", _vp), ("asd", _vp), ("v", _vp), ("stats", _vp), ("y", _vp),
+        ("gy", _vp), ("gy_bf16", _vp), ("g_pool", _vp),
+        ("g_xh", _vp), ("g_res", _vp), ("g_x0", _vp), ("g_a_edge", _vp), ("part", _vp),
+    ]
+
+
+class TrxGatPrologueBwdArgs(ctypes.Structure):
+    """trx_gat_prologue_bwd_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("nodes_per_graph", _i32), ("edges_per_graph", _i32), ("node_dim", _i32),
+        ("edge_dim", _i32), ("A", _i32), ("node_x", _vp), ("edge_x", _vp),
+        ("node_ln_w", _vp), ("node_ln_b", _vp), ("node_ln_eps", _f32),
+        ("edge_ln_w", _vp), ("edge_ln_b", _vp), ("edge_ln_eps", _f32),
+        ("src", _vp), ("dst", _vp), ("rowptr", _vp), ("pos_src", _vp),
+        ("m_work", _vp), ("g_a_edge", _vp), ("g_x0", _vp), ("g_ea_head", _vp), ("part", _vp),
+    ]
+
+
+class TrxSacLossArgs(ctypes.Structure):
+    """trx_sac_loss_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("edges_per_graph", _i32),
+        ("next_probs", _vp), ("qt1", _vp), ("qt2", _vp), ("reward", _vp), ("done", _vp), ("q1", _vp), ("q2", _vp),
+        ("logits", _vp), ("mask", _vp), ("action", _vp), ("weights", _vp), ("log_alpha", _vp),
+        ("gamma", _f32), ("target_entropy", _f32), ("target_entropy_ratio", _f32), ("target_entropy_given", _i32),
+        ("g_q1", _vp), ("g_q2", _vp), ("g_logits", _vp), ("td_error", _vp), ("part", _vp), ("out", _vp),
+        ("g_log_alpha", _vp),
     ]
 
 
@@ -181,6 +223,12 @@ def load():
     L = ctypes.CDLL(LIB_PATH)
     L.trx_abi_version.restype = ctypes.c_int32
     L.trx_last_error.restype = ctypes.c_char_p
+    L.trx_gat_layer_backward.argtypes = [ctypes.POINTER(TrxGatLayerBwdArgs), _vp]
+    L.trx_gat_layer_backward_part_floats.argtypes = [_i32, _i32, _i32]
+    L.trx_gat_layer_backward_part_floats.restype = ctypes.c_int64
+    L.trx_partial_sum.argtypes = [_vp, _i32, _i32, ctypes.c_int64, _vp, _vp]
+    L.trx_gat_prologue_backward.argtypes = [ctypes.POINTER(TrxGatPrologueBwdArgs), _vp]
+    L.trx_sac_loss.argtypes = [ctypes.POINTER(TrxSacLossArgs), _vp]
     L.trx_env_kernel_name.argtypes = [_vp, ctypes.POINTER(TrxParams)]
     L.trx_env_kernel_name.restype = ctypes.c_char_p
     L.trx_graph_create.argtypes = [ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp,
@@ -244,7 +292,8 @@ def load():
                  "trx_bf16_round", "trx_multi_copy",
                  "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
                  "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
-                 "trx_episode_step"):
+                 "trx_episode_step", "trx_gat_layer_backward", "trx_partial_sum", "trx_gat_prologue_backward",
+                 "trx_sac_loss"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

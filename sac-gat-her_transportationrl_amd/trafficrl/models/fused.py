@@ -190,10 +190,11 @@ def _head_weights(head):
     return wn, wc.t(), we, w2, b2
 
 
-def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology):
+def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology, keep_m: bool = False):
     """Actor/Critic input LayerNorms + every encoder layer's edge logits in
     CSR order (trx_gat_prologue_infer: one small kernel for the M rows, one
-    wave per graph for the rest).  Returns (x0, ea, a_all)."""
+    wave per graph for the rest).  Returns (x0, ea, a_all), or with keep_m
+    ((x0, ea, a_all, M rows), None, None) for the training backward."""
     L = _lib.load()
     layers = list(model.encoder.layers)
     dev = node_x.device
@@ -226,6 +227,8 @@ def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topolog
     a.m_work, a.x0, a.ea, a.a_edge = m_work.data_ptr(), x0.data_ptr(), ea.data_ptr(), a_all.data_ptr()
     _lib.check(L.trx_gat_prologue_infer(a, _lib.stream_ptr(dev)), "trx_gat_prologue_infer")
     del keep
+    if keep_m:
+        return (x0, ea, a_all, m_work), None, None
     return x0, ea, a_all
 
 

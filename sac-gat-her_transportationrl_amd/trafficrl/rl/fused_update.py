@@ -1,0 +1,414 @@
+"""Fused SAC update (src/rl/sac.py:157-243) for the trainer's regular batches.
+
+The general update (DiscreteSAC.compute_gradients) runs the three training
+forwards through torch autograd: ~700 kernels per update at batch 256, most of
+them casts, elementwise glue and small reductions of a few microseconds each.
+Here every network is evaluated by the fused inference kernels
+(models/fused.py, csrc/gat_infer.hip) with their save_* outputs, the three
+losses and their gradients come from one kernel (trx_sac_loss), and each
+network's backward is explicit: the edge scorer's backward kernel, one
+trx_gat_layer_backward launch per GAT layer, one prologue backward, the
+bf16 GEMMs of the lin / edge-head weights (split-K float32 weight gradients),
+and trx_partial_sum for the per-column parameter gradients.  About 230
+launches per update, all graph-capturable (no host synchronisation).
+
+Numerics: the forward is the fused inference path's (bf16 roundings where
+torch autocast rounds, fp32 reductions in its own order); the backward is its
+exact derivative with autocast's dtype rules (gradients of bf16 tensors rounded
+to bf16 once, parameter gradients float32).  tests/test_fused_update.py checks
+it against the autograd path and the fp32 restatement.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import _lib
+from ..models import fused
+from ..models.fused import Topology
+from ..models.skinny import _splitk_wgrad
+
+
+def supported(agent, topo: Optional[Topology]) -> bool:
+    """The fused update takes regular batches of <= 32-node graphs under bf16
+    autocast on the GPU, with the reference's network shapes."""
+    if topo is None or agent.amp_dtype != torch.bfloat16 or not agent.log_alpha.is_cuda:
+        return False
+    for net in (agent.actor, agent.critic1, agent.critic2, agent.target1, agent.target2):
+        enc = net.encoder
+        if not (fused.encoder_supported(enc) and fused.head_supported(net) and fused.prologue_supported(net)):
+            return False
+        layers = list(enc.layers)
+        if len(layers) != 3 or net.edge_mlp[0].weight.shape[0] > 256:
+            return False
+    return topo.e <= 256 and topo.n <= 32
+
+
+@dataclass
+class NetCtx:
+    """What one network's training forward keeps for its backward."""
+    x0: torch.Tensor
+    ea: torch.Tensor
+    a_all: torch.Tensor
+    m_work: torch.Tensor
+    node_x: torch.Tensor
+    edge_x: torch.Tensor
+    layers: List[Dict]
+    emb: torch.Tensor
+    ctx: torch.Tensor
+    p: torch.Tensor
+    c: torch.Tensor
+    head_w: tuple
+
+
+def _layer_args(l, norm, topo, a_all, off, stride, i, last):
+    args = _lib.TrxGatLayerArgs()
+    args.num_graphs, args.nodes_per_graph, args.heads, args.channels = topo.B, topo.n, l.heads, l.out_channels
+    args.concat, args.max_graph_edges = int(l.concat), topo.max_graph_edges
+    args.rowptr, args.col = topo.g.rowptr.data_ptr(), topo.g.col.data_ptr()
+    args.a_edge, args.a_edge_stride, args.a_edge_offset = a_all.data_ptr(), stride, off
+    args.negative_slope = float(l.negative_slope)
+    args.ln_eps = float(norm.eps)
+    args.activation = 1 if last else 0
+    return args
+
+
+def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology, save: bool,
+                mask: Optional[torch.Tensor] = None):
+    """Actor/Critic raw edge logits [B*e] (fp32) through the fused kernels, or
+    with `mask` the Actor's masked softmax probabilities (sac.py:45-46).
+    save=True also returns the NetCtx the backward needs."""
+    L = _lib.load()
+    dev = node_x.device
+    stream = _lib.stream_ptr(dev)
+    enc = net.encoder
+    layers = list(enc.layers)
+    x0, ea, a_all = fused.prologue(net, node_x, edge_x, topo, keep_m=save)
+    m_work = None
+    if save:
+        x0, ea, a_all, m_work = x0
+    N = x0.shape[0]
+    stride = a_all.shape[1]
+    wts = fused._encoder_weights(enc, layers) if save else fused._prepared(
+        enc, "enc", [l.lin.weight for l in layers] + [enc.input_proj.weight, enc.input_proj.bias],
+        lambda: fused._encoder_weights(enc, layers))
+    keep = []
+    recs = []
+    prev_f32 = prev_bf16 = None
+    ctx = None
+    off = 0
+    for i, l in enumerate(layers):
+        last = i == len(layers) - 1
+        HC = l.heads * l.out_channels
+        norm = enc.norms[i]
+        args = _layer_args(l, norm, topo, a_all, off, stride, i, last)
+        rec = {"off": off, "heads": l.heads, "channels": l.out_channels}
+        if i == 0:
+            w0, wp, bp = wts[0]
+            args.in_dim, args.x0, args.w0 = x0.shape[1], x0.data_ptr(), w0.data_ptr()
+            args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
+            rec.update(w0=w0, wp=wp)
+        else:
+            xh = torch.mm(prev_bf16, wts[i].t())
+            args.in_dim, args.xh = 0, xh.data_ptr()
+            rec.update(xh=xh, x_in=prev_bf16, w=wts[i])
+            if last:
+                args.residual = 0
+            else:
+                args.residual, args.res = 1, prev_f32.data_ptr()
+        att_s = l.att_src.detach().reshape(-1)
+        att_d = l.att_dst.detach().reshape(-1)
+        bias = l.bias.detach()
+        lw, lb = norm.weight.detach(), norm.bias.detach()
+        keep += [att_s, att_d, bias, lw, lb]
+        args.att_src, args.att_dst, args.bias = att_s.data_ptr(), att_d.data_ptr(), bias.data_ptr()
+        args.ln_weight, args.ln_bias = lw.data_ptr(), lb.data_ptr()
+        out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+        args.out_bf16 = out_bf16.data_ptr()
+        out_f32 = None
+        if save or (i + 1 < len(layers) - 1):
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32)
+            args.out_f32 = out_f32.data_ptr()
+        if last:
+            ctx = torch.empty(topo.B, 2 * HC, device=dev, dtype=torch.float32)
+            args.pool = ctx.data_ptr()
+        if save:
+            Et = topo.g.col.numel()
+            rec.update(alpha=torch.empty(Et, l.heads, device=dev), asd=torch.empty(N, 2 * l.heads, device=dev),
+                       v=torch.empty(N, HC, device=dev), stats=torch.empty(N, 2, device=dev), y=out_f32)
+            args.save_alpha, args.save_asd = rec["alpha"].data_ptr(), rec["asd"].data_ptr()
+            args.save_v, args.save_stats = rec["v"].data_ptr(), rec["stats"].data_ptr()
+        _lib.check(L.trx_gat_layer_infer(args, stream), "trx_gat_layer_infer")
+        recs.append(rec)
+        prev_f32, prev_bf16 = out_f32, out_bf16
+        off += l.heads
+    emb = prev_bf16
+    head_w = fused._head_weights(net) if save else fused._prepared(
+        net, "edge", (net.edge_mlp[0].weight, net.edge_mlp[0].bias, net.edge_mlp[2].weight, net.edge_mlp[2].bias),
+        lambda: fused._head_weights(net))
+    wn, wc, we, w2, b2 = head_w
+    b1 = net.edge_mlp[0].bias.detach()
+    p = torch.mm(emb, wn.t())                                   # bf16 [N, 2H] per-node projections
+    c = torch.mm(ctx.to(torch.bfloat16), wc) + b1               # autocast's bf16 product + fp32 bias
+    logits = torch.empty(topo.B * topo.e, device=dev, dtype=torch.float32)
+    a = fused._edge_args(p, c, ea, we, w2, b2, topo.src32, topo.dst32, topo.B, topo.n, topo.e)
+    a.out = logits.data_ptr()
+    if mask is not None:
+        m = mask.float().contiguous()
+        a.mask, a.softmax = m.data_ptr(), 1
+        keep.append(m)
+    _lib.check(L.trx_edge_head_infer(a, stream), "trx_edge_head_infer")
+    del keep
+    if not save:
+        return logits, None
+    return logits, NetCtx(x0, ea, a_all, m_work, node_x, edge_x, recs, emb, ctx, p, c, head_w)
+
+
+class GradFlat:
+    """Every gradient of one fused update as a view into ONE float32 buffer,
+    carved in the order the backward produces them, so each producer (GEMM,
+    partial-sum kernel, loss kernel) writes its parameters' gradients in place:
+    the data-parallel all-reduce (train.GradAllReduce) then reduces this
+    buffer directly -- no concatenation and no copy back."""
+
+    def __init__(self, total: int, device):
+        self.buf = torch.empty(total, device=device, dtype=torch.float32)
+        self.off = 0
+
+    def take(self, n: int) -> torch.Tensor:
+        t = self.buf[self.off:self.off + n]
+        self.off += n
+        assert self.off <= self.buf.numel(), "GradFlat layout overflow"
+        return t
+
+
+def flat_size(net) -> int:
+    """GradFlat floats one network's backward takes: its parameters plus the
+    prologue partial sums' padding (M-row gradients, 8-wide LayerNorm rows)."""
+    A = sum(l.heads for l in net.encoder.layers)
+    ed, nd = net.edge_norm.weight.numel(), net.node_norm.weight.numel()
+    return sum(p.numel() for p in net.parameters()) + 8 * A + 32 - 2 * ed - 2 * nd
+
+
+def _grad(param, g):
+    """param.grad = g (set_to_none semantics of the reference's zero_grad():
+    the gradient tensor is handed over, not accumulated)."""
+    param.grad = g.view_as(param) if g.shape != param.shape else g
+
+
+def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: GradFlat):
+    """Gradients of every parameter of `net` from dL/dlogits [B*e] fp32,
+    written into `sink` and handed to the parameters as views."""
+    L = _lib.load()
+    dev = g_logits.device
+    stream = _lib.stream_ptr(dev)
+    enc = net.encoder
+    layers = list(enc.layers)
+    B, n, e = topo.B, topo.n, topo.e
+    N = B * n
+    wn, wc, we, w2, b2 = cx.head_w
+    Hd = wn.shape[0] // 2
+    # ---- edge scorer (sac.py:42-44 factored): kernel + link-feature / weight products
+    a = fused._edge_args(cx.p, cx.c, cx.ea, we, w2, b2, topo.src32, topo.dst32, B, n, e)
+    g_p = torch.empty_like(cx.p)
+    g_c = torch.empty(B, Hd, device=dev, dtype=torch.float32)
+    g_z = torch.empty(B * e, Hd, device=dev, dtype=torch.bfloat16)
+    gw2p = torch.empty(B, Hd, device=dev, dtype=torch.float32)
+    gl = g_logits.contiguous()
+    _lib.check(L.trx_edge_head_backward(a, _lib.ptr(gl), _lib.ptr(g_p), _lib.ptr(g_c), _lib.ptr(g_z),
+                                        _lib.ptr(gw2p), stream), "trx_edge_head_backward")
+    ea_b = cx.ea.to(torch.bfloat16)
+    g_we = _splitk_wgrad(g_z, ea_b)                                     # [H, k] fp32
+    g_ea_head = (g_z @ we.to(torch.bfloat16)).float()                   # [B*e, k]
+    g_wn = _splitk_wgrad(g_p, cx.emb)                                   # [2H, embed] fp32
+    g_emb = g_p @ wn                                                    # bf16 [N, embed]
+    g_cb = g_c.to(torch.bfloat16)
+    ctx_b = cx.ctx.to(torch.bfloat16)
+    g_wc = (g_cb.t() @ ctx_b).float()                                   # [H, 2*embed]
+    g_ctx = (g_cb @ wc.t()).float()                                     # [B, 2*embed]
+    W1 = net.edge_mlp[0].weight
+    gW1 = sink.take(W1.numel()).view_as(W1)
+    torch.cat([g_wn[:Hd], g_wn[Hd:], g_we, g_wc], 1, out=gW1)
+    _grad(W1, gW1)
+    for prm, src in ((net.edge_mlp[0].bias, g_c), (net.edge_mlp[2].weight, gw2p)):
+        dst = sink.take(prm.numel())
+        torch.sum(src, 0, out=dst)
+        _grad(prm, dst)
+    gb2 = sink.take(1)
+    torch.sum(gl.to(torch.bfloat16), 0, keepdim=True, dtype=torch.float32, out=gb2)
+    _grad(net.edge_mlp[2].bias, gb2)
+    # ---- GAT layers, last to first
+    a_all = cx.a_all
+    g_a_all = torch.empty_like(a_all)
+    g_x0 = torch.empty_like(cx.x0)
+    gy_f32, gy_b16, g_pool = None, g_emb, g_ctx
+    for i in range(len(layers) - 1, -1, -1):
+        l, rec = layers[i], cx.layers[i]
+        last = i == len(layers) - 1
+        norm = enc.norms[i]
+        HC = l.heads * l.out_channels
+        ba = _lib.TrxGatLayerBwdArgs()
+        ba.num_graphs, ba.nodes_per_graph, ba.heads, ba.channels = B, n, l.heads, l.out_channels
+        ba.max_graph_edges, ba.in_dim = topo.max_graph_edges, 4 if i == 0 else 0
+        g = topo.g
+        ba.rowptr, ba.col, ba.sptr, ba.spos = g.rowptr.data_ptr(), g.col.data_ptr(), g.sptr.data_ptr(), g.spos.data_ptr()
+        att_s, att_d = l.att_src.detach().reshape(-1), l.att_dst.detach().reshape(-1)
+        lw = norm.weight.detach()
+        ba.att_src, ba.att_dst, ba.ln_weight = att_s.data_ptr(), att_d.data_ptr(), lw.data_ptr()
+        ba.a_edge, ba.a_edge_stride, ba.a_edge_offset = a_all.data_ptr(), a_all.shape[1], rec["off"]
+        ba.negative_slope = float(l.negative_slope)
+        ba.activation = 1 if last else 0
+        ba.residual = 0 if last else (2 if i == 0 else 1)
+        if i == 0:
+            ba.x0, ba.w0, ba.wp, ba.g_x0 = cx.x0.data_ptr(), rec["w0"].data_ptr(), rec["wp"].data_ptr(), g_x0.data_ptr()
+        else:
+            ba.xh = rec["xh"].data_ptr()
+        ba.alpha, ba.asd, ba.v, ba.stats, ba.y = (rec["alpha"].data_ptr(), rec["asd"].data_ptr(), rec["v"].data_ptr(),
+                                                   rec["stats"].data_ptr(), rec["y"].data_ptr())
+        ba.gy = 0 if gy_f32 is None else gy_f32.data_ptr()
+        ba.gy_bf16 = 0 if gy_b16 is None else gy_b16.data_ptr()
+        ba.g_pool = 0 if g_pool is None else g_pool.data_ptr()
+        g_xh = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+        g_res = torch.empty(N, HC, device=dev, dtype=torch.float32)
+        PW = int(L.trx_gat_layer_backward_part_floats(l.heads, l.out_channels, ba.in_dim))
+        part = torch.empty(B, PW, device=dev, dtype=torch.float32)
+        ba.g_xh, ba.g_res, ba.g_a_edge, ba.part = g_xh.data_ptr(), g_res.data_ptr(), g_a_all.data_ptr(), part.data_ptr()
+        _lib.check(L.trx_gat_layer_backward(ba, stream), "trx_gat_layer_backward")
+        pg = sink.take(PW)
+        _lib.check(L.trx_partial_sum(_lib.ptr(part), B, PW, PW, _lib.ptr(pg), stream), "trx_partial_sum")
+        _grad(l.bias, pg[:HC])
+        _grad(norm.weight, pg[HC:2 * HC])
+        _grad(norm.bias, pg[2 * HC:3 * HC])
+        _grad(l.att_src, pg[3 * HC:4 * HC])
+        _grad(l.att_dst, pg[4 * HC:5 * HC])
+        if i == 0:
+            _grad(l.lin.weight, pg[5 * HC:9 * HC])
+            _grad(enc.input_proj.weight, pg[9 * HC:13 * HC])
+            _grad(enc.input_proj.bias, pg[13 * HC:14 * HC])
+        else:
+            # lin: xh = x_in @ w^T (bf16): split-K fp32 weight gradient, bf16 input gradient
+            x_in = rec["x_in"]
+            S = 4 if N % 4 == 0 else 1
+            part_w = torch.bmm(g_xh.view(S, N // S, -1).transpose(1, 2), x_in.view(S, N // S, -1))
+            gw = sink.take(l.lin.weight.numel()).view_as(l.lin.weight)
+            torch.sum(part_w, 0, dtype=torch.float32, out=gw)
+            _grad(l.lin.weight, gw)
+            # the previous layer's output reaches this layer twice: bf16 through lin,
+            # fp32 as the residual of a middle layer (gat_encoder.py:44-46)
+            gy_b16 = g_xh @ rec["w"]
+            gy_f32 = g_res if ba.residual == 1 else None
+            g_pool = None
+    # ---- prologue: input LayerNorms, loop attrs, edge-logit projections
+    A = a_all.shape[1]
+    pa = _lib.TrxGatPrologueBwdArgs()
+    pa.num_graphs, pa.nodes_per_graph, pa.edges_per_graph = B, n, e
+    pa.node_dim, pa.edge_dim, pa.A = cx.node_x.shape[1], cx.edge_x.shape[1], A
+    nx, ex = cx.node_x, cx.edge_x
+    pa.node_x, pa.edge_x = nx.data_ptr(), ex.data_ptr()
+    nw, nb = net.node_norm.weight.detach(), net.node_norm.bias.detach()
+    ew, eb = net.edge_norm.weight.detach(), net.edge_norm.bias.detach()
+    pa.node_ln_w, pa.node_ln_b, pa.node_ln_eps = nw.data_ptr(), nb.data_ptr(), float(net.node_norm.eps)
+    pa.edge_ln_w, pa.edge_ln_b, pa.edge_ln_eps = ew.data_ptr(), eb.data_ptr(), float(net.edge_norm.eps)
+    pa.src, pa.dst, pa.rowptr, pa.pos_src = (topo.src32.data_ptr(), topo.dst32.data_ptr(), topo.g.rowptr.data_ptr(),
+                                             topo.pos_src.data_ptr())
+    pa.m_work, pa.g_a_edge, pa.g_x0, pa.g_ea_head = (cx.m_work.data_ptr(), g_a_all.data_ptr(), g_x0.data_ptr(),
+                                                     g_ea_head.data_ptr())
+    PP = 8 * A + 32
+    ppart = torch.empty(B, PP, device=dev, dtype=torch.float32)
+    pa.part = ppart.data_ptr()
+    _lib.check(L.trx_gat_prologue_backward(pa, stream), "trx_gat_prologue_backward")
+    pp = sink.take(PP)
+    _lib.check(L.trx_partial_sum(_lib.ptr(ppart), B, PP, PP, _lib.ptr(pp), stream), "trx_partial_sum")
+    ed, nd = cx.edge_x.shape[1], cx.node_x.shape[1]
+    _grad(net.edge_norm.weight, pp[8 * A:8 * A + ed])
+    _grad(net.edge_norm.bias, pp[8 * A + 8:8 * A + 8 + ed])
+    _grad(net.node_norm.weight, pp[8 * A + 16:8 * A + 16 + nd])
+    _grad(net.node_norm.bias, pp[8 * A + 24:8 * A + 24 + nd])
+    gM = pp[:8 * A].view(A, 8)[:, :ed]
+    off = 0
+    for l in layers:
+        H, C = l.heads, l.out_channels
+        gm = gM[off:off + H]                                           # [H, ed]
+        att = l.att_edge.detach().view(H, C, 1)
+        W = l.lin_edge.weight.detach().view(H, C, ed)
+        # M[h, j] = sum_c W[h*C + c, j] * att[h, c]  (fp32, then bf16-rounded in the forward)
+        gwe = sink.take(H * C * ed).view(H, C, ed)
+        torch.mul(gm.view(H, 1, ed), att, out=gwe)
+        _grad(l.lin_edge.weight, gwe.view(H * C, ed))
+        gae = sink.take(H * C).view(H, C)
+        torch.sum(W * gm.view(H, 1, ed), 2, out=gae)
+        _grad(l.att_edge, gae)
+        off += H
+
+
+def compute_gradients_fused(agent, batch, weights, topo: Topology):
+    """DiscreteSAC.compute_gradients (sac.py:157-243) on the fused path: the
+    same returned metrics (device tensors), every gradient set."""
+    (node_x, edge_index, edge_attr, action_mask, batch_vec, action, reward, next_node_x, next_edge_attr,
+     next_action_mask, next_batch_vec, done) = batch
+    B = reward.shape[0]
+    E = topo.e
+    dev = reward.device
+    nx, ex = node_x.float().contiguous(), edge_attr.float().contiguous()
+    nnx, nex = next_node_x.float().contiguous(), next_edge_attr.float().contiguous()
+    # no-grad next-state passes (sac.py:184-191): next actor probs, two target critics
+    with torch.no_grad():
+        nprobs, qt1, qt2 = agent._concurrent([
+            lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask)[0],
+            lambda: net_forward(agent.target1, nnx, nex, topo, save=False)[0],
+            lambda: net_forward(agent.target2, nnx, nex, topo, save=False)[0]])
+        # training forwards of the two critics and the actor (raw logits), with saves
+        ctxs = agent._concurrent([lambda net=net: net_forward(net, nx, ex, topo, save=True)
+                                  for net in (agent.critic1, agent.critic2, agent.actor)])
+    (q1, c1), (q2, c2), (lg, ca) = ctxs
+    L = _lib.load()
+    la = agent.log_alpha.detach().reshape(1)
+    act_local = action % E      # the batch tuple carries graph offsets (arange(B) * E + action)
+    g_q1, g_q2, g_lg = torch.empty_like(q1), torch.empty_like(q2), torch.empty_like(lg)
+    td = torch.empty(B, device=dev, dtype=torch.float32)
+    part = torch.empty(B, 8, device=dev, dtype=torch.float32)
+    out = torch.empty(8, device=dev, dtype=torch.float32)
+    nets = (agent.critic1, agent.critic2, agent.actor)
+    sizes = [flat_size(net) for net in nets]
+    flat = torch.empty(sum(sizes) + 1, device=dev, dtype=torch.float32)
+    sinks = []
+    o = 0
+    for sz in sizes:   # one GradFlat window per network (their backwards run on three streams)
+        gf = GradFlat.__new__(GradFlat)
+        gf.buf, gf.off = flat[o:o + sz], 0
+        sinks.append(gf)
+        o += sz
+    g_la = flat[o:o + 1]
+    w = torch.ones(B, device=dev) if weights is None else torch.as_tensor(weights, device=dev).float().reshape(B)
+    sa = _lib.TrxSacLossArgs()
+    sa.num_graphs, sa.edges_per_graph = B, E
+    npf = nprobs.contiguous()
+    r32, d32 = reward.float().contiguous(), done.float().contiguous()
+    mk = action_mask.float().contiguous()
+    act = act_local.to(torch.int64).contiguous()
+    keep = [npf, r32, d32, mk, act, w, la]
+    for name, t in (("next_probs", npf), ("qt1", qt1), ("qt2", qt2), ("reward", r32), ("done", d32), ("q1", q1),
+                    ("q2", q2), ("logits", lg), ("mask", mk), ("action", act), ("weights", w), ("log_alpha", la),
+                    ("g_q1", g_q1), ("g_q2", g_q2), ("g_logits", g_lg), ("td_error", td), ("part", part),
+                    ("out", out), ("g_log_alpha", g_la)):
+        setattr(sa, name, t.data_ptr())
+    sa.gamma = float(agent.gamma)
+    if agent.target_entropy is None:
+        sa.target_entropy_given, sa.target_entropy_ratio = 0, float(agent.target_entropy_ratio)
+    else:
+        sa.target_entropy_given, sa.target_entropy = 1, float(agent.target_entropy)
+    _lib.check(L.trx_sac_loss(sa, _lib.stream_ptr(dev)), "trx_sac_loss")
+    del keep
+    agent.critic_opt.zero_grad(set_to_none=True)
+    agent.actor_opt.zero_grad(set_to_none=True)
+    agent.alpha_opt.zero_grad(set_to_none=True)
+    agent._concurrent([lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0]),
+                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1]),
+                       lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2])])
+    agent.log_alpha.grad = g_la.view_as(agent.log_alpha)
+    agent.grad_flat = flat        # every gradient of this update is a view of it (GradAllReduce)
+    agent._warm = True
+    return {"critic_loss": out[0], "actor_loss": out[1], "alpha": out[7], "alpha_loss": out[2],
+            "policy_entropy": out[3], "q_taken": out[4], "q_mean": out[5], "logp_mean": out[6], "td_errors": td}

@@ -193,6 +193,7 @@ def clip_grad_norm_listwise_(params, max_norm: float):
 
 FUSED_INFERENCE = True   # module switch (tests compare both paths)
 FUSED_EDGE_TRAIN = True  # training-path edge scorer kernels (tests compare both paths)
+FUSED_UPDATE = True      # whole-update fused path (rl/fused_update.py) for regular bf16 batches
 
 
 def _fused_topology(encoder, node_x, edge_index, batch, B, head=None):
@@ -362,6 +363,8 @@ class DiscreteSAC:
         self.concurrent = True
         self._side = None
         self._warm = False
+        self.last_update_path = None   # "fused" (rl/fused_update.py) or "autograd"
+        self.grad_flat = None          # fused path: the one buffer every gradient is a view of
 
     @property
     def alpha(self):
@@ -428,6 +431,14 @@ class DiscreteSAC:
         (node_x, edge_index, edge_attr, action_mask, batch_vec, action, reward, next_node_x, next_edge_attr,
          next_action_mask, next_batch_vec, done) = batch
         B = reward.shape[0]
+        if FUSED_UPDATE and reward.is_cuda and next_batch_vec is batch_vec:
+            from . import fused_update
+            topo = fused.topology(edge_index, batch_vec, B)
+            if fused_update.supported(self, topo):
+                self.last_update_path = "fused"
+                return fused_update.compute_gradients_fused(self, batch, weights, topo)
+        self.last_update_path = "autograd"
+        self.grad_flat = None
         if weights is None:
             weights_tensor = torch.ones_like(reward)
         else:

@@ -108,13 +108,34 @@ def batched_topology(edge_index: torch.Tensor, num_nodes: int, B: int):
 
 
 class GradAllReduce:
-    """One bucketed all-reduce (sum / world) of every gradient per update."""
+    """One bucketed all-reduce (sum / world) of every gradient per update.
 
-    def __init__(self, world: int):
+    The fused update (rl/fused_update.py) produces every gradient as a view of
+    one flat buffer (agent.grad_flat): that buffer is reduced in place -- one
+    RCCL call, no concatenation, no copy back.  Other paths (autograd) are
+    concatenated into a bucket and copied back."""
+
+    def __init__(self, world: int, agent=None):
         import torch.distributed as dist
-        self.dist, self.world = dist, world
+        self.dist, self.world, self.agent = dist, world, agent
+
+    def _flat_of(self, grads):
+        flat = getattr(self.agent, "grad_flat", None) if self.agent is not None else None
+        if flat is None or not grads:
+            return None
+        base = flat.untyped_storage().data_ptr()
+        lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * 4
+        for g in grads:
+            if g.untyped_storage().data_ptr() != base or not (lo <= g.data_ptr() < hi):
+                return None
+        return flat
 
     def __call__(self, grads):
+        flat = self._flat_of(grads)
+        if flat is not None:
+            self.dist.all_reduce(flat)
+            flat.div_(self.world)
+            return
         flat = torch.cat([g.reshape(-1) for g in grads])
         self.dist.all_reduce(flat)
         flat.div_(self.world)
@@ -265,7 +286,7 @@ class Trainer:
                 for t in list(m.parameters()) + list(m.buffers()):
                     dist.broadcast(t.data, src=0)
             dist.broadcast(self.agent.log_alpha.data, src=0)
-            self.agent.grad_sync = GradAllReduce(world)
+            self.agent.grad_sync = GradAllReduce(world, self.agent)
         cap = min(int(cfg["buffer_size"]), max(int(cfg["buffer_size"]) // world, B))
         self.replay = DeviceReplay(cap, self.N, self.E, alpha=cfg["per_alpha"], beta=cfg["per_beta"],
                                    eps=cfg["per_eps"], device=self.device, tree_dtype=cfg["per_tree"])

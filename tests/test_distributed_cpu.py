@@ -1,7 +1,8 @@
 """N>1 path on CPU (gloo, world_size 2): the SAC gradient bucket all-reduce
 (trafficrl.train.GradAllReduce, the only data-parallel collective) averages
-every gradient and leaves ranks bit-identical; the bench's max-over-ranks
-timing reduction picks the slowest rank."""
+every gradient and leaves ranks bit-identical -- both the concatenated bucket
+and the zero-copy in-place reduction of the fused update's flat gradient
+buffer; the bench's max-over-ranks timing reduction picks the slowest rank."""
 import os
 import socket
 
@@ -30,6 +31,19 @@ def _worker(rank, world, port, q):
     dist.all_gather_object(gathered, [g for g in mine])
     mean = [sum(x[i] for x in gathered) / world for i in range(len(mine))]
     ok = all(torch.allclose(a, b, atol=1e-6) for a, b in zip(grads, mean))
+    # zero-copy path: gradients that are views of the agent's flat buffer (the
+    # fused update's layout) are reduced in place, the buffer itself reduced once
+    from types import SimpleNamespace
+    flat = torch.randn(30)
+    views = [flat[0:21].view(7, 3), flat[21:29], flat[29:30]]
+    before = flat.clone()
+    red = GradAllReduce(world, SimpleNamespace(grad_flat=flat))
+    assert red._flat_of(views) is flat and red._flat_of([torch.zeros(3)]) is None
+    red(views)
+    allb = [None] * world
+    dist.all_gather_object(allb, before)
+    ok = ok and torch.allclose(flat, sum(allb) / world, atol=1e-6)
+    ok = ok and views[1].data_ptr() == flat.data_ptr() + 21 * 4          # still views: nothing copied back
     t = torch.tensor([0.5 + rank], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     q.put((rank, ok, float(t), [g.sum().item() for g in grads]))

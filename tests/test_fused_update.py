@@ -1,0 +1,185 @@
+"""The fused SAC update (trafficrl/rl/fused_update.py: fused forwards with
+saves, trx_sac_loss, trx_gat_layer_backward / trx_gat_prologue_backward /
+edge-head backward kernels + bf16 GEMMs) against
+
+  * autograd over the plain fp32 restatement of the reference's networks and
+    losses (tests/test_sac_e2e.py: src/rl/sac.py:35-78, 184-219 and
+    src/models/gat_encoder.py:32-53 via PyG GATConv semantics) -- per
+    parameter tensor ||g - g_ref|| / (||g_ref|| + floor) below 6e-2 (bf16
+    autocast: 8-bit mantissas through six forwards and three backwards), at
+    the bench's hidden = embed = 256 (the fused kernels take heads*channels of
+    256 / 512 / 1024; smaller networks take the autograd path, which
+    tests/test_sac_e2e.py checks at 64);
+  * the general autograd path of this repo (same bf16 rounding points, its own
+    summation order): below 3e-2;
+  * a 10-update trajectory: the same agent trained by fused updates, by the
+    autograd path and by fp32-restatement gradients through the same Adam
+    steps (drift bounds in the test's docstring).
+"""
+import copy
+
+import pytest
+import torch
+
+from test_sac_e2e import _update_batch, make_agent, ref_losses
+
+pytestmark = pytest.mark.gpu
+
+MODS = ("actor", "critic1", "critic2")
+
+
+def _grads(agent):
+    return {f"{m}.{n}": p.grad.detach().float().clone() for m in MODS
+            for n, p in getattr(agent, m).named_parameters() if p.grad is not None}
+
+
+def _zero(agent):
+    for m in MODS:
+        getattr(agent, m).zero_grad(set_to_none=True)
+    agent.log_alpha.grad = None
+
+
+def _ref_grads(agent, batch, w, B):
+    _zero(agent)
+    cl, al, aal = ref_losses(agent, batch, w, B)
+    cl.backward()
+    al.backward()
+    aal.backward()
+    return _grads(agent), float(agent.log_alpha.grad), (float(cl), float(al), float(aal))
+
+
+def _worst(got, ref):
+    """Largest per-tensor relative error; the floor (1e-2 x the module's RMS
+    tensor norm) keeps analytically vanishing gradients (the actor's last bias:
+    softmax is shift-invariant) from dividing rounding noise by ~0."""
+    errs = []
+    for m in MODS:
+        keys = [k for k in ref if k.startswith(m + ".")]
+        floor = 1e-2 * float(torch.stack([ref[k].norm() for k in keys]).pow(2).mean().sqrt())
+        for k in keys:
+            assert k in got, f"no gradient for {k}"
+            rel = float((got[k] - ref[k]).norm()) / (float(ref[k].norm()) + floor)
+            errs.append((rel, k))
+    errs.sort(reverse=True)
+    print("largest relative gradient errors:", [(round(e, 4), k) for e, k in errs[:12]])
+    return errs[0]
+
+
+@pytest.fixture(autouse=True)
+def _fp32_matmul():
+    old = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    yield
+    torch.backends.cuda.matmul.allow_tf32 = old
+
+
+def _autograd_grads(agent, batch, w):
+    from trafficrl.rl import sac
+    sac.FUSED_UPDATE = False
+    try:
+        _zero(agent)
+        out = agent.compute_gradients(batch, weights=w)
+        assert agent.last_update_path == "autograd"
+    finally:
+        sac.FUSED_UPDATE = True
+    return _grads(agent), float(agent.log_alpha.grad), out
+
+
+def test_fused_update_vs_fp32_restatement():
+    """At the bench's sizes the bf16 actor gradient is ~9 % off the fp32 one
+    on BOTH bf16 paths: at random init a graph's logits span ~1e-2 while bf16
+    rounds logits of ~0.3 to ~1e-3, and the actor's gradient is made of the
+    centred logits (softmax backward).  So: critics within 6e-2 of fp32, the
+    actor within 1.2 x the autograd path's own error + 1e-2, losses 6e-2."""
+    B = 256
+    batch = _update_batch(B)
+    agent = make_agent(hidden=256, embed=256)
+    w = torch.rand(B, device="cuda") * 0.5 + 0.5
+    out = agent.compute_gradients(batch, weights=w)
+    assert agent.last_update_path == "fused"
+    got, got_alpha = _grads(agent), float(agent.log_alpha.grad)
+    auto, _, _ = _autograd_grads(agent, batch, w)
+    ref, ref_alpha, losses = _ref_grads(agent, batch, w, B)
+    for m in MODS:
+        sub = {k: v for k, v in ref.items() if k.startswith(m + ".")}
+        wf = _worst({k: got[k] for k in sub}, sub)
+        wa = _worst({k: auto[k] for k in sub}, sub)
+        print(f"{m}: fused {wf}, autograd {wa} (relative to fp32)")
+        assert wf[0] < (6e-2 if m != "actor" else 1.2 * wa[0] + 1e-2), (m, wf, wa)
+    assert abs(got_alpha - ref_alpha) <= 6e-2 * max(1e-6, abs(ref_alpha))
+    for k, r in zip(("critic_loss", "actor_loss", "alpha_loss"), losses):
+        assert abs(float(out[k]) - r) <= 6e-2 * max(1e-3, abs(r)), (k, float(out[k]), r)
+
+
+def test_fused_update_vs_autograd_path():
+    """Same bf16 rounding points, different summation orders: per tensor
+    within 3e-2 (measured 3.6e-3; 1.4e-2 on the actor's last bias, whose
+    gradient vanishes analytically), metrics within 3e-2."""
+    B = 256
+    batch = _update_batch(B)
+    agent = make_agent(hidden=256, embed=256)
+    w = torch.rand(B, device="cuda") * 0.5 + 0.5
+    out_f = agent.compute_gradients(batch, weights=w)
+    assert agent.last_update_path == "fused"
+    got, got_alpha = _grads(agent), float(agent.log_alpha.grad)
+    td_f = out_f["td_errors"].clone()
+    ref, ref_alpha, out_a = _autograd_grads(agent, batch, w)
+    worst = _worst(got, ref)
+    print(f"fused vs autograd path: worst relative gradient error {worst}")
+    assert worst[0] < 3e-2, worst
+    assert abs(got_alpha - ref_alpha) <= 3e-2 * max(1e-6, abs(ref_alpha))
+    torch.testing.assert_close(td_f, out_a["td_errors"].float(), rtol=3e-2, atol=3e-2 * float(td_f.abs().mean()))
+    for k in ("critic_loss", "actor_loss", "alpha_loss", "policy_entropy", "q_taken", "q_mean", "logp_mean"):
+        a, b = float(out_f[k]), float(out_a[k])
+        assert abs(a - b) <= 3e-2 * max(1e-3, abs(b)), (k, a, b)
+
+
+def _drift(a, b, start, m):
+    num = den = 0.0
+    sa, sb = getattr(a, m).state_dict(), getattr(b, m).state_dict()
+    for k in sb:
+        num += float((sa[k].float() - sb[k].float()).pow(2).sum())
+        den += float((sb[k].float() - start[f"{m}.{k}"].float()).pow(2).sum())
+    return (num / max(den, 1e-30)) ** 0.5
+
+
+def test_fused_update_trajectory():
+    """10 updates on one batch from the same initial weights, each agent
+    stepping its own Adam (apply_gradients): fused bf16 gradients, the
+    autograd path's bf16 gradients, and fp32-restatement gradients.
+    Parameter drift = ||theta_x - theta_y|| / distance travelled, per module.
+    Fused vs autograd (same numerics): below 5e-2.  Against fp32 the fused
+    run drifts no more than the autograd bf16 run (x 1.2 + 2e-2): Adam turns
+    the actor's ~9 % bf16 gradient noise (see above) into full-size steps on
+    small-gradient weights.  Losses of every step within 6e-2 of fp32."""
+    from trafficrl.rl import sac
+    B = 256
+    batch = _update_batch(B)
+    w = torch.rand(B, device="cuda") * 0.5 + 0.5
+    a_f = make_agent(hidden=256, embed=256)
+    a_a, a_r = copy.deepcopy(a_f), copy.deepcopy(a_f)
+    start = {f"{m}.{k}": v.detach().clone() for m in MODS for k, v in getattr(a_r, m).state_dict().items()}
+    for step in range(10):
+        out = a_f.compute_gradients(batch, weights=w)
+        assert a_f.last_update_path == "fused"
+        a_f.apply_gradients(2.5)
+        sac.FUSED_UPDATE = False
+        try:
+            a_a.compute_gradients(batch, weights=w)
+        finally:
+            sac.FUSED_UPDATE = True
+        a_a.apply_gradients(2.5)
+        _zero(a_r)
+        cl, al, aal = ref_losses(a_r, batch, w, B)
+        cl.backward()
+        al.backward()
+        aal.backward()
+        a_r.apply_gradients(2.5)
+        for k, r in zip(("critic_loss", "actor_loss", "alpha_loss"), (cl, al, aal)):
+            r = float(r)
+            assert abs(float(out[k]) - r) <= 6e-2 * max(1e-3, abs(r)), (step, k, float(out[k]), r)
+    for m in MODS:
+        dfa, dfr, dar = _drift(a_f, a_a, start, m), _drift(a_f, a_r, start, m), _drift(a_a, a_r, start, m)
+        print(f"{m}: drift fused-autograd {dfa:.4f}, fused-fp32 {dfr:.4f}, autograd-fp32 {dar:.4f}")
+        assert dfa < 5e-2, (m, dfa)
+        assert dfr <= 1.2 * dar + 2e-2, (m, dfr, dar)
