@@ -113,10 +113,15 @@ def _bf16r(t: torch.Tensor) -> torch.Tensor:
 # updates parameters without bumping their version counters, so the trainer
 # and DiscreteSAC.apply_gradients advance an epoch after every update; the key
 # also holds each parameter's (address, version) for in-place edits from Python
-# (load_state_dict, eager optimizer steps).  Never used while a graph is being
-# captured (the captured update must recompute them on every replay).
+# (load_state_dict, eager optimizer steps).  A stale slot is refreshed IN PLACE
+# (same buffers), so a captured acting graph (train.GraphedAct) that reads the
+# slots stays valid: it calls refresh_static() eagerly before each replay, and
+# captures under static_weights() (slots read, never written, inside the
+# graph).  Any other capture (the SAC update) recomputes the copies inside the
+# graph on every replay.
 _PREP_EPOCH = [0]
 _prep_cache: Dict[Tuple, Tuple] = {}
+_STATIC = [False]
 
 
 def _round_into(pairs):
@@ -143,47 +148,91 @@ def weights_changed():
     _PREP_EPOCH[0] += 1
 
 
+class static_weights:
+    """Context for capturing a graph that reads the prepared-weight slots."""
+
+    def __enter__(self):
+        _STATIC[0] = True
+
+    def __exit__(self, *exc):
+        _STATIC[0] = False
+
+
 def _prepared(owner, name: str, params, make):
-    if torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing():
-        return make()
+    """make(into) -> prepared tensors; `into` (the slot's previous value, or
+    None) is refilled in place when given."""
+    capturing = torch.cuda.is_current_stream_capturing()
+    if torch.is_grad_enabled() or (capturing and not _STATIC[0]):
+        return make(None)
     key = (_PREP_EPOCH[0],) + tuple((p.data_ptr(), p._version) for p in params)
     slot = (id(owner), name)
     hit = _prep_cache.get(slot)
     if hit is not None and hit[0] == key:
         return hit[1]
-    val = make()
-    if len(_prep_cache) > 256:
-        _prep_cache.clear()
-    _prep_cache[slot] = (key, val)
+    if capturing:
+        raise RuntimeError("prepared weights are stale inside a static-weight capture (call refresh_static first)")
+    sig = tuple((p.device, p.dtype, tuple(p.shape)) for p in params)   # a recycled id(owner) must not reuse a slot
+    val = make(hit[1] if hit is not None and hit[2] == sig else None)
+    _prep_cache[slot] = (key, val, sig)
     return val
 
 
-def _encoder_weights(enc, layers):
+def _enc_params(enc, layers):
+    return [l.lin.weight for l in layers] + [enc.input_proj.weight, enc.input_proj.bias]
+
+
+def _head_params(head):
+    return (head.edge_mlp[0].weight, head.edge_mlp[0].bias, head.edge_mlp[2].weight, head.edge_mlp[2].bias)
+
+
+def prepared_encoder(enc, layers):
+    return _prepared(enc, "enc", _enc_params(enc, layers), lambda into: _encoder_weights(enc, layers, into))
+
+
+def prepared_head(head):
+    return _prepared(head, "edge", _head_params(head), lambda into: _head_weights(head, into))
+
+
+def refresh_static(model):
+    """Bring an Actor/Critic's prepared-weight slots up to date (in place)."""
+    with torch.no_grad():
+        prepared_encoder(model.encoder, list(model.encoder.layers))
+        prepared_head(model)
+
+
+def _encoder_weights(enc, layers, into=None):
     """bf16-rounded float32 (w0, wp, bp) of layer 0, bf16 lin weights of the
-    later layers: one trx_bf16_round launch."""
+    later layers: one trx_bf16_round launch (into `into` when given)."""
     l0, ip = layers[0], enc.input_proj
-    w0, wp, bp = (torch.empty_like(l0.lin.weight), torch.empty_like(ip.weight), torch.empty_like(ip.bias))
+    if into is None:
+        w0, wp, bp = (torch.empty_like(l0.lin.weight), torch.empty_like(ip.weight), torch.empty_like(ip.bias))
+        out = [(w0, wp, bp)] + [torch.empty(l.lin.weight.shape, device=w0.device, dtype=torch.bfloat16)
+                                for l in layers[1:]]
+    else:
+        out = into
+    w0, wp, bp = out[0]
     pairs = [(l0.lin.weight, w0), (ip.weight, wp), (ip.bias, bp)]
-    out = [(w0, wp, bp)]
-    for l in layers[1:]:
-        w = torch.empty(l.lin.weight.shape, device=w0.device, dtype=torch.bfloat16)
-        pairs.append((l.lin.weight, w))
-        out.append(w)
+    pairs += [(l.lin.weight, w) for l, w in zip(layers[1:], out[1:])]
     _round_into(pairs)
     return out
 
 
-def _head_weights(head):
-    """(w_nodes bf16 [2H, d], W_ctx^T bf16 view, we, w2, b2 bf16-rounded float32): one launch."""
+def _head_weights(head, into=None):
+    """(w_nodes bf16 [2H, d], W_ctx^T bf16 view, we, w2, b2 bf16-rounded
+    float32): one launch (into `into` when given)."""
     W1, b1 = head.edge_mlp[0].weight, head.edge_mlp[0].bias
     d, k = head.embed, head.edge_in
     hid = W1.shape[0]
     dev = W1.device
-    wn = torch.empty(2 * hid, d, device=dev, dtype=torch.bfloat16)
-    wc = torch.empty(hid, W1.shape[1] - 2 * d - k, device=dev, dtype=torch.bfloat16)
-    we = torch.empty(hid, k, device=dev, dtype=torch.float32)
-    w2 = torch.empty(hid, device=dev, dtype=torch.float32)
-    b2 = torch.empty(1, device=dev, dtype=torch.float32)
+    if into is None:
+        wn = torch.empty(2 * hid, d, device=dev, dtype=torch.bfloat16)
+        wc = torch.empty(hid, W1.shape[1] - 2 * d - k, device=dev, dtype=torch.bfloat16)
+        we = torch.empty(hid, k, device=dev, dtype=torch.float32)
+        w2 = torch.empty(hid, device=dev, dtype=torch.float32)
+        b2 = torch.empty(1, device=dev, dtype=torch.float32)
+    else:
+        wn, wct, we, w2, b2 = into
+        wc = wct.t()
     _round_into([(W1[:, :d], wn[:hid]), (W1[:, d:2 * d], wn[hid:]), (W1[:, 2 * d + k:], wc),
                  (W1[:, 2 * d:2 * d + k], we), (head.edge_mlp[2].weight.reshape(-1), w2),
                  (head.edge_mlp[2].bias.reshape(-1), b2)])
@@ -266,9 +315,7 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
         a_all = a_edge
     stride = a_all.shape[1]
     stream = _lib.stream_ptr(dev)
-    wts = _prepared(enc, "enc", [p for l in layers for p in (l.lin.weight,)] + [enc.input_proj.weight,
-                                                                                enc.input_proj.bias],
-                    lambda: _encoder_weights(enc, layers))
+    wts = prepared_encoder(enc, layers)
     prev_f32, prev_bf16 = None, None
     emb = ctx = None
     for i, l in enumerate(layers):
@@ -328,8 +375,7 @@ def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: 
     W1, b1 = head.edge_mlp[0].weight, head.edge_mlp[0].bias
     d, k = head.embed, head.edge_in
     hid = W1.shape[0]
-    w_nodes, wc, we, w2, b2 = _prepared(head, "edge", (W1, b1, head.edge_mlp[2].weight, head.edge_mlp[2].bias),
-                                        lambda: _head_weights(head))
+    w_nodes, wc, we, w2, b2 = prepared_head(head)
     p = torch.mm(emb_bf16, w_nodes.t()).contiguous()                      # bf16 [N, 2*hid]
     c = (torch.mm(ctx.to(torch.bfloat16), wc) + b1).float().contiguous()  # autocast's bf16 GEMM + fp32 bias
     ea = edge_attr.float().contiguous()

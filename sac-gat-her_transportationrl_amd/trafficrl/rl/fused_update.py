@@ -91,9 +91,7 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         x0, ea, a_all, m_work = x0
     N = x0.shape[0]
     stride = a_all.shape[1]
-    wts = fused._encoder_weights(enc, layers) if save else fused._prepared(
-        enc, "enc", [l.lin.weight for l in layers] + [enc.input_proj.weight, enc.input_proj.bias],
-        lambda: fused._encoder_weights(enc, layers))
+    wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
     keep = []
     recs = []
     prev_f32 = prev_bf16 = None
@@ -145,9 +143,7 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         prev_f32, prev_bf16 = out_f32, out_bf16
         off += l.heads
     emb = prev_bf16
-    head_w = fused._head_weights(net) if save else fused._prepared(
-        net, "edge", (net.edge_mlp[0].weight, net.edge_mlp[0].bias, net.edge_mlp[2].weight, net.edge_mlp[2].bias),
-        lambda: fused._head_weights(net))
+    head_w = fused._head_weights(net) if save else fused.prepared_head(net)
     wn, wc, we, w2, b2 = head_w
     b1 = net.edge_mlp[0].bias.detach()
     p = torch.mm(emb, wn.t())                                   # bf16 [N, 2H] per-node projections

@@ -390,15 +390,20 @@ class DiscreteSAC:
         return SACOutput(action=action, log_prob=log_prob, probs=probs)
 
     def select_actions(self, node_x, edge_index, edge_attr, action_mask, batch, num_graphs: int,
-                       deterministic: bool = False, generator=None) -> torch.Tensor:
+                       deterministic: bool = False, generator=None, u: torch.Tensor = None) -> torch.Tensor:
         """Batched acting for B graphs with identical link counts (VecRepairEnv):
-        one actor forward, one multinomial draw per graph, no host sync."""
+        one actor forward, one multinomial draw per graph, no host sync.
+        `u`: the B uniforms of the fused draw, if already drawn (a captured
+        acting graph reads them from a static buffer)."""
         with torch.no_grad(), self._amp():
             if not deterministic:  # fused path: the draw happens inside the edge-head kernel
-                u = torch.rand(num_graphs, device=node_x.device, generator=generator)
+                if u is None:
+                    u = torch.rand(num_graphs, device=node_x.device, generator=generator)
                 out = self.actor._fused(node_x, edge_index, edge_attr, batch, num_graphs, mask=action_mask, u=u)
                 if out is not None:
+                    self.last_act_path = "fused"
                     return out[2]
+            self.last_act_path = "general"
             _, probs, _ = self.actor(node_x, edge_index, edge_attr, action_mask, batch, num_graphs=num_graphs)
         p = probs.view(num_graphs, -1)
         if deterministic:

@@ -239,6 +239,45 @@ class GraphedUpdate:
         self.g_grads, self.out = g1, out
 
 
+class GraphedAct:
+    """Trainer.act (stochastic, fused path) replayed from a HIP graph.
+
+    Acting one vector step is ~10 kernels (prologue, three GAT layers, two
+    GEMMs, the edge head with its in-kernel draw) plus the Python that builds
+    their argument blocks; at 4096 environments the host side is as long as
+    the kernels.  The graph reads the environment's persistent observation
+    buffers, the actor's prepared-weight slots (refreshed in place, eagerly,
+    when an update changed the weights: models/fused.py refresh_static) and a
+    static buffer of uniforms, drawn from the trainer's generator before each
+    replay exactly as the eager path draws them (same stream of numbers)."""
+
+    def __init__(self, trainer: "Trainer"):
+        self.tr = trainer
+        self.g = self.key = self.out = None
+        self.disabled = False
+        self.u = torch.empty(trainer.B, device=trainer.device)
+
+    def __call__(self, obs):
+        tr = self.tr
+        torch.rand(tr.B, device=tr.device, generator=tr.gen, out=self.u)
+        key = (obs.node_x.data_ptr(), obs.edge_x.data_ptr(), obs.action_mask.data_ptr())
+        if self.disabled:
+            return tr._act(obs, u=self.u)
+        fused.refresh_static(tr.agent.actor)
+        if self.g is None or key != self.key:
+            out = tr._act(obs, u=self.u)       # eager: caches (topology, slots), and which path runs
+            if tr.agent.last_act_path != "fused":
+                self.disabled = True
+                return out
+            torch.cuda.synchronize(tr.device)
+            with fused.static_weights():
+                self.g, self.out = capture_graph(lambda: tr._act(obs, u=self.u))
+            self.key = key
+            return out
+        self.g.replay()
+        return self.out
+
+
 class Trainer:
     def __init__(self, cfg: Dict, device="cuda", rank: int = 0, world: int = 1, log: bool = True):
         self.cfg, self.rank, self.world = cfg, rank, world
@@ -312,15 +351,21 @@ class Trainer:
         self._u = torch.empty(bs, dtype=torch.float64, device=self.device)      # PER draws
         self._her_u = torch.empty(bs, dtype=torch.float32, device=self.device)  # HER draws
         self._graphed = GraphedUpdate(self) if self.use_graphs else None
+        self._graphed_act = GraphedAct(self) if self.use_graphs and cfg.get("graph_act", True) else None
         self._transitions = 0   # env transitions added so far (update schedule)
 
     # ------------------------------------------------------------ acting
     def act(self, obs, deterministic=False):
+        if self._graphed_act is not None and not deterministic:
+            return self._graphed_act(obs)
+        return self._act(obs, deterministic)
+
+    def _act(self, obs, deterministic=False, u=None):
         B = self.B
         return self.agent.select_actions(obs.node_x.reshape(B * self.N, 4), self.act_ei,
                                          obs.edge_x.reshape(B * self.E, 6), obs.action_mask.reshape(-1),
                                          self.act_batch, num_graphs=B, deterministic=deterministic,
-                                         generator=self.gen)
+                                         generator=self.gen, u=u)
 
     def _reset_envs(self, done_mask: Optional[torch.Tensor]):
         env = self.env

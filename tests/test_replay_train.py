@@ -232,6 +232,39 @@ def test_graphed_update_matches_eager(tmp_path, her, hidden, embed):
 
 
 @pytest.mark.gpu
+def test_graphed_act_matches_eager(tmp_path):
+    """train.GraphedAct: the replayed acting graph draws the same actions as
+    the eager fused pass from the same generator state, across weight changes
+    (prepared-weight slots refreshed in place) and new observations written
+    into the env's persistent buffers."""
+    from trafficrl.models import fused
+    from trafficrl.train import Trainer, sf_config
+    cfg = sf_config()
+    cfg.update(num_envs=64, batch_start=64, batch_size=16, hidden_dim=64, embed_dim=256, eval_every=0,
+               output_dir=str(tmp_path), update_unit="iterations")
+    tr = Trainer(cfg, device="cuda", log=False)
+    assert tr._graphed_act is not None
+    tr._reset_envs(None)
+    obs = tr.env.observe()
+    for it in range(5):
+        st = tr.gen.get_state()
+        a_g = tr.act(obs).clone()
+        st_after = tr.gen.get_state()
+        tr.gen.set_state(st)
+        a_e = tr._act(obs)
+        assert torch.equal(tr.gen.get_state(), st_after)     # same number of draws
+        assert tr.agent.last_act_path == "fused"
+        assert torch.equal(a_g, a_e), it
+        if it >= 1:
+            assert tr._graphed_act.g is not None
+        with torch.no_grad():   # an "update": new weights, same parameter storage
+            for p in tr.agent.actor.parameters():
+                p.add_(0.05 * torch.randn_like(p))
+        fused.weights_changed()
+        obs = tr.env.step(a_e.to(torch.int32), check=False)[0]
+
+
+@pytest.mark.gpu
 def test_graph_memset_replay_selftest():
     """capture_graph rewrites captured memset nodes into fill kernels, so a
     small hipMemsetAsync replays correctly (ROCm 7.2 packet-capture defect)
