@@ -482,19 +482,44 @@ hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t str
 
 // ------------------------------------------------------------ partial sums
 // out[k] = sum_r part[r * stride + k] for r < rows, k < width, r ascending.
-__global__ void __launch_bounds__(kT) partial_sum_kernel(const float* __restrict__ part, int rows, int width,
-                                                         int64_t stride, float* __restrict__ out) {
-    const int k = blockIdx.x * kT + threadIdx.x;
-    if (k >= width) return;
+// Column sums of a [rows][width] partial block in a fixed order (deterministic):
+// 16 waves per 64 columns, wave w sums rows w, w+16, ... (loads four rows
+// ahead), then wave 0 adds the 16 wave sums in wave order.
+constexpr int kPsWaves = 16;
+__global__ void __launch_bounds__(kW * kPsWaves) partial_sum_kernel(const float* __restrict__ part, int rows, int width,
+                                                                    int64_t stride, float* __restrict__ out) {
+    __shared__ float red[kPsWaves][kW];
+    const int lane = threadIdx.x & (kW - 1), w = threadIdx.x / kW;
+    const int k = blockIdx.x * kW + lane;
     float s = 0.0f;
-    for (int r = 0; r < rows; ++r) s += part[(size_t)r * stride + k];
-    out[k] = s;
+    if (k < width) {
+        int r = w;
+        for (; r + 3 * kPsWaves < rows; r += 4 * kPsWaves) {
+            const float a0 = part[(size_t)r * stride + k];
+            const float a1 = part[(size_t)(r + kPsWaves) * stride + k];
+            const float a2 = part[(size_t)(r + 2 * kPsWaves) * stride + k];
+            const float a3 = part[(size_t)(r + 3 * kPsWaves) * stride + k];
+            s += a0;
+            s += a1;
+            s += a2;
+            s += a3;
+        }
+        for (; r < rows; r += kPsWaves) s += part[(size_t)r * stride + k];
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && k < width) {
+        float t = red[0][lane];
+#pragma unroll
+        for (int j = 1; j < kPsWaves; ++j) t += red[j][lane];
+        out[k] = t;
+    }
 }
 
 hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t stride, float* out,
                               hipStream_t stream) {
-    hipLaunchKernelGGL(partial_sum_kernel, dim3((width + kT - 1) / kT), dim3(kT), 0, stream, part, rows, width, stride,
-                       out);
+    hipLaunchKernelGGL(partial_sum_kernel, dim3((width + kW - 1) / kW), dim3(kW * kPsWaves), 0, stream, part, rows,
+                       width, stride, out);
     return hipGetLastError();
 }
 

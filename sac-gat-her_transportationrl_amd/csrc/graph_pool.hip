@@ -73,12 +73,34 @@ namespace {
 __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     const int k = blockIdx.y;
     if (k >= l.count) return;
-    const int64_t rows = l.rows[k], cols = l.cols[k], n = rows * cols;
+    // 32-bit index arithmetic (every tensor < 2^31 elements, checked at launch);
+    // four consecutive elements of one row per thread when the row length allows
+    const uint32_t cols = (uint32_t)l.cols[k], n = (uint32_t)(l.rows[k] * l.cols[k]);
     const float* src = l.src[k];
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int64_t r = i / cols, c = i - r * cols;
-        const __bf16 h = (__bf16)src[r * l.src_stride[k] + c];
-        if (l.out_bf16[k])
+    const int64_t ss = l.src_stride[k];
+    const bool bf = l.out_bf16[k] != 0;
+    const uint32_t step = gridDim.x * 256u;
+    if ((cols & 3u) == 0 && (ss & 3) == 0 && ((uintptr_t)src & 15) == 0) {
+        for (uint32_t q = blockIdx.x * 256u + threadIdx.x; 4 * q < n; q += step) {
+            const uint32_t i = 4 * q, r = i / cols, c = i - r * cols;
+            const float4 v = *reinterpret_cast<const float4*>(src + r * ss + c);
+            const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+            if (bf) {
+                uint2 u;
+                u.x = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+                u.y = (uint32_t)__builtin_bit_cast(uint16_t, h2) | ((uint32_t)__builtin_bit_cast(uint16_t, h3) << 16);
+                *reinterpret_cast<uint2*>(static_cast<uint16_t*>(l.dst[k]) + i) = u;
+            } else {
+                *reinterpret_cast<float4*>(static_cast<float*>(l.dst[k]) + i) =
+                    make_float4((float)h0, (float)h1, (float)h2, (float)h3);
+            }
+        }
+        return;
+    }
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += step) {
+        const uint32_t r = i / cols, c = i - r * cols;
+        const __bf16 h = (__bf16)src[r * ss + c];
+        if (bf)
             static_cast<uint16_t*>(l.dst[k])[i] = __builtin_bit_cast(uint16_t, h);
         else
             static_cast<float*>(l.dst[k])[i] = (float)h;
@@ -88,8 +110,13 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
 
 hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream) {
     int64_t mx = 1;
-    for (int k = 0; k < l.count; ++k) mx = l.rows[k] * l.cols[k] > mx ? l.rows[k] * l.cols[k] : mx;
-    const unsigned bx = (unsigned)((mx + 255) / 256 < 64 ? (mx + 255) / 256 : 64);
+    for (int k = 0; k < l.count; ++k) {
+        const int64_t n = l.rows[k] * l.cols[k];
+        if (n >= ((int64_t)1 << 31) || l.rows[k] * l.src_stride[k] >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+        mx = n > mx ? n : mx;
+    }
+    const int64_t blocks = (mx + 1023) / 1024;  // ~4 elements per thread
+    const unsigned bx = (unsigned)(blocks < 1024 ? blocks : 1024);
     hipLaunchKernelGGL(bf16_round_kernel, dim3(bx, l.count), dim3(256), 0, stream, l);
     return hipGetLastError();
 }
