@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 6
+#define TRX_ABI_VERSION 7
 
 /* error codes */
 #define TRX_OK 0
@@ -444,6 +444,40 @@ typedef struct trx_sac_loss_args {
     float* g_log_alpha;         /* [1] */
 } trx_sac_loss_args;
 int trx_sac_loss(const trx_sac_loss_args* a, void* stream);
+
+/* trx_sac_adam: DiscreteSAC.apply_gradients (src/rl/sac.py:224-263) after
+ * the gradients of one update sit in one flat buffer: clip_grad_norm_ per
+ * optimizer group (0 critics, 1 actor, 2 log_alpha), the three Adam steps
+ * (torch.optim.Adam, no weight decay), the log_alpha clamps and the Polyak
+ * update of the target critics, in three launches.  Segment k: parameter
+ * p (n floats), gradient at g_base + goff, moments at m / v + moff, Polyak
+ * target t (or NULL), group.  blocks: (segment, begin, end) chunks of one
+ * segment each (the host splits tensors into <= 8192-float chunks).  step[3]
+ * is incremented on the device (graph-capturable). */
+typedef struct trx_adam_seg {
+    float* p;
+    float* t;
+    int64_t goff, moff, n;
+    int32_t group, _pad;
+} trx_adam_seg;
+typedef struct trx_adam_block {
+    int32_t seg, begin, end, _pad;
+} trx_adam_block;
+typedef struct trx_adam_args {
+    const trx_adam_seg* segs;     /* device [nseg] */
+    const trx_adam_block* blocks; /* device [nblocks] */
+    int32_t nseg, nblocks;
+    const float* g_base;
+    float* m;                     /* [total] first moments */
+    float* v;                     /* [total] second moments */
+    float* partial;               /* [nblocks] scratch */
+    float* step;                  /* [3] step counts */
+    float* scal;                  /* [12] scratch: coef, step size, sqrt(bias correction 2), grad norm */
+    float lr[3], max_norm[3];     /* max_norm <= 0: no clipping */
+    float beta1, beta2, eps, tau;
+    float log_alpha_min, log_alpha_max;
+} trx_adam_args;
+int trx_sac_adam(const trx_adam_args* a, void* stream);
 
 /* ------------------------------------------------- prioritized replay
  * Sum tree of src/train.py:27-91 (ReplayBuffer) on the device: tree[1] is the

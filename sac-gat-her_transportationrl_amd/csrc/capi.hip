@@ -367,7 +367,7 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
                 acc += cost(perm[i]);
             }
             if ((int)lane_start.size() <= big_g) {
-                KMAX = T;
+                KMAX = (T + 3) & ~3;  // a multiple of the entry loops' pipeline depth (assign_big.hip kBigD)
                 break;
             }
         }
@@ -956,6 +956,16 @@ int trx_sac_loss(const trx_sac_loss_args* a, void* stream) {
         return fail(TRX_EINVAL, "sac_loss: NULL buffer");
     hipError_t e = trx::launch_sac_loss(*a, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "sac_loss launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_sac_adam(const trx_adam_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "sac_adam: NULL args");
+    if (a->nseg < 1 || a->nblocks < 1) return fail(TRX_EINVAL, "sac_adam: empty segment / block table");
+    if (!a->segs || !a->blocks || !a->g_base || !a->m || !a->v || !a->partial || !a->step || !a->scal)
+        return fail(TRX_EINVAL, "sac_adam: NULL buffer");
+    hipError_t e = trx::launch_sac_adam(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "sac_adam launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
 

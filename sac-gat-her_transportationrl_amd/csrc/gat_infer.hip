@@ -118,9 +118,10 @@ extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
 
 // ------------------------------------------------------------- layer kernel
 // IN: 0 = xh given (layers >= 1), else the layer-0 input width (4).
-template <int HC, int IN>
-__global__ void __launch_bounds__(kInferThreads) gat_layer_infer_kernel(trx_gat_layer_args a) {
+template <int HC, int IN, int NT>
+__global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int kInferThreads = NT, kInferWaves = NT / kWave;  // this instance's workgroup
     constexpr int KC = HC / 256;  // float4 chunks per lane in a row
     const int g = blockIdx.x;
     const int n = a.nodes_per_graph, H = a.heads, C = a.channels;
@@ -782,30 +783,43 @@ size_t gat_layer_infer_smem(const trx_gat_layer_args& a) {
     return b;
 }
 
-template <int HC, int IN>
+template <int HC, int IN, int NT>
 static void set_lds_attr() {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_infer_kernel<HC, IN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_infer_kernel<HC, IN, NT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
+// One workgroup per graph.  The acting pass (4096 graphs) fills the CUs with
+// 4-wave workgroups; the SAC update's passes (256 graphs: one workgroup per
+// CU) take 8-wave workgroups, so each CU still has two waves per SIMD.
 hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream) {
     const int HC = a.heads * a.channels;
     const size_t smem = gat_layer_infer_smem(a);
     static bool attr_set = false;
     if (!attr_set) {  // allow > 64 KB of dynamic LDS (gfx950: 160 KB per CU)
-        set_lds_attr<1024, 0>();
-        set_lds_attr<1024, 4>();
-        set_lds_attr<512, 0>();
-        set_lds_attr<512, 4>();
-        set_lds_attr<256, 0>();
-        set_lds_attr<256, 4>();
+        set_lds_attr<1024, 0, 256>();
+        set_lds_attr<1024, 4, 256>();
+        set_lds_attr<512, 0, 256>();
+        set_lds_attr<512, 4, 256>();
+        set_lds_attr<256, 0, 256>();
+        set_lds_attr<256, 4, 256>();
+        set_lds_attr<1024, 0, 512>();
+        set_lds_attr<1024, 4, 512>();
+        set_lds_attr<512, 0, 512>();
+        set_lds_attr<512, 4, 512>();
+        set_lds_attr<256, 0, 512>();
+        set_lds_attr<256, 4, 512>();
         attr_set = true;
     }
-    const dim3 grid(a.num_graphs), block(kInferThreads);
-#define TRX_LAYER_CASE(HCV, INV)                                                                         \
-    if (HC == HCV && a.in_dim == INV) {                                                                  \
-        hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV>), grid, block, smem, stream, a);            \
-        return hipGetLastError();                                                                        \
+    const dim3 grid(a.num_graphs);
+    const bool wide = a.num_graphs < 2048;
+#define TRX_LAYER_CASE(HCV, INV)                                                                          \
+    if (HC == HCV && a.in_dim == INV) {                                                                   \
+        if (wide)                                                                                         \
+            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 512>), grid, dim3(512), smem, stream, a); \
+        else                                                                                              \
+            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 256>), grid, dim3(256), smem, stream, a); \
+        return hipGetLastError();                                                                         \
     }
     TRX_LAYER_CASE(1024, 0)
     TRX_LAYER_CASE(1024, 4)

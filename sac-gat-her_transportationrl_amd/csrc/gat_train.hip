@@ -31,7 +31,6 @@ namespace {
 
 constexpr int kW = 64;
 constexpr int kT = 256;  // threads per workgroup
-constexpr int kNW = kT / kW;
 
 #define TRX_TDPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false))
 __device__ __forceinline__ float wsum(float v) {
@@ -71,10 +70,11 @@ __device__ __forceinline__ float hi_bf(uint32_t u) { return __uint_as_float(u & 
 // Partial-sum layout per graph (floats): [0,F) bias, [F,2F) ln weight, [2F,3F) ln
 // bias, [3F,4F) att_src, [4F,5F) att_dst; layer 0 adds [5F,9F) lin.weight (F x 4,
 // row-major), [9F,13F) input_proj.weight, [13F,14F) input_proj.bias.  F = heads*channels.
-template <int HC, int IN>
-__global__ void __launch_bounds__(kT) gat_layer_bwd_kernel(trx_gat_layer_bwd_args a) {
+template <int HC, int IN, int NT>
+__global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int KC = HC / 256;  // float4 chunks per lane in a row
+    constexpr int kT = NT, kNW = NT / kW;  // threads / waves per workgroup
     constexpr int INR = IN > 0 ? IN : 1;
     const int g = blockIdx.x;
     const int n = a.nodes_per_graph, H = a.heads, C = a.channels;
@@ -445,37 +445,40 @@ size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a) {
            (a.g_pool ? 2 * HC * 4 : 0) + (2 * me + 2 * (n + 1) + me) * 4;
 }
 
-template <int HC, int IN>
+template <int HC, int IN, int NT>
 static void set_bwd_lds_attr() {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_bwd_kernel<HC, IN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_bwd_kernel<HC, IN, NT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
+// One workgroup per graph and ~144 KB of LDS for HC 1024: one workgroup per
+// CU, so the waves per workgroup are the occupancy -- 8 (two per SIMD) where
+// the registers allow it (HC 1024: up to 218 VGPRs), 16 for the narrower layers.
 hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t stream) {
     static bool attr_set = false;
     if (!attr_set) {
-        set_bwd_lds_attr<1024, 0>();
-        set_bwd_lds_attr<1024, 4>();
-        set_bwd_lds_attr<512, 0>();
-        set_bwd_lds_attr<512, 4>();
-        set_bwd_lds_attr<256, 0>();
-        set_bwd_lds_attr<256, 4>();
+        set_bwd_lds_attr<1024, 0, 512>();
+        set_bwd_lds_attr<1024, 4, 512>();
+        set_bwd_lds_attr<512, 0, 1024>();
+        set_bwd_lds_attr<512, 4, 1024>();
+        set_bwd_lds_attr<256, 0, 1024>();
+        set_bwd_lds_attr<256, 4, 1024>();
         attr_set = true;
     }
     const int HC = a.heads * a.channels;
     const size_t smem = gat_layer_bwd_smem(a);
-    const dim3 grid(a.num_graphs), block(kT);
-#define TRX_BWD_CASE(HCV, INV)                                                                 \
-    if (HC == HCV && a.in_dim == INV) {                                                        \
-        hipLaunchKernelGGL((gat_layer_bwd_kernel<HCV, INV>), grid, block, smem, stream, a);    \
-        return hipGetLastError();                                                              \
+    const dim3 grid(a.num_graphs);
+#define TRX_BWD_CASE(HCV, INV, NTV)                                                                    \
+    if (HC == HCV && a.in_dim == INV) {                                                                \
+        hipLaunchKernelGGL((gat_layer_bwd_kernel<HCV, INV, NTV>), grid, dim3(NTV), smem, stream, a);   \
+        return hipGetLastError();                                                                      \
     }
-    TRX_BWD_CASE(1024, 0)
-    TRX_BWD_CASE(1024, 4)
-    TRX_BWD_CASE(512, 0)
-    TRX_BWD_CASE(512, 4)
-    TRX_BWD_CASE(256, 0)
-    TRX_BWD_CASE(256, 4)
+    TRX_BWD_CASE(1024, 0, 512)
+    TRX_BWD_CASE(1024, 4, 512)
+    TRX_BWD_CASE(512, 0, 1024)
+    TRX_BWD_CASE(512, 4, 1024)
+    TRX_BWD_CASE(256, 0, 1024)
+    TRX_BWD_CASE(256, 4, 1024)
 #undef TRX_BWD_CASE
     return hipErrorInvalidValue;
 }

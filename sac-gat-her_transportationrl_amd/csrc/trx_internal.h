@@ -209,6 +209,7 @@ hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t st
 size_t gat_prologue_bwd_smem(const trx_gat_prologue_bwd_args& a);
 hipError_t launch_gat_prologue_bwd(const trx_gat_prologue_bwd_args& a, hipStream_t stream);
 hipError_t launch_sac_loss(const trx_sac_loss_args& a, hipStream_t stream);
+hipError_t launch_sac_adam(const trx_adam_args& a, hipStream_t stream);
 hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* pri, int n,
                              hipStream_t stream);
 hipError_t launch_per_update_range(double* tree, int64_t capacity, int64_t lo, const double* pri, int n,

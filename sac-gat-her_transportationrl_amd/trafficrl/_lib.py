@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 6
+ABI_VERSION = 7
 SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
@@ -31,7 +31,7 @@ EXPORTS = (
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
     "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
     "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_gat_prologue_backward",
-    "trx_sac_loss",
+    "trx_sac_loss", "trx_sac_adam",
 )
 
 
@@ -157,6 +157,22 @@ class TrxSacLossArgs(ctypes.Structure):
     ]
 
 
+class TrxAdamSeg(ctypes.Structure):
+    """trx_adam_seg (include/trafficrl.h): 48 bytes."""
+    _fields_ = [("p", _vp), ("t", _vp), ("goff", ctypes.c_int64), ("moff", ctypes.c_int64), ("n", ctypes.c_int64),
+                ("group", _i32), ("_pad", _i32)]
+
+
+class TrxAdamArgs(ctypes.Structure):
+    """trx_adam_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("segs", _vp), ("blocks", _vp), ("nseg", _i32), ("nblocks", _i32), ("g_base", _vp), ("m", _vp), ("v", _vp),
+        ("partial", _vp), ("step", _vp), ("scal", _vp), ("lr", _f32 * 3), ("max_norm", _f32 * 3),
+        ("beta1", _f32), ("beta2", _f32), ("eps", _f32), ("tau", _f32), ("log_alpha_min", _f32),
+        ("log_alpha_max", _f32),
+    ]
+
+
 MAX_ROUND = 16
 
 
@@ -229,6 +245,7 @@ def load():
     L.trx_partial_sum.argtypes = [_vp, _i32, _i32, ctypes.c_int64, _vp, _vp]
     L.trx_gat_prologue_backward.argtypes = [ctypes.POINTER(TrxGatPrologueBwdArgs), _vp]
     L.trx_sac_loss.argtypes = [ctypes.POINTER(TrxSacLossArgs), _vp]
+    L.trx_sac_adam.argtypes = [ctypes.POINTER(TrxAdamArgs), _vp]
     L.trx_env_kernel_name.argtypes = [_vp, ctypes.POINTER(TrxParams)]
     L.trx_env_kernel_name.restype = ctypes.c_char_p
     L.trx_graph_create.argtypes = [ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp,
@@ -293,7 +310,7 @@ def load():
                  "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
                  "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
                  "trx_episode_step", "trx_gat_layer_backward", "trx_partial_sum", "trx_gat_prologue_backward",
-                 "trx_sac_loss"):
+                 "trx_sac_loss", "trx_sac_adam"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

@@ -194,6 +194,7 @@ def clip_grad_norm_listwise_(params, max_norm: float):
 FUSED_INFERENCE = True   # module switch (tests compare both paths)
 FUSED_EDGE_TRAIN = True  # training-path edge scorer kernels (tests compare both paths)
 FUSED_UPDATE = True      # whole-update fused path (rl/fused_update.py) for regular bf16 batches
+FLAT_ADAM = True         # optimizer step over the fused update's flat gradient buffer (rl/flat_adam.py)
 
 
 def _fused_topology(encoder, node_x, edge_index, batch, B, head=None):
@@ -561,9 +562,33 @@ class DiscreteSAC:
                     t.record_stream(main)
         return outs
 
+    def _flat_opt(self):
+        """The flat-buffer optimizer step (rl/flat_adam.py), or None where it
+        does not apply (CPU, shared critic encoder, non-default Adam options)."""
+        fa = getattr(self, "_flat_adam", None)
+        if fa is None:
+            if not (FLAT_ADAM and self.log_alpha.is_cuda and not self.share_critic_encoder):
+                return None
+            for opt in (self.critic_opt, self.actor_opt, self.alpha_opt):
+                d = opt.defaults
+                if d.get("weight_decay", 0) != 0 or d.get("amsgrad") or d.get("maximize") or len(opt.param_groups) != 1:
+                    return None
+            from .flat_adam import FlatAdam
+            fa = self._flat_adam = FlatAdam(self)
+        return fa
+
     def apply_gradients(self, alpha_max: float = None):
         """Clipping, the three optimizer steps, the log_alpha clamps and the
-        Polyak target update (sac.py:224-263), in the reference's order."""
+        Polyak target update (sac.py:224-263), in the reference's order.  After
+        a fused update: one trx_sac_adam call over the flat gradient buffer."""
+        fa = self._flat_opt()
+        if fa is not None and getattr(self, "last_update_path", None) == "fused" and fa.usable():
+            fa.step([o.param_groups[0]["lr"] for o in (self.critic_opt, self.actor_opt, self.alpha_opt)],
+                    self.grad_clip, self.target_tau, alpha_max)
+            fused.weights_changed()
+            return
+        if fa is not None and fa.owner == "flat":
+            fa.export_torch()
         clip = self.grad_clip is not None and self.grad_clip > 0
         if clip:
             clip_grad_norm_listwise_(list(self.critic1.parameters()) + list(self.critic2.parameters()), self.grad_clip)
@@ -601,6 +626,11 @@ class DiscreteSAC:
                     "target2": self.target2.state_dict(), "log_alpha": self.log_alpha.detach().cpu()}, path)
 
     def load(self, path: str, map_location: str = "cpu"):
+        fa = getattr(self, "_flat_adam", None)
+        if fa is not None:   # hand the moments back before log_alpha / alpha_opt are replaced
+            if fa.owner == "flat":
+                fa.export_torch()
+            self._flat_adam = None
         state = torch.load(path, map_location=map_location, weights_only=True)
         self.actor.load_state_dict(state["actor"])
         self.critic1.load_state_dict(state["critic1"])
