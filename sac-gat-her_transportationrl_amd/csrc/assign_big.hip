@@ -139,115 +139,6 @@ __device__ __forceinline__ void exact_replay(const DevGraph& g, const float* tt,
     exact_sssp_links(g.N, g.b_indptr, g.b_indices, ce, [tt, ce](int j) { return tt[ce[j]]; }, origin, &fb, pe);
 }
 
-constexpr int kBigD = 4;  // prefetch depth of the predecessor pass (the host pads KMAX to a multiple of 4)
-
-// One Gauss-Seidel sweep over this lane's entries (FWD: ascending, group end =
-// last flag; else descending, group end = first flag).  Returns whether a
-// label improved.  Two entries in flight: entry k + 2's label loads are issued
-// right after entry k's store, so only entry k + 1's write can be missing
-// from them -- forwarded from a one-entry record (exact Gauss-Seidel order).
-template <bool FWD>
-__device__ __forceinline__ bool label_sweep(const uint2* __restrict__ ent, double* __restrict__ dist, const int KMAX,
-                                            const int G, const int lt) {
-    auto at = [&](int i) {
-        const int c = i < KMAX ? i : KMAX - 1;
-        return ent[(FWD ? c : KMAX - 1 - c) * G + lt];
-    };
-    uint2 ea[2], eb[2];
-    double xu[2], xv[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) ea[j] = at(j);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        xu[j] = dist[ea[j].x & 0xFFFF];
-        xv[j] = dist[(ea[j].x >> 16) & 0x3FFF];
-        eb[j] = at(2 + j);
-    }
-    int wv = -1;  // node written by the previous entry (-1: none), and its label
-    double wm = 0.0;
-    bool changed = false;
-    double m = kInfD;
-    for (int i0 = 0; i0 < KMAX; i0 += 2) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint2 e = ea[j];
-            const int u = e.x & 0xFFFF, v = (e.x >> 16) & 0x3FFF;
-            const double x = wv == u ? wm : xu[j];
-            m = __builtin_fmin(m, __dadd_rn(x, (double)__uint_as_float(e.y)));
-            const bool end = FWD ? (e.x >> 31) != 0 : ((e.x >> 30) & 1u) != 0;
-            const bool better = end && m < xv[j];  // strict improvement
-            if (better) dist[v] = m;
-            wv = better ? v : -1;
-            wm = m;
-            changed |= better;
-            m = end ? kInfD : m;
-            ea[j] = eb[j];  // entry i0 + j + 2: loads issued after this entry's store
-            xu[j] = dist[ea[j].x & 0xFFFF];
-            xv[j] = dist[(ea[j].x >> 16) & 0x3FFF];
-            eb[j] = at(i0 + j + 4);
-        }
-    }
-    return changed;
-}
-
-// Predecessor of every reached node: scipy keeps the first scanned tail
-// achieving d[v], i.e. the achieving tail of smallest label; true when some
-// node has two achieving tails of equal smallest label (heap order decides).
-__device__ __forceinline__ bool pred_pass(const uint2* __restrict__ ent, const int16_t* __restrict__ lnk,
-                                          const double* __restrict__ dist, int32_t* __restrict__ pe, const int KMAX,
-                                          const int G, const int lt, const int origin, const int N) {
-    constexpr int D = kBigD;
-    uint2 ea[D];
-    double du[D], dv[D];
-    int lk[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const int c = j < KMAX ? j : KMAX - 1;
-        ea[j] = ent[c * G + lt];
-        lk[j] = lnk[c * G + lt];
-        du[j] = dist[ea[j].x & 0xFFFF];
-        dv[j] = dist[(ea[j].x >> 16) & 0x3FFF];
-    }
-    bool amb = false;
-    double mdu = kInfD;
-    int cnt = 0, best = -1;
-    for (int i0 = 0; i0 < KMAX; i0 += D) {
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const uint2 e = ea[j];
-            const double xu = du[j], xv = dv[j];
-            const int link = lk[j];
-            const int c = i0 + j + D < KMAX ? i0 + j + D : KMAX - 1;  // prefetch entry i0 + j + D
-            ea[j] = ent[c * G + lt];
-            lk[j] = lnk[c * G + lt];
-            du[j] = dist[ea[j].x & 0xFFFF];
-            dv[j] = dist[(ea[j].x >> 16) & 0x3FFF];
-            if ((e.x >> 30) & 1u) {
-                mdu = kInfD;
-                cnt = 0;
-                best = -1;
-            }
-            const int u = e.x & 0xFFFF, v = (e.x >> 16) & 0x3FFF;
-            const double nd = __dadd_rn(xu, (double)__uint_as_float(e.y));
-            if (nd == xv && xv < kInfD) {
-                if (xu < mdu) {
-                    mdu = xu;
-                    cnt = 1;
-                    best = (int)(uint16_t)link | (u << 16);
-                } else if (xu == mdu) {
-                    ++cnt;
-                }
-            }
-            if (e.x >> 31) {
-                const bool real = v != origin && v < N && xv < kInfD;
-                if (v < N) pe[v] = real ? best : -1;
-                amb |= real && cnt > 1;
-            }
-        }
-    }
-    return amb;
-}
-
 }  // namespace
 
 // entry word: u | v << 16 | first << 30 | last << 31 (u, v: DFS positions)
@@ -361,14 +252,40 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
             for (int v = lt; v <= N; v += G) dist[v] = v == origin ? 0.0 : kInfD;
             for (int v = lt; v < N; v += G) pe[v] = -1;
             wave_sync();
-            // ---------------- labels: alternating Gauss-Seidel sweeps (label_sweep:
-            // two entries' label loads in flight, the previous entry's write
-            // forwarded in registers -- the same order of updates as one entry
-            // at a time).
+            // ---------------- labels: alternating Gauss-Seidel sweeps.  Branch-free
+            // entry step (the own label is re-stored at every entry, changed
+            // only at a group end) and the next entry word prefetched, so the
+            // per-entry chain is one label load pair and one store.
+            auto relax = [&](const uint2 e, const bool end, double& m, bool& changed) {
+                const int v = (e.x >> 16) & 0x3FFF;
+                const double xu = dist[e.x & 0xFFFF], dv = dist[v];
+                m = __builtin_fmin(m, __dadd_rn(xu, (double)__uint_as_float(e.y)));
+                const bool better = end && m < dv;  // strict improvement
+                dist[v] = better ? m : dv;
+                changed |= better;
+                m = end ? kInfD : m;
+            };
             int dir = 0;
             for (int sweep = 0; sweep <= N; ++sweep) {
-                const bool changed = dir == 0 ? label_sweep<true>(ent, dist, KMAX, G, lt)
-                                              : label_sweep<false>(ent, dist, KMAX, G, lt);
+                bool changed = false;
+                double m = kInfD;
+                if (dir == 0) {
+                    uint2 e = ent[lt];
+#pragma unroll 2
+                    for (int k = 0; k < KMAX; ++k) {
+                        const uint2 en = ent[(k + 1 < KMAX ? k + 1 : k) * G + lt];
+                        relax(e, (e.x >> 31) != 0, m, changed);
+                        e = en;
+                    }
+                } else {
+                    uint2 e = ent[(KMAX - 1) * G + lt];
+#pragma unroll 2
+                    for (int k = KMAX - 1; k >= 0; --k) {
+                        const uint2 en = ent[(k > 0 ? k - 1 : k) * G + lt];
+                        relax(e, ((e.x >> 30) & 1u) != 0, m, changed);
+                        e = en;
+                    }
+                }
                 wave_sync();
                 if (__ballot(changed) == 0) {
                     TRX_BIG_COUNT(1, (sweep + 1) * ((Z - z0) < TPW ? (Z - z0) : TPW));
@@ -378,9 +295,37 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
             }
             [[maybe_unused]] unsigned long long clk1 = TRX_BIG_CLOCK();
             TRX_BIG_COUNT(3, clk1 - clk0);
-            // ---------------- predecessors: smallest-label achieving tail (labels
-            // final: the loads run kBigD entries ahead with nothing to forward)
-            const bool amb = pred_pass(ent, lnk, dist, pe, KMAX, G, lt, origin, N);
+            // ---------------- predecessors: smallest-label achieving tail
+            bool amb = false;
+            {
+                double mdu = kInfD;
+                int cnt = 0, best = -1;
+                for (int k = 0; k < KMAX; ++k) {
+                    const uint2 e = ent[k * G + lt];
+                    if ((e.x >> 30) & 1u) {
+                        mdu = kInfD;
+                        cnt = 0;
+                        best = -1;
+                    }
+                    const int u = e.x & 0xFFFF, v = (e.x >> 16) & 0x3FFF;
+                    const double du = dist[u], dv = dist[v];
+                    const double nd = __dadd_rn(du, (double)__uint_as_float(e.y));
+                    if (nd == dv && dv < kInfD) {
+                        if (du < mdu) {
+                            mdu = du;
+                            cnt = 1;
+                            best = (int)(uint16_t)lnk[k * G + lt] | (u << 16);
+                        } else if (du == mdu) {
+                            ++cnt;
+                        }
+                    }
+                    if (e.x >> 31) {
+                        const bool real = v != origin && v < N && dv < kInfD;
+                        if (v < N) pe[v] = real ? best : -1;
+                        amb |= real && cnt > 1;
+                    }
+                }
+            }
             wave_sync();
             const uint64_t ambm = __ballot(amb);
             [[maybe_unused]] unsigned long long clk2 = TRX_BIG_CLOCK();
@@ -391,36 +336,21 @@ __global__ void __launch_bounds__(512) env_kernel_big(const DevGraph g, const tr
                 if (mine != 0 && lt == 0) exact_replay(g, tt, origin, fib_slot, pe);
                 wave_sync();
             }
-            // ---------------- all-or-nothing by path walks (repair_env.py:490-502, 707-722),
-            // a lane's destinations two at a time: both pointer chases in flight
+            // ---------------- all-or-nothing by path walks (repair_env.py:490-502, 707-722)
             if (on) {
-                const int qend = g.od_ptr[zi + 1];
-                for (int qa = g.od_ptr[zi] + lt; qa < qend; qa += 2 * G) {
-                    int vw[2];
-                    uint32_t dw[2];
-#pragma unroll
-                    for (int w = 0; w < 2; ++w) {
-                        const int q = qa + w * G;
-                        vw[w] = -1;
-                        dw[w] = 0;
-                        if (q < qend) {
-                            const int d = g.b_od_dst[q];
-                            const float dm = g.od_dem[q];
-                            if (d == origin || pe[d] < 0) {
-                                un += dm;  // intrazonal or unreachable (708-709)
-                            } else {
-                                vw[w] = d;
-                                dw[w] = (uint32_t)dm;  // integral demands: u32 atomics
-                            }
-                        }
+                for (int q = g.od_ptr[zi] + lt; q < g.od_ptr[zi + 1]; q += G) {
+                    const int d = g.b_od_dst[q];
+                    const float dm = g.od_dem[q];
+                    if (d == origin || pe[d] < 0) {
+                        un += dm;  // intrazonal or unreachable (708-709)
+                        continue;
                     }
-                    for (int h = 0; h < N && (vw[0] >= 0 || vw[1] >= 0); ++h) {
-                        const int pk0 = vw[0] >= 0 ? pe[vw[0]] : -1;
-                        const int pk1 = vw[1] >= 0 ? pe[vw[1]] : -1;
-                        if (pk0 >= 0) atomicAdd(&auxi[pk0 & 0xFFFF], dw[0]);
-                        if (pk1 >= 0) atomicAdd(&auxi[pk1 & 0xFFFF], dw[1]);
-                        vw[0] = pk0 < 0 || (pk0 >> 16) == origin ? -1 : pk0 >> 16;
-                        vw[1] = pk1 < 0 || (pk1 >> 16) == origin ? -1 : pk1 >> 16;
+                    int v = d;
+                    for (int h = 0; h < N && v != origin; ++h) {
+                        const int pk = pe[v];
+                        if (pk < 0) break;
+                        atomicAdd(&auxi[pk & 0xFFFF], (uint32_t)dm);  // integral demands: u32 atomics
+                        v = pk >> 16;
                     }
                 }
             }

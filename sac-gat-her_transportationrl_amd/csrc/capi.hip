@@ -367,7 +367,7 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
                 acc += cost(perm[i]);
             }
             if ((int)lane_start.size() <= big_g) {
-                KMAX = (T + 3) & ~3;  // a multiple of the entry loops' pipeline depth (assign_big.hip kBigD)
+                KMAX = T;
                 break;
             }
         }

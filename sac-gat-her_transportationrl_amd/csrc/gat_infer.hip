@@ -90,8 +90,9 @@ typedef unsigned int trx_u4 __attribute__((ext_vector_type(4)));
 
 #ifdef TRX_PHASE_STAMPS
 // Diagnostic build only (make stamps): per-phase cycle totals of the layer
-// kernel, thread 0 of each workgroup, rows 0 = layer 0, 1 = HC 1024, 2 = other.
-__device__ unsigned long long trx_infer_cycles[3][8];
+// kernel, thread 0 of each workgroup, rows 0 = layer 0, 1 = HC 1024, 2 = other;
+// row 3 = the edge scorer (stage, links, softmax, draw).
+__device__ unsigned long long trx_infer_cycles[4][8];
 #define TRX_ISTAMP(slot)                                                      \
     do {                                                                      \
         if (threadIdx.x == 0) {                                               \
@@ -100,18 +101,29 @@ __device__ unsigned long long trx_infer_cycles[3][8];
             stamp_prev_ = now_;                                               \
         }                                                                     \
     } while (0)
+#define TRX_ESTAMP(slot)                                                      \
+    do {                                                                      \
+        if (threadIdx.x == 0) {                                               \
+            unsigned long long now_ = __builtin_amdgcn_s_memtime();            \
+            atomicAdd(&trx_infer_cycles[3][slot], now_ - stamp_prev_);        \
+            stamp_prev_ = now_;                                               \
+        }                                                                     \
+    } while (0)
 extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -2;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_infer_cycles), sizeof(unsigned long long) * 24) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_infer_cycles), sizeof(unsigned long long) * 32) != hipSuccess)
         return -2;
     if (reset) {
-        unsigned long long z[24] = {};
+        unsigned long long z[32] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(trx_infer_cycles), z, sizeof(z)) != hipSuccess) return -2;
     }
     return 0;
 }
 #else
 #define TRX_ISTAMP(slot) \
+    do {                 \
+    } while (0)
+#define TRX_ESTAMP(slot) \
     do {                 \
     } while (0)
 #endif
@@ -409,6 +421,9 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
             a.save_stats[2 * (size_t)node] = mean;
             a.save_stats[2 * (size_t)node + 1] = rstd;
         }
+        float xr[IN > 0 ? IN : 1];  // the node's layer-0 inputs in registers (the LDS pool stores below
+#pragma unroll                      // would otherwise force a reload per column)
+        for (int j = 0; j < (IN > 0 ? IN : 1); ++j) xr[j] = IN > 0 ? x0l[i * IN + j] : 0.0f;
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
             const int f0 = 4 * (lane + kWave * k);
@@ -420,7 +435,7 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
                 if (IN > 0 && a.residual == 2) {
                     float t = 0.0f;
 #pragma unroll
-                    for (int j = 0; j < (IN > 0 ? IN : 1); ++j) t += x0l[i * IN + j] * wp_r[k][r][j];
+                    for (int j = 0; j < (IN > 0 ? IN : 1); ++j) t += xr[j] * wp_r[k][r][j];
                     y = y + bf16r(t + bp_r[k][r]);
                 } else if (a.residual == 1) {
                     y = y + resv[r];
@@ -475,6 +490,9 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
     const int g = blockIdx.x;
     const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
+#ifdef TRX_PHASE_STAMPS
+    unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+#endif
     uint16_t* pr = reinterpret_cast<uint16_t*>(smem);               // [n][2*Hd] bf16
     float* eal = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);  // [E][ED] bf16-rounded features
     float* lg = eal + (size_t)E * ED;                                // [E] logits
@@ -555,6 +573,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         return;
     }
 
+    TRX_ESTAMP(0);
     constexpr int EU = 2;  // links per wave iteration
     for (int e0 = wave * EU; e0 < E; e0 += kInferWaves * EU) {
         float part[EU];
@@ -598,6 +617,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         }
     }
     __syncthreads();
+    TRX_ESTAMP(1);
     if (!a.softmax) {
         for (int e = tid; e < E; e += kInferThreads) a.out[(int64_t)g * E + e] = lg[e];
         return;
@@ -612,6 +632,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
     for (int e0 = 0; e0 < E; e0 += kWave) ssum += wave_sum_f(e0 + lane < E ? expf(lg[e0 + lane] - m) : 0.0f);
     const float denom = ssum + 1e-16f;
     for (int e = lane; e < E; e += kWave) a.out[(int64_t)g * E + e] = expf(lg[e] - m) / denom;
+    TRX_ESTAMP(2);
     if (a.u && lane == 0) {  // one categorical draw per graph (inverse CDF over the same exp terms)
         const float target = a.u[g] * ssum;
         float acc = 0.0f;
@@ -624,6 +645,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         }
         a.action[g] = pick >= 0 ? pick : last;  // u * total above the serial sum: last link with mass
     }
+    TRX_ESTAMP(3);
 }
 
 // -------------------------------------------------------------- prologue
@@ -665,29 +687,31 @@ __device__ __forceinline__ void layer_norm_row(float (&x)[kProMD], int d, const 
         if (j < d) x[j] = (x[j] - mu) * r * w[j] + b[j];
 }
 
-// One wave per graph: input LayerNorms, self-loop means, a_edge of every
-// layer in CSR order.  The self-loop sums walk the links in order, broadcast
-// 64 at a time with readlane (no LDS round trip per link).
-__global__ void __launch_bounds__(kWave) gat_prologue_kernel(trx_gat_prologue_args a, int A) {
+// One workgroup per graph: input LayerNorms, self-loop means, a_edge of every
+// layer in CSR order.  A node's self-loop attr is the mean over its kept
+// in-links, summed in link order: its CSR-by-destination row lists them in
+// that order (stable sort by destination), so each node walks only its own
+// row.  NT threads per graph: 128 for the acting pass, 256 for the 256-graph
+// update batches (one workgroup per CU either way has work for every SIMD).
+template <int NT>
+__global__ void __launch_bounds__(NT) gat_prologue_kernel(trx_gat_prologue_args a, int A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MD = kProMD;
-    const int g = blockIdx.x, lane = threadIdx.x;
+    const int g = blockIdx.x, tid = threadIdx.x;
     const int n = a.nodes_per_graph, E = a.edges_per_graph, ND = a.node_dim, D = a.edge_dim;
     float* ean = reinterpret_cast<float*>(smem);  // [E][8] normalised link features
     float* lp = ean + E * MD;                     // [n][8] self-loop attrs
     float* Ml = lp + n * MD;                      // [A][8] bf16-rounded M rows
-    int* ld = reinterpret_cast<int*>(Ml + A * MD);  // [E] graph-local dst of kept links, else -1
     const int64_t node0 = (int64_t)g * n, link0 = (int64_t)g * E;
     const int p0 = a.rowptr[node0], p1 = a.rowptr[node0 + n];
-    for (int v = lane; v < A * D; v += kWave) {
+    for (int v = tid; v < A * D; v += NT) {
         const int k = v / D, j = v - (v / D) * D;
         Ml[k * MD + j] = bf16r(a.m_work[v]);
     }
-    for (int l = lane; l < E; l += kWave) {
+    for (int l = tid; l < E; l += NT) {
         float x[MD];
 #pragma unroll
         for (int j = 0; j < MD; ++j) x[j] = j < D ? a.edge_x[(link0 + l) * D + j] : 0.0f;
-        const int64_t s = a.src[link0 + l] - node0, d = a.dst[link0 + l] - node0;
         layer_norm_row(x, D, a.edge_ln_w, a.edge_ln_b, a.edge_ln_eps);
 #pragma unroll
         for (int j = 0; j < MD; ++j)
@@ -695,9 +719,8 @@ __global__ void __launch_bounds__(kWave) gat_prologue_kernel(trx_gat_prologue_ar
                 ean[l * MD + j] = x[j];
                 a.ea[(link0 + l) * D + j] = x[j];
             }
-        ld[l] = (s == d || d < 0 || d >= n) ? -1 : (int)d;
     }
-    for (int i = lane; i < n; i += kWave) {
+    for (int i = tid; i < n; i += NT) {
         float x[MD];
 #pragma unroll
         for (int j = 0; j < MD; ++j) x[j] = j < ND ? a.node_x[(node0 + i) * ND + j] : 0.0f;
@@ -707,37 +730,27 @@ __global__ void __launch_bounds__(kWave) gat_prologue_kernel(trx_gat_prologue_ar
             if (j < ND) a.x0[(node0 + i) * ND + j] = x[j];
     }
     __syncthreads();
-    {  // self-loop attr of node i = lane: mean over kept in-links, in link order (n <= 64)
+    for (int i = tid; i < n; i += NT) {  // self-loop attr: mean over the kept in-links of i, in link order
         float s[MD];
 #pragma unroll
         for (int j = 0; j < MD; ++j) s[j] = 0.0f;
         int cnt = 0;
-        for (int c0 = 0; c0 < E; c0 += kWave) {
-            const int l = c0 + lane;
-            const int myd = l < E ? ld[l] : -1;
-            float myv[MD];
-#pragma unroll
-            for (int j = 0; j < MD; ++j) myv[j] = (l < E && j < D) ? ean[l * MD + j] : 0.0f;
-            const int lim = E - c0 < kWave ? E - c0 : kWave;
-            for (int k = 0; k < lim; ++k) {
-                const bool hit = __builtin_amdgcn_readlane(myd, k) == lane;
-                cnt += hit;
-#pragma unroll
-                for (int j = 0; j < MD; ++j) {
-                    const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(myv[j]), k));
-                    if (hit && j < D) s[j] += v;
-                }
-            }
-        }
-        if (lane < n) {
-            const float deg = cnt > 0 ? (float)cnt : 1.0f;
+        for (int p = a.rowptr[node0 + i]; p < a.rowptr[node0 + i + 1]; ++p) {
+            const int code = a.pos_src[p];
+            const int64_t li = (int64_t)code - link0;
+            if (code < 0 || li < 0 || li >= E) continue;  // the appended self loop (or a foreign link)
+            ++cnt;
 #pragma unroll
             for (int j = 0; j < MD; ++j)
-                if (j < D) lp[lane * MD + j] = s[j] / deg;
+                if (j < D) s[j] += ean[li * MD + j];
         }
+        const float deg = cnt > 0 ? (float)cnt : 1.0f;
+#pragma unroll
+        for (int j = 0; j < MD; ++j)
+            if (j < D) lp[i * MD + j] = s[j] / deg;
     }
     __syncthreads();
-    for (int p = p0 + lane; p < p1; p += kWave) {
+    for (int p = p0 + tid; p < p1; p += NT) {
         const int code = a.pos_src[p];
         const int64_t li = (int64_t)code - link0, ni = -(int64_t)code - 1 - node0;
         const bool ok = code >= 0 ? (li >= 0 && li < E) : (ni >= 0 && ni < n);
@@ -766,7 +779,10 @@ hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t strea
     int A = 0;
     for (int l = 0; l < a.num_layers; ++l) A += a.heads[l];
     hipLaunchKernelGGL(edge_att_weights_kernel, dim3(A * a.edge_dim), dim3(kWave), 0, stream, a);
-    hipLaunchKernelGGL(gat_prologue_kernel, dim3(a.num_graphs), dim3(kWave), gat_prologue_smem(a), stream, a, A);
+    if (a.num_graphs < 2048)
+        hipLaunchKernelGGL(gat_prologue_kernel<256>, dim3(a.num_graphs), dim3(256), gat_prologue_smem(a), stream, a, A);
+    else
+        hipLaunchKernelGGL(gat_prologue_kernel<128>, dim3(a.num_graphs), dim3(128), gat_prologue_smem(a), stream, a, A);
     return hipGetLastError();
 }
 
@@ -839,7 +855,11 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 // gradient and d relu = bf16(g * w2) are bf16, relu backward on the fp32 z,
 // the gradient reaching the bf16 sum of the gathers and the link term is
 // rounded to bf16 (grad_z), p gradients are fp32 sums over the graph's links
-// (thread k owns LDS column k: no atomics) rounded to bf16 at the end.
+// (fixed link order) rounded to bf16 at the end.  Two passes, no LDS
+// read-modify-write chains: (1) per link, thread k's gradient through unit k
+// (stored bf16 in LDS: it is bf16-rounded anyway) with grad_c / grad_w2 sums;
+// (2) per node, the sums over its out-links (p[:, :H]) and in-links
+// (p[:, H:]) in link order from per-node link lists.
 // Outputs: grad_p [N, 2H] bf16, grad_c [B, H], grad_z [E_total, H] bf16 (for
 // the link-feature weight / input gradients, GEMMs on the host side) and
 // grad_w2_part [B, H] (per-graph sums of bf16(g) * bf16(relu(z))).
@@ -850,20 +870,22 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
     constexpr int ED = kEdgeED;
     const int g = blockIdx.x, k = threadIdx.x;
     const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
-    uint16_t* pr = reinterpret_cast<uint16_t*>(smem);                 // [n][2*Hd] bf16
-    float* gps = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);   // [n][Hd] grad of p[:, :Hd]
-    float* gpd = gps + (size_t)n * Hd;                                 // [n][Hd] grad of p[:, Hd:]
-    float* eal = gpd + (size_t)n * Hd;                                 // [E][ED] bf16-rounded link features
-    float* gl = eal + (size_t)E * ED;                                  // [E] bf16(grad logit)
-    int* sl = reinterpret_cast<int*>(gl + E);                          // [E]
-    int* dl = sl + E;                                                  // [E]
+    uint16_t* pr = reinterpret_cast<uint16_t*>(smem);                   // [n][2*Hd] bf16
+    uint16_t* dzs = pr + (size_t)n * 2 * Hd;                            // [E][Hd] bf16 dL/dz
+    float* eal = reinterpret_cast<float*>(dzs + (size_t)E * Hd + ((E * Hd) & 1));  // [E][ED] link features
+    float* gl = eal + (size_t)E * ED;                                   // [E] bf16(grad logit)
+    int* sl = reinterpret_cast<int*>(gl + E);                           // [E]
+    int* dl = sl + E;                                                   // [E]
+    int* lo = dl + E;                                                   // [E] links by source node, link order
+    int* li = lo + E;                                                   // [E] links by destination node
+    int* op = li + E;                                                   // [n+1] out-list offsets
+    int* ip = op + n + 1;                                               // [n+1] in-list offsets
     const int64_t node0 = (int64_t)g * n;
     {
         const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.p) + node0 * 2 * Hd);
         trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
         for (int v = k; v < n * 2 * Hd / 8; v += kInferThreads) dst4[v] = src4[v];
     }
-    for (int v = k; v < n * Hd; v += kInferThreads) gps[v] = gpd[v] = 0.0f;
     for (int e = k; e < E; e += kInferThreads) {
         const int64_t eg = (int64_t)g * E + e;
         int s = (int)(a.src[eg] - node0), d = (int)(a.dst[eg] - node0);
@@ -883,8 +905,32 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
     for (int j = 0; j < ED; ++j) we[j] = (on && j < D) ? a.we[k * D + j] : 0.0f;
     const float w2 = on ? a.w2[k] : 0.0f, ck = on ? a.c[(int64_t)g * Hd + k] : 0.0f;
     __syncthreads();
+    if (k < n) {  // per-node link lists (link order); counts first
+        int co = 0, ci = 0;
+        for (int e = 0; e < E; ++e) {
+            co += sl[e] == k;
+            ci += dl[e] == k;
+        }
+        op[k + 1] = co;
+        ip[k + 1] = ci;
+    }
+    if (k == 0) op[0] = ip[0] = 0;
+    __syncthreads();
+    if (k == 0)
+        for (int i = 0; i < n; ++i) {
+            op[i + 1] += op[i];
+            ip[i + 1] += ip[i];
+        }
+    __syncthreads();
+    if (k < n) {
+        int wo = op[k], wi = ip[k];
+        for (int e = 0; e < E; ++e) {
+            if (sl[e] == k) lo[wo++] = e;
+            if (dl[e] == k) li[wi++] = e;
+        }
+    }
     float gc = 0.0f, gw2 = 0.0f;
-    if (on) {
+    if (on) {  // (1) per link
         for (int e = 0; e < E; ++e) {
             const int s = sl[e], d = dl[e];
             float ew = 0.0f;
@@ -898,23 +944,27 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
             gw2 += gb * bf16r(fmaxf(z3, 0.0f));
             const float dz = z3 > 0.0f ? bf16r(gb * w2) : 0.0f;
             gc += dz;
-            const float dzz = bf16r(dz);
-            grad_z[((int64_t)g * E + e) * Hd + k] = f2bf(dzz);
-            gps[s * Hd + k] += dzz;
-            gpd[d * Hd + k] += dzz;
+            const uint16_t dzz = f2bf(bf16r(dz));
+            grad_z[((int64_t)g * E + e) * Hd + k] = dzz;
+            dzs[e * Hd + k] = dzz;
         }
         grad_c[(int64_t)g * Hd + k] = gc;
         grad_w2_part[(int64_t)g * Hd + k] = gw2;
-        for (int i = 0; i < n; ++i) {
-            grad_p[(node0 + i) * 2 * Hd + k] = f2bf(gps[i * Hd + k]);
-            grad_p[(node0 + i) * 2 * Hd + Hd + k] = f2bf(gpd[i * Hd + k]);
-        }
     }
+    __syncthreads();
+    if (on)  // (2) per node: out-links feed p[:, :H], in-links p[:, H:]
+        for (int i = 0; i < n; ++i) {
+            float so = 0.0f, si = 0.0f;
+            for (int q = op[i]; q < op[i + 1]; ++q) so += bf2f(dzs[lo[q] * Hd + k]);
+            for (int q = ip[i]; q < ip[i + 1]; ++q) si += bf2f(dzs[li[q] * Hd + k]);
+            grad_p[(node0 + i) * 2 * Hd + k] = f2bf(so);
+            grad_p[(node0 + i) * 2 * Hd + Hd + k] = f2bf(si);
+        }
 }
 
 size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
-    return (size_t)a.nodes_per_graph * 2 * a.hidden * 2 + (size_t)a.nodes_per_graph * 2 * a.hidden * 4 +
-           (size_t)a.edges_per_graph * (kEdgeED * 4 + 4 + 8);
+    const size_t n = a.nodes_per_graph, E = a.edges_per_graph, H = a.hidden;
+    return n * 2 * H * 2 + (E * H + ((E * H) & 1)) * 2 + E * (kEdgeED * 4 + 4 + 16) + 2 * (n + 1) * 4;
 }
 
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,

@@ -527,7 +527,7 @@ hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t st
 }
 
 // --------------------------------------------------------- prologue backward
-// One wave per graph.  Forward (gat_infer.hip gat_prologue_kernel): ea = LN(edge_x),
+// One 4-wave workgroup per graph.  Forward (gat_infer.hip gat_prologue_kernel): ea = LN(edge_x),
 // x0 = LN(node_x), loop[i] = mean of ea over i's kept in-links, a_edge[p, k] =
 // bf16(bf16(full[p]) . Ml[k]) with Ml = bf16(M).  Per-graph partials (floats,
 // width 8A + 32): [0, 8A) dL/dMl (rows of 8), then edge LN weight / bias,
@@ -556,10 +556,12 @@ __device__ __forceinline__ void ln_fwd_row(float (&x)[kPD], int d, const float* 
     }
 }
 
-__global__ void __launch_bounds__(kW) gat_prologue_bwd_kernel(trx_gat_prologue_bwd_args a) {
+constexpr int kPBT = 256;  // prologue backward: threads per graph
+
+__global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(trx_gat_prologue_bwd_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int MD = kPD;
-    const int g = blockIdx.x, lane = threadIdx.x;
+    constexpr int MD = kPD, NW = kPBT / kW;
+    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & (kW - 1), wave = tid / kW;
     const int n = a.nodes_per_graph, E = a.edges_per_graph, ND = a.node_dim, D = a.edge_dim, A = a.A;
     float* ean = reinterpret_cast<float*>(smem);  // [E][8] normalised link features
     float* exh = ean + E * MD;                    // [E][8] their xhat
@@ -572,11 +574,11 @@ __global__ void __launch_bounds__(kW) gat_prologue_bwd_kernel(trx_gat_prologue_b
     const int64_t node0 = (int64_t)g * n, link0 = (int64_t)g * E;
     const int p0 = a.rowptr[node0], p1 = a.rowptr[node0 + n];
     float* part = a.part + (size_t)g * (8 * A + 32);
-    for (int v = lane; v < A * MD; v += kW) {
+    for (int v = tid; v < A * MD; v += kPBT) {
         const int k = v / MD, j = v - (v / MD) * MD;
         Ml[v] = j < D ? rbf(a.m_work[k * D + j]) : 0.0f;
     }
-    for (int l = lane; l < E; l += kW) {
+    for (int l = tid; l < E; l += kPBT) {
         float x[MD], xh[MD];
 #pragma unroll
         for (int j = 0; j < MD; ++j) x[j] = j < D ? a.edge_x[(link0 + l) * D + j] : 0.0f;
@@ -591,31 +593,32 @@ __global__ void __launch_bounds__(kW) gat_prologue_bwd_kernel(trx_gat_prologue_b
         ld[l] = (s == d || d < 0 || d >= n) ? -1 : (int)d;
     }
     __syncthreads();
-    {  // loop attrs, the forward's order (links ascending)
+    // loop attrs, the forward's order: a node's CSR row lists its kept in-links in link order
+    for (int i = tid; i < n; i += kPBT) {
         float s[MD];
 #pragma unroll
         for (int j = 0; j < MD; ++j) s[j] = 0.0f;
         int cnt = 0;
-        for (int l = 0; l < E; ++l)
-            if (ld[l] == lane) {
-                ++cnt;
+        for (int p = a.rowptr[node0 + i]; p < a.rowptr[node0 + i + 1]; ++p) {
+            const int code = a.pos_src[p];
+            const int64_t li = (int64_t)code - link0;
+            if (code < 0 || li < 0 || li >= E) continue;
+            ++cnt;
 #pragma unroll
-                for (int j = 0; j < MD; ++j) s[j] += ean[l * MD + j];
-            }
-        if (lane < n) {
-            const float deg = cnt > 0 ? (float)cnt : 1.0f;
-            dg[lane] = deg;
+            for (int j = 0; j < MD; ++j) s[j] += ean[li * MD + j];
+        }
+        const float deg = cnt > 0 ? (float)cnt : 1.0f;
+        dg[i] = deg;
 #pragma unroll
-            for (int j = 0; j < MD; ++j) {
-                lp[lane * MD + j] = j < D ? s[j] / deg : 0.0f;
-                glp[lane * MD + j] = 0.0f;
-            }
+        for (int j = 0; j < MD; ++j) {
+            lp[i * MD + j] = j < D ? s[j] / deg : 0.0f;
+            glp[i * MD + j] = 0.0f;
         }
     }
     __syncthreads();
     // positions: dL/dfull into the link / loop rows (each position is its link's or
-    // node's only one), then dL/dMl row by row (lane partials + wave sums)
-    for (int p = p0 + lane; p < p1; p += kW) {
+    // node's only one)
+    for (int p = p0 + tid; p < p1; p += kPBT) {
         const int code = a.pos_src[p];
         const int64_t li = (int64_t)code - link0, ni = -(int64_t)code - 1 - node0;
         float gf[MD];
@@ -630,7 +633,8 @@ __global__ void __launch_bounds__(kW) gat_prologue_bwd_kernel(trx_gat_prologue_b
 #pragma unroll
         for (int j = 0; j < MD; ++j) dstg[j] += gf[j];
     }
-    for (int k = 0; k < A; ++k) {
+    // dL/dMl row by row, rows dealt to the waves (lane partials over positions + wave sums)
+    for (int k = wave; k < A; k += NW) {
         float gm[MD];
 #pragma unroll
         for (int j = 0; j < MD; ++j) gm[j] = 0.0f;
@@ -648,50 +652,49 @@ __global__ void __launch_bounds__(kW) gat_prologue_bwd_kernel(trx_gat_prologue_b
         }
     }
     __syncthreads();
-    // loop-mean backward into the kept links, then edge LayerNorm weight / bias
     float pw[MD], pb[MD];
 #pragma unroll
     for (int j = 0; j < MD; ++j) pw[j] = pb[j] = 0.0f;
-    for (int l = lane; l < E; l += kW) {
-        const int d = ld[l];
+    if (wave == 0) {  // loop-mean backward into the kept links, then edge LayerNorm weight / bias
+        for (int l = lane; l < E; l += kW) {
+            const int d = ld[l];
 #pragma unroll
-        for (int j = 0; j < MD; ++j) {
-            float gj = gea[l * MD + j];
-            if (d >= 0) gj += glp[d * MD + j] / dg[d];
-            pw[j] += gj * exh[l * MD + j];
-            pb[j] += gj;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < MD; ++j) {
-        const float w = wsum(pw[j]), b = wsum(pb[j]);
-        if (lane == 0) {
-            part[8 * A + j] = w;
-            part[8 * A + 8 + j] = b;
-        }
-    }
-    // node LayerNorm weight / bias from dL/dx0
-#pragma unroll
-    for (int j = 0; j < MD; ++j) pw[j] = pb[j] = 0.0f;
-    for (int i = lane; i < n; i += kW) {
-        float x[MD], xh[MD];
-#pragma unroll
-        for (int j = 0; j < MD; ++j) x[j] = j < ND ? a.node_x[(node0 + i) * ND + j] : 0.0f;
-        ln_fwd_row(x, ND, a.node_ln_w, a.node_ln_b, a.node_ln_eps, xh);
-#pragma unroll
-        for (int j = 0; j < MD; ++j)
-            if (j < ND) {
-                const float gj = a.g_x0[(node0 + i) * ND + j];
-                pw[j] += gj * xh[j];
+            for (int j = 0; j < MD; ++j) {
+                float gj = gea[l * MD + j];
+                if (d >= 0) gj += glp[d * MD + j] / dg[d];
+                pw[j] += gj * exh[l * MD + j];
                 pb[j] += gj;
             }
-    }
+        }
 #pragma unroll
-    for (int j = 0; j < MD; ++j) {
-        const float w = wsum(pw[j]), b = wsum(pb[j]);
-        if (lane == 0) {
-            part[8 * A + 16 + j] = w;
-            part[8 * A + 24 + j] = b;
+        for (int j = 0; j < MD; ++j) {
+            const float w = wsum(pw[j]), b = wsum(pb[j]);
+            if (lane == 0) {
+                part[8 * A + j] = w;
+                part[8 * A + 8 + j] = b;
+            }
+        }
+    } else if (wave == 1) {  // node LayerNorm weight / bias from dL/dx0
+        for (int i = lane; i < n; i += kW) {
+            float x[MD], xh[MD];
+#pragma unroll
+            for (int j = 0; j < MD; ++j) x[j] = j < ND ? a.node_x[(node0 + i) * ND + j] : 0.0f;
+            ln_fwd_row(x, ND, a.node_ln_w, a.node_ln_b, a.node_ln_eps, xh);
+#pragma unroll
+            for (int j = 0; j < MD; ++j)
+                if (j < ND) {
+                    const float gj = a.g_x0[(node0 + i) * ND + j];
+                    pw[j] += gj * xh[j];
+                    pb[j] += gj;
+                }
+        }
+#pragma unroll
+        for (int j = 0; j < MD; ++j) {
+            const float w = wsum(pw[j]), b = wsum(pb[j]);
+            if (lane == 0) {
+                part[8 * A + 16 + j] = w;
+                part[8 * A + 24 + j] = b;
+            }
         }
     }
 }
@@ -702,7 +705,7 @@ size_t gat_prologue_bwd_smem(const trx_gat_prologue_bwd_args& a) {
 }
 
 hipError_t launch_gat_prologue_bwd(const trx_gat_prologue_bwd_args& a, hipStream_t stream) {
-    hipLaunchKernelGGL(gat_prologue_bwd_kernel, dim3(a.num_graphs), dim3(kW), gat_prologue_bwd_smem(a), stream, a);
+    hipLaunchKernelGGL(gat_prologue_bwd_kernel, dim3(a.num_graphs), dim3(kPBT), gat_prologue_bwd_smem(a), stream, a);
     return hipGetLastError();
 }
 

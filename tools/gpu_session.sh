@@ -70,6 +70,8 @@ for s in "$@"; do
              grep -h "step kernel" gpurun_out/ab_*.log ;;
         vtest) cp sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_${VARIANT}.so $LIB && sha256sum $LIB | cut -c1-16 > gpurun_out/lib_sha16.txt
                step vtest_$VARIANT 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sparse.py tests/test_gpu_fallback.py tests/test_torch_sp.py tests/test_gpu_large.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        abbig) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); case $n in *stats*|*stamps*) continue;; esac; step abbig_$n 200 python tools/ab_big.py $f 1024 || exit 1; done
+               grep -h "step kernel" gpurun_out/abbig_*.log ;;
         abx) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl*.so; do n=$(basename $f .so); step ab_$n 200 python tools/ab_env.py $f 4096 30 || exit 1; done ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -22,15 +22,17 @@ tr = Trainer(cfg, device="cuda:0", log=False)
 tr._reset_envs(None)
 obs = tr.env.observe()
 tr.act(obs)
-buf = (ctypes.c_ulonglong * 24)()
+buf = (ctypes.c_ulonglong * 32)()
 L.trx_debug_infer_cycles(buf, 1)
 reps = 10
 for _ in range(reps):
     tr.act(obs)
 L.trx_debug_infer_cycles(buf, 0)
 names = ["stage", "layer0 xh", "att dots", "edge logits", "softmax", "aggregate+LN", "pool sync", "pool"]
-for row, title in enumerate(["layer 0 (HC 1024, IN 4)", "HC 1024", "HC 256 (last)"]):
+for row, title in enumerate(["layer 0 (HC 1024, IN 4)", "HC 1024", "HC 256 (last)", "edge scorer"]):
     vals = [buf[row * 8 + i] for i in range(8)]
+    if row == 3:
+        names = ["stage", "links", "softmax", "draw", "", "", "", ""]
     tot = sum(vals) or 1
     print(f"== {title}: {tot / reps / B:.0f} cycles per workgroup")
     for n, v in zip(names, vals):
