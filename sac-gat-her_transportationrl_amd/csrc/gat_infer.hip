@@ -130,8 +130,12 @@ extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
 
 // ------------------------------------------------------------- layer kernel
 // IN: 0 = xh given (layers >= 1), else the layer-0 input width (4).
+#ifndef TRX_L0_WAVES
+#define TRX_L0_WAVES 1  // A/B knob: waves-per-SIMD register budget of the layer-0 instances
+#endif
 template <int HC, int IN, int NT>
-__global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args a) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(IN > 0 ? TRX_L0_WAVES : 1)))
+gat_layer_infer_kernel(trx_gat_layer_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int kInferThreads = NT, kInferWaves = NT / kWave;  // this instance's workgroup
     constexpr int KC = HC / 256;  // float4 chunks per lane in a row
@@ -176,7 +180,8 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
     float* al = ad_ + n * H;        // [me*H] edge logits, then attention weights (in place)
     int* cl = reinterpret_cast<int*>(al + a.max_graph_edges * H);  // [me] source, graph-local
     int* rp = cl + a.max_graph_edges;                    // [n+1] graph-local row pointers
-    float* x0l = reinterpret_cast<float*>(rp + n + 1);   // [n*IN]
+    int* dlc = rp + n + 1;                               // [me] graph-local destination per CSR position
+    float* x0l = reinterpret_cast<float*>(dlc + a.max_graph_edges);  // [n*IN]
     float* yt = x0l + n * IN;                            // [n][HC] (pool only)
 
     // 0b. graph-local CSR slice, this layer's edge logits, layer-0 inputs: every
@@ -213,6 +218,8 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
         for (int v = tid + kInferThreads * kStageBatch; v < nq; v += kInferThreads) dst4[v] = xsrc[v];
     }
     __syncthreads();
+    for (int i = tid; i < n; i += kInferThreads)
+        for (int p = rp[i]; p < rp[i + 1]; ++p) dlc[p] = i;
     TRX_ISTAMP(0);
 
     // 1. layer 0: xh = bf16(bf16(x0) @ w0^T); a thread owns 4 consecutive columns
@@ -330,19 +337,34 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
     TRX_ISTAMP(2);
     TRX_ISTAMP(3);
 
-    // 3. softmax over in-edges: one thread per (node, head), LDS only
+    // 3. softmax over in-edges, LDS only: (a) every (edge, head) logit
+    //    leaky(a_src + a_dst + a_edge) in place, one thread each; (b) per (node,
+    //    head) the max, the exp terms (kept in place) and their sum in edge
+    //    order, the denominator into ad_ (a_dst is consumed); (c) every
+    //    (edge, head) weight = exp / denominator.  Same values as one thread
+    //    per (node, head) doing all three passes.
+    for (int v = tid; v < ne * H; v += kInferThreads) {
+        const int p = v / H, h = v - (v / H) * H;
+        al[v] = leaky_f(as_[cl[p] * H + h] + ad_[dlc[p] * H + h] + al[v], a.negative_slope);
+    }
+    __syncthreads();
     for (int t = tid; t < n * H; t += kInferThreads) {
         const int i = t / H, h = t - (t / H) * H;
         const int p0 = rp[i], p1 = rp[i + 1];
-        const float ad = ad_[t];
         float m = -__builtin_huge_valf();
-        for (int p = p0; p < p1; ++p) m = fmaxf(m, leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope));
+        for (int p = p0; p < p1; ++p) m = fmaxf(m, al[p * H + h]);
         float ssum = 0.0f;
-        for (int p = p0; p < p1; ++p)
-            ssum += __expf(leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope) - m);
-        const float denom = ssum + 1e-16f;
-        for (int p = p0; p < p1; ++p)  // in place: logit -> attention weight
-            al[p * H + h] = __expf(leaky_f(as_[cl[p] * H + h] + ad + al[p * H + h], a.negative_slope) - m) / denom;
+        for (int p = p0; p < p1; ++p) {
+            const float ex = __expf(al[p * H + h] - m);
+            al[p * H + h] = ex;
+            ssum += ex;
+        }
+        ad_[t] = ssum + 1e-16f;
+    }
+    __syncthreads();
+    for (int v = tid; v < ne * H; v += kInferThreads) {
+        const int p = v / H, h = v - (v / H) * H;
+        al[v] = al[v] / ad_[dlc[p] * H + h];
     }
     __syncthreads();
     if (a.save_alpha)
@@ -372,7 +394,8 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
         float4 res4[KC];  // issue the residual loads before the aggregation (latency overlap)
 #pragma unroll
         for (int k = 0; k < KC; ++k)
-            res4[k] = a.residual == 1 ? *reinterpret_cast<const float4*>(a.res + (size_t)node * HC + 4 * (lane + kWave * k))
+            res4[k] = IN == 0 && a.residual == 1  // layer 0's residual is its input projection
+                          ? *reinterpret_cast<const float4*>(a.res + (size_t)node * HC + 4 * (lane + kWave * k))
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 acc[KC];
 #pragma unroll
@@ -437,7 +460,7 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
 #pragma unroll
                     for (int j = 0; j < (IN > 0 ? IN : 1); ++j) t += xr[j] * wp_r[k][r][j];
                     y = y + bf16r(t + bp_r[k][r]);
-                } else if (a.residual == 1) {
+                } else if (IN == 0 && a.residual == 1) {
                     y = y + resv[r];
                 }
                 if (a.activation == 0)
@@ -509,7 +532,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
     trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
     const int nq = n * 2 * Hd / 8;
 #ifndef TRX_EH_ROWS
-#define TRX_EH_ROWS 4
+#define TRX_EH_ROWS 6
 #endif
     constexpr int kRowRegs = TRX_EH_ROWS;
     trx_u4 rows[kRowRegs];
@@ -628,22 +651,32 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         for (int e = lane; e < E; e += kWave) a.logits[(int64_t)g * E + e] = lg[e];
     float m = -__builtin_huge_valf();
     for (int e0 = 0; e0 < E; e0 += kWave) m = fmaxf(m, wave_max_f(e0 + lane < E ? lg[e0 + lane] : -__builtin_huge_valf()));
-    float ssum = 0.0f;
-    for (int e0 = 0; e0 < E; e0 += kWave) ssum += wave_sum_f(e0 + lane < E ? expf(lg[e0 + lane] - m) : 0.0f);
+    float ssum = 0.0f;  // each exp term computed once, kept in mk[] (the mask is no longer needed)
+    for (int e0 = 0; e0 < E; e0 += kWave) {
+        const int e = e0 + lane;
+        const float ex = e < E ? expf(lg[e] - m) : 0.0f;
+        if (e < E) mk[e] = ex;
+        ssum += wave_sum_f(ex);
+    }
     const float denom = ssum + 1e-16f;
-    for (int e = lane; e < E; e += kWave) a.out[(int64_t)g * E + e] = expf(lg[e] - m) / denom;
+    for (int e = lane; e < E; e += kWave) a.out[(int64_t)g * E + e] = mk[e] / denom;
     TRX_ESTAMP(2);
-    if (a.u && lane == 0) {  // one categorical draw per graph (inverse CDF over the same exp terms)
-        const float target = a.u[g] * ssum;
-        float acc = 0.0f;
-        int pick = -1, last = 0;
-        for (int e = 0; e < E; ++e) {
-            const float ex = expf(lg[e] - m);
-            if (ex > 0.0f) last = e;
-            acc += ex;
-            if (pick < 0 && acc > target) pick = e;
+    if (a.u) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // mk[] written by every lane, read by lane 0
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) {  // one categorical draw per graph (inverse CDF over the same exp terms)
+            const float target = a.u[g] * ssum;
+            float acc = 0.0f;
+            int pick = -1, last = 0;
+            for (int e = 0; e < E; ++e) {
+                const float ex = mk[e];
+                if (ex > 0.0f) last = e;
+                acc += ex;
+                if (pick < 0 && acc > target) pick = e;
+            }
+            a.action[g] = pick >= 0 ? pick : last;  // u * total above the serial sum: last link with mass
         }
-        a.action[g] = pick >= 0 ? pick : last;  // u * total above the serial sum: last link with mass
     }
     TRX_ESTAMP(3);
 }
@@ -793,7 +826,7 @@ size_t edge_head_infer_smem(const trx_edge_head_args& a) {
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a) {
     const int HC = a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
     const size_t alsz = (size_t)me * H;
-    size_t b = (size_t)n * HC * 2 + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 + (size_t)(n + 1) * 4 +
+    size_t b = (size_t)n * HC * 2 + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 * 2 + (size_t)(n + 1) * 4 +
                (size_t)n * a.in_dim * 4;
     if (a.pool) b += (size_t)n * HC * 4;
     return b;
@@ -856,25 +889,30 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 // the gradient reaching the bf16 sum of the gathers and the link term is
 // rounded to bf16 (grad_z), p gradients are fp32 sums over the graph's links
 // (fixed link order) rounded to bf16 at the end.  Two passes, no LDS
-// read-modify-write chains: (1) per link, thread k's gradient through unit k
-// (stored bf16 in LDS: it is bf16-rounded anyway) with grad_c / grad_w2 sums;
-// (2) per node, the sums over its out-links (p[:, :H]) and in-links
-// (p[:, H:]) in link order from per-node link lists.
+// read-modify-write chains, and four threads per hidden unit (1024 per graph:
+// the update's 256 graphs are one workgroup per CU): (1) per link (links
+// dealt to the four parts), thread k's gradient through unit k, stored bf16
+// in LDS (it is bf16-rounded anyway), with per-part grad_c / grad_w2 sums
+// added in part order; (2) per node (nodes dealt to the parts), the sums over
+// its out-links (p[:, :H]) and in-links (p[:, H:]) in link order.
 // Outputs: grad_p [N, 2H] bf16, grad_c [B, H], grad_z [E_total, H] bf16 (for
 // the link-feature weight / input gradients, GEMMs on the host side) and
 // grad_w2_part [B, H] (per-graph sums of bf16(g) * bf16(relu(z))).
-__global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
-                                                                      uint16_t* grad_p, float* grad_c,
-                                                                      uint16_t* grad_z, float* grad_w2_part) {
+constexpr int kEhbThreads = 1024, kEhbParts = kEhbThreads / 256;
+
+__global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
+                                                                    uint16_t* grad_p, float* grad_c,
+                                                                    uint16_t* grad_z, float* grad_w2_part) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int ED = kEdgeED;
-    const int g = blockIdx.x, k = threadIdx.x;
+    constexpr int ED = kEdgeED, NT = kEhbThreads, P = kEhbParts;
+    const int g = blockIdx.x, tid = threadIdx.x, k = tid & 255, part = tid >> 8;
     const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
     uint16_t* pr = reinterpret_cast<uint16_t*>(smem);                   // [n][2*Hd] bf16
     uint16_t* dzs = pr + (size_t)n * 2 * Hd;                            // [E][Hd] bf16 dL/dz
     float* eal = reinterpret_cast<float*>(dzs + (size_t)E * Hd + ((E * Hd) & 1));  // [E][ED] link features
     float* gl = eal + (size_t)E * ED;                                   // [E] bf16(grad logit)
-    int* sl = reinterpret_cast<int*>(gl + E);                           // [E]
+    float* red = gl + E;                                                // [P][2][256] per-part sums
+    int* sl = reinterpret_cast<int*>(red + P * 2 * 256);                // [E]
     int* dl = sl + E;                                                   // [E]
     int* lo = dl + E;                                                   // [E] links by source node, link order
     int* li = lo + E;                                                   // [E] links by destination node
@@ -884,9 +922,9 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
     {
         const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.p) + node0 * 2 * Hd);
         trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
-        for (int v = k; v < n * 2 * Hd / 8; v += kInferThreads) dst4[v] = src4[v];
+        for (int v = tid; v < n * 2 * Hd / 8; v += NT) dst4[v] = src4[v];
     }
-    for (int e = k; e < E; e += kInferThreads) {
+    for (int e = tid; e < E; e += NT) {
         const int64_t eg = (int64_t)g * E + e;
         int s = (int)(a.src[eg] - node0), d = (int)(a.dst[eg] - node0);
         s = s < 0 ? 0 : (s >= n ? n - 1 : s);  // out-of-block links are refused on the host (topology check)
@@ -895,7 +933,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
         dl[e] = d;
         gl[e] = bf16r(grad_logits[eg]);
     }
-    for (int v = k; v < E * ED; v += kInferThreads) {
+    for (int v = tid; v < E * ED; v += NT) {
         const int e = v / ED, j = v - (v / ED) * ED;
         eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
     }
@@ -905,33 +943,33 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
     for (int j = 0; j < ED; ++j) we[j] = (on && j < D) ? a.we[k * D + j] : 0.0f;
     const float w2 = on ? a.w2[k] : 0.0f, ck = on ? a.c[(int64_t)g * Hd + k] : 0.0f;
     __syncthreads();
-    if (k < n) {  // per-node link lists (link order); counts first
+    if (tid < n) {  // per-node link lists (link order); counts first
         int co = 0, ci = 0;
         for (int e = 0; e < E; ++e) {
-            co += sl[e] == k;
-            ci += dl[e] == k;
+            co += sl[e] == tid;
+            ci += dl[e] == tid;
         }
-        op[k + 1] = co;
-        ip[k + 1] = ci;
+        op[tid + 1] = co;
+        ip[tid + 1] = ci;
     }
-    if (k == 0) op[0] = ip[0] = 0;
+    if (tid == 0) op[0] = ip[0] = 0;
     __syncthreads();
-    if (k == 0)
+    if (tid == 0)
         for (int i = 0; i < n; ++i) {
             op[i + 1] += op[i];
             ip[i + 1] += ip[i];
         }
     __syncthreads();
-    if (k < n) {
-        int wo = op[k], wi = ip[k];
+    if (tid < n) {
+        int wo = op[tid], wi = ip[tid];
         for (int e = 0; e < E; ++e) {
-            if (sl[e] == k) lo[wo++] = e;
-            if (dl[e] == k) li[wi++] = e;
+            if (sl[e] == tid) lo[wo++] = e;
+            if (dl[e] == tid) li[wi++] = e;
         }
     }
     float gc = 0.0f, gw2 = 0.0f;
     if (on) {  // (1) per link
-        for (int e = 0; e < E; ++e) {
+        for (int e = part; e < E; e += P) {
             const int s = sl[e], d = dl[e];
             float ew = 0.0f;
 #pragma unroll
@@ -948,12 +986,22 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
             grad_z[((int64_t)g * E + e) * Hd + k] = dzz;
             dzs[e * Hd + k] = dzz;
         }
-        grad_c[(int64_t)g * Hd + k] = gc;
-        grad_w2_part[(int64_t)g * Hd + k] = gw2;
     }
+    red[(part * 2 + 0) * 256 + k] = gc;
+    red[(part * 2 + 1) * 256 + k] = gw2;
     __syncthreads();
+    if (on && part == 0) {
+        float tc = red[k], tw = red[256 + k];
+#pragma unroll
+        for (int q = 1; q < P; ++q) {
+            tc += red[(q * 2) * 256 + k];
+            tw += red[(q * 2 + 1) * 256 + k];
+        }
+        grad_c[(int64_t)g * Hd + k] = tc;
+        grad_w2_part[(int64_t)g * Hd + k] = tw;
+    }
     if (on)  // (2) per node: out-links feed p[:, :H], in-links p[:, H:]
-        for (int i = 0; i < n; ++i) {
+        for (int i = part; i < n; i += P) {
             float so = 0.0f, si = 0.0f;
             for (int q = op[i]; q < op[i + 1]; ++q) so += bf2f(dzs[lo[q] * Hd + k]);
             for (int q = ip[i]; q < ip[i + 1]; ++q) si += bf2f(dzs[li[q] * Hd + k]);
@@ -964,7 +1012,8 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_bwd_kernel(trx_edge_h
 
 size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
     const size_t n = a.nodes_per_graph, E = a.edges_per_graph, H = a.hidden;
-    return n * 2 * H * 2 + (E * H + ((E * H) & 1)) * 2 + E * (kEdgeED * 4 + 4 + 16) + 2 * (n + 1) * 4;
+    return n * 2 * H * 2 + (E * H + ((E * H) & 1)) * 2 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * 2 * 256 * 4 +
+           2 * (n + 1) * 4;
 }
 
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
@@ -975,7 +1024,7 @@ hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_l
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(edge_head_bwd_kernel, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a, grad_logits,
+    hipLaunchKernelGGL(edge_head_bwd_kernel, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
                        static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
     return hipGetLastError();
 }

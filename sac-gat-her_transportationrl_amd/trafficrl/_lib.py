@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtrafficrl.so")
+# TRX_LIB: an A/B build of the same library (tools/, never a fallback)
+LIB_PATH = os.environ.get("TRX_LIB") or os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}

@@ -24,6 +24,7 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional
 
 import torch
+import torch.nn.functional as F
 
 from .. import _lib
 from ..models import fused
@@ -109,7 +110,7 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
             args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
             rec.update(w0=w0, wp=wp)
         else:
-            xh = torch.mm(prev_bf16, wts[i].t())
+            xh = F.linear(prev_bf16, wts[i])
             args.in_dim, args.xh = 0, xh.data_ptr()
             rec.update(xh=xh, x_in=prev_bf16, w=wts[i])
             if last:
@@ -146,7 +147,7 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     head_w = fused._head_weights(net) if save else fused.prepared_head(net)
     wn, wc, we, w2, b2 = head_w
     b1 = net.edge_mlp[0].bias.detach()
-    p = torch.mm(emb, wn.t())                                   # bf16 [N, 2H] per-node projections
+    p = F.linear(emb, wn)                                       # bf16 [N, 2H] per-node projections
     c = torch.mm(ctx.to(torch.bfloat16), wc) + b1               # autocast's bf16 product + fp32 bias
     logits = torch.empty(topo.B * topo.e, device=dev, dtype=torch.float32)
     a = fused._edge_args(p, c, ea, we, w2, b2, topo.src32, topo.dst32, topo.B, topo.n, topo.e)

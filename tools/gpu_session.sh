@@ -61,6 +61,9 @@ for s in "$@"; do
         abk) step ab_quad 200 env TRX_KERNEL=quad python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
         fused) step fused_tests 600 python -u -m pytest tests/test_flat_adam.py tests/test_fused_update.py tests/test_sac_e2e.py tests/test_sac.py -m gpu -v -s --timeout 300 --timeout-method thread ;;
         bigstats) step big_stats 300 python tools/big_stats.py 1024 fw ;;
+        actab) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_l03.so; do [ -f $f ] || continue; n=$(basename $f .so); TRX_LIB=$PWD/$f step actab_$n 200 python tools/act_host_probe.py 4096 || exit 1; done
+               grep -h "eager" gpurun_out/actab_*.log ;;
+        gemmlay) step gemm_layouts 200 python tools/act_gemm_layouts.py ;;
         actprobe) step act_probe 300 python tools/act_host_probe.py 4096 ;;
         graphtests) step graph_tests 400 python -u -m pytest tests/test_replay_train.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         fallback) step fallback_tests 400 python -u -m pytest tests/test_gpu_fallback.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
