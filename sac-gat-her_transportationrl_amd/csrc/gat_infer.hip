@@ -389,14 +389,27 @@ gat_layer_infer_kernel(trx_gat_layer_args a) {
                 bp_r[k][r] = a.bp[f];
             }
         }
+    // the residual rows (middle layers) are loaded one node ahead: node i's arrive
+    // while the wave aggregates node i - kInferWaves (layer 0's residual is its
+    // input projection, computed in registers)
+    const bool res_in = IN == 0 && a.residual == 1;
+    float4 res_next[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+        res_next[k] = res_in && wave < n
+                          ? *reinterpret_cast<const float4*>(a.res + (size_t)(node0 + wave) * HC + 4 * (lane + kWave * k))
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int i = wave; i < n; i += kInferWaves) {
         const int node = node0 + i;
-        float4 res4[KC];  // issue the residual loads before the aggregation (latency overlap)
+        float4 res4[KC];
 #pragma unroll
-        for (int k = 0; k < KC; ++k)
-            res4[k] = IN == 0 && a.residual == 1  // layer 0's residual is its input projection
-                          ? *reinterpret_cast<const float4*>(a.res + (size_t)node * HC + 4 * (lane + kWave * k))
-                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = 0; k < KC; ++k) {
+            res4[k] = res_next[k];
+            res_next[k] = res_in && i + kInferWaves < n
+                              ? *reinterpret_cast<const float4*>(a.res + (size_t)(node + kInferWaves) * HC +
+                                                                 4 * (lane + kWave * k))
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         float4 acc[KC];
 #pragma unroll
         for (int k = 0; k < KC; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);

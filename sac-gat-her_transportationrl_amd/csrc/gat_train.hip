@@ -244,7 +244,9 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
     }
     __syncthreads();
 
-    // ---- B: thread per 4 columns -- bias / LayerNorm (/ input_proj) partials
+    // ---- B: thread per 4 columns -- bias / LayerNorm (/ input_proj) partials.
+    //      Nodes four at a time: their global rows are loaded before the first
+    //      is used (one memory round trip per four nodes, same summation order).
     const int PW = IN > 0 ? 14 * HC : 5 * HC;
     float* part = a.part + (size_t)g * PW;
     for (int q = tid; q < HC / 4; q += kT) {
@@ -254,11 +256,8 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int j = 0; j < INR; ++j) pwp[r][j] = 0.0f;
-        for (int i = 0; i < n; ++i) {
-            const size_t row = (size_t)(node0 + i) * HC;
+        auto node_terms = [&](int i, const float4 t4, const float4 v4) {
             const float4 g4 = *reinterpret_cast<const float4*>(gv + i * HC + 4 * q);
-            const float4 t4 = *reinterpret_cast<const float4*>(a.g_res + row + 4 * q);
-            const float4 v4 = *reinterpret_cast<const float4*>(a.v + row + 4 * q);
             const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w},
                         vv[4] = {v4.x, v4.y, v4.z, v4.w};
             const float mean = st[2 * i], rstd = st[2 * i + 1];
@@ -273,6 +272,23 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
                     for (int j = 0; j < INR; ++j) pwp[r][j] += tt[r] * x0l[i * IN + j];
                 }
             }
+        };
+        int i = 0;
+        for (; i + 4 <= n; i += 4) {
+            float4 t4[4], v4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const size_t row = (size_t)(node0 + i + u) * HC;
+                t4[u] = *reinterpret_cast<const float4*>(a.g_res + row + 4 * q);
+                v4[u] = *reinterpret_cast<const float4*>(a.v + row + 4 * q);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) node_terms(i + u, t4[u], v4[u]);
+        }
+        for (; i < n; ++i) {
+            const size_t row = (size_t)(node0 + i) * HC;
+            node_terms(i, *reinterpret_cast<const float4*>(a.g_res + row + 4 * q),
+                       *reinterpret_cast<const float4*>(a.v + row + 4 * q));
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -399,6 +415,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
     __syncthreads();
 
     // ---- E: thread per 4 columns -- att_src / att_dst (/ layer-0 lin.weight) partials
+    //      (layer 0: the g_xh rows four nodes at a time, as in B)
     for (int q = tid; q < HC / 4; q += kT) {
         const int h = (4 * q) / C;
         float ps[4] = {0, 0, 0, 0}, pd[4] = {0, 0, 0, 0};
@@ -407,7 +424,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int j = 0; j < INR; ++j) pw0[r][j] = 0.0f;
-        for (int j = 0; j < n; ++j) {
+        auto node_terms = [&](int j, const uint2 w) {
             const uint2 u = *reinterpret_cast<const uint2*>(xs + j * HC + 4 * q);
             const float xv[4] = {lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y)};
             const float gs = gas[j * H + h], gd = gad[j * H + h];
@@ -417,15 +434,27 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
                 pd[r] += gd * xv[r];
             }
             if (IN > 0) {
-                const uint2 w = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(a.g_xh) +
-                                                                (size_t)(node0 + j) * HC + 4 * q);
                 const float gb[4] = {lo_bf(w.x), hi_bf(w.x), lo_bf(w.y), hi_bf(w.y)};
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
                     for (int jj = 0; jj < INR; ++jj) pw0[r][jj] += gb[r] * x0l[j * IN + jj];
             }
+        };
+        auto gxh = [&](int j) {
+            return IN > 0 ? *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(a.g_xh) +
+                                                           (size_t)(node0 + j) * HC + 4 * q)
+                          : make_uint2(0u, 0u);
+        };
+        int j = 0;
+        for (; j + 4 <= n; j += 4) {
+            uint2 w[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w[u] = gxh(j + u);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) node_terms(j + u, w[u]);
         }
+        for (; j < n; ++j) node_terms(j, gxh(j));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int c = 4 * q + r;
@@ -433,7 +462,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             part[4 * HC + c] = pd[r];
             if (IN > 0) {
 #pragma unroll
-                for (int j = 0; j < INR; ++j) part[5 * HC + c * IN + j] = pw0[r][j];
+                for (int jj = 0; jj < INR; ++jj) part[5 * HC + c * IN + jj] = pw0[r][jj];
             }
         }
     }
