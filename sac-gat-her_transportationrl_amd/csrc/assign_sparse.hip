@@ -89,6 +89,12 @@ constexpr int kQs = 4;
 constexpr uint64_t kUnreached = 0x7FF8000000000000ull;
 constexpr uint32_t kScannedHi = 0xFFF80000u;
 constexpr int kMaxDeg = 16;   // out-degree (out-slot rounds of 4: 1, 2, 4)
+#ifndef TRX_DS_PAD
+#define TRX_DS_PAD 0  // A/B knob: float padding of a node's out-slot cost row (2: rows of 10 floats)
+#endif
+#ifndef TRX_KEY_PAD
+#define TRX_KEY_PAD 0  // A/B knob: u64 padding of a tree's key row (2: the 16 rows of a wave start on distinct banks)
+#endif
 
 struct SmemS {
     uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [EPW*E] f32 (dprev: CFW only); aux: u32 AON link
@@ -126,9 +132,9 @@ __host__ __device__ inline SmemS smems_layout(int E, int N, int Z, int NP, int E
     o.t = take(el);
     o.aux = take(el);
     o.dprev = take(cfw ? el : 0u);
-    o.ocost = take((uint32_t)(EPW * NP * DS * 4));
-    o.ov = take((uint32_t)(NP * DS));
-    o.keys = take((uint32_t)(rows * NP * 8));
+    o.ocost = take((uint32_t)(EPW * NP * (DS + TRX_DS_PAD) * 4));
+    o.ov = take((uint32_t)(NP * (DS + TRX_DS_PAD)));
+    o.keys = take((uint32_t)(rows * (NP + TRX_KEY_PAD) * 8));
     o.pred = take((uint32_t)(EPW * Z * NP));
     o.ord = take((uint32_t)(EPW * Z * NP));
     o.eid = take((uint32_t)(NP * NP));
@@ -251,7 +257,8 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     float* const sunas = (float*)(smem_raw + O.unas);
     int* const sact = (int*)(smem_raw + O.act);
     double* const sred = (double*)(smem_raw + O.red);
-    const int NDS = NP * DS;
+    const int DSP = DS + TRX_DS_PAD;  // row stride of the out-slot tables
+    const int NDS = NP * DSP;
 #ifdef TRX_PHASE_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -284,14 +291,14 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     // tests: an empty out-slot of u targets u itself (scanned before its
     // relaxation: never improved) at cost +inf; an empty in-slot of v names v
     // itself as tail over link 0 (label(v) + cost > label(v): never achieving)
-    for (int i = tid; i < NDS; i += L) sov[i] = (uint8_t)(i / DS);
+    for (int i = tid; i < NDS; i += L) sov[i] = (uint8_t)(i / DSP);
     for (int i = tid; i < NP * NP; i += L) seid[i] = (uint8_t)g.eid_of[i];
     for (int i = tid; i < EPW * NDS; i += L) socost[i] = kInfF;
     for (int u = tid; u < N; u += L) {
         const int a0 = g.indptr[u], a1 = g.indptr[u + 1];
         for (int a = a0; a < a1; ++a) {
             // out-link k of u -> lane k % 4, round k / 4: each lane's R slots are contiguous
-            const int pos = u * DS + ((a - a0) & (kQs - 1)) * R + (a - a0) / kQs;
+            const int pos = u * DSP + ((a - a0) & (kQs - 1)) * R + (a - a0) / kQs;
             sov[pos] = (uint8_t)g.indices[a];
             opos_tmp[g.csr_eid[a]] = (int16_t)pos;
         }
@@ -341,7 +348,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     if (!opos_reg) {  // generic path: cost-table entries from the static out-adjacency
         for (int x = tid; x < EPW * NDS; x += L) {
             const int el = x / NDS, r = x - el * NDS;
-            const int u = r / DS, v = sov[r];
+            const int u = r / DSP, v = sov[r];
             socost[x] = v != u ? st[el * E + g.eid_of[u * NP + v]] : kInfF;
         }
     }
@@ -360,7 +367,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     for (int it = 0; it < p.iters; ++it) {
         // ---------------- shortest-path tree per quad (Dijkstra, sparse relaxation)
         if (tree_on) {
-            uint64_t* const kt = skeys + tree * NP;
+            uint64_t* const kt = skeys + tree * (NP + TRX_KEY_PAD);
             uint32_t* const kt32 = reinterpret_cast<uint32_t*>(kt);
             const float* const oc = socost + lenv * NDS;
             uint8_t* const ol = sord + tree * NP;
@@ -403,7 +410,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 uint32_t v[R];
                 float c[R];
                 {  // lane j's R slots of u: one read each for heads and costs
-                    const int sl = (int)u * DS + j * R;
+                    const int sl = (int)u * DSP + j * R;
                     if constexpr (R == 1) {
                         v[0] = sov[sl];
                         c[0] = oc[sl];
@@ -583,7 +590,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
         if (!opos_reg) {
             for (int x = tid; x < EPW * NDS; x += L) {
                 const int el = x / NDS, r = x - el * NDS;
-                const int u = r / DS, v = sov[r];
+                const int u = r / DSP, v = sov[r];
                 if (v != u) socost[x] = st[el * E + g.eid_of[u * NP + v]];
             }
             __syncthreads();
