@@ -174,8 +174,11 @@ gat_layer_infer_kernel(trx_gat_layer_args a) {
         return;
     }
 
-    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // [n][HC] bf16
-    float* as_ = reinterpret_cast<float*>(xs + n * HC);  // [n*H]
+    // xh rows padded by 8 bf16 (16 B): the attention dots read four nodes' rows
+    // per wave instruction, which an unpadded 2 KB stride puts on the same banks
+    constexpr int XS = HC + 8;
+    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // [n][XS] bf16
+    float* as_ = reinterpret_cast<float*>(xs + n * XS);  // [n*H]
     float* ad_ = as_ + n * H;                            // [n*H]
     float* al = ad_ + n * H;        // [me*H] edge logits, then attention weights (in place)
     int* cl = reinterpret_cast<int*>(al + a.max_graph_edges * H);  // [me] source, graph-local
@@ -209,13 +212,16 @@ gat_layer_infer_kernel(trx_gat_layer_args a) {
     }
     if (IN > 0 && tid < n * IN) x0l[tid] = bf16r(x0v);
     if (IN == 0) {
-        trx_u4* dst4 = reinterpret_cast<trx_u4*>(xs);
+        constexpr int Q8 = HC / 8;  // 16-byte pieces per row
+        auto dst4 = [&](int v) -> trx_u4& {
+            return *reinterpret_cast<trx_u4*>(xs + (v / Q8) * XS + (v - (v / Q8) * Q8) * 8);
+        };
 #pragma unroll
         for (int j = 0; j < kStageBatch; ++j) {
             const int v = tid + kInferThreads * j;
-            if (v < nq) dst4[v] = stg[j];
+            if (v < nq) dst4(v) = stg[j];
         }
-        for (int v = tid + kInferThreads * kStageBatch; v < nq; v += kInferThreads) dst4[v] = xsrc[v];
+        for (int v = tid + kInferThreads * kStageBatch; v < nq; v += kInferThreads) dst4(v) = xsrc[v];
     }
     __syncthreads();
     for (int i = tid; i < n; i += kInferThreads)
@@ -246,7 +252,7 @@ gat_layer_infer_kernel(trx_gat_layer_args a) {
                 uint2 u;
                 u.x = pk_bf16(acc[0], acc[1]);
                 u.y = pk_bf16(acc[2], acc[3]);
-                *reinterpret_cast<uint2*>(xs + i * HC + 4 * q) = u;
+                *reinterpret_cast<uint2*>(xs + i * XS + 4 * q) = u;
             }
         }
         __syncthreads();
@@ -285,7 +291,7 @@ gat_layer_infer_kernel(trx_gat_layer_args a) {
 #pragma unroll
                     for (int m = 0; m < 4; ++m)
                         if (m < CM) {
-                            const uint2 u = *reinterpret_cast<const uint2*>(xs + i * HC + h * C + 4 * sl + 64 * m);
+                            const uint2 u = *reinterpret_cast<const uint2*>(xs + i * XS + h * C + 4 * sl + 64 * m);
                             const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
                             const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
                             s1 += (v0 * sa[m].x + v1 * sa[m].y) + (v2 * sa[m].z + v3 * sa[m].w);
@@ -312,7 +318,7 @@ gat_layer_infer_kernel(trx_gat_layer_args a) {
                 for (int c = 4 * sl; c < C; c += 64) {
                     const float4 sa = *reinterpret_cast<const float4*>(a.att_src + h * C + c);
                     const float4 da = *reinterpret_cast<const float4*>(a.att_dst + h * C + c);
-                    const uint2 u = *reinterpret_cast<const uint2*>(xs + i * HC + h * C + c);
+                    const uint2 u = *reinterpret_cast<const uint2*>(xs + i * XS + h * C + c);
                     const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
                     const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
                     s1 += (v0 * sa.x + v1 * sa.y) + (v2 * sa.z + v3 * sa.w);
@@ -414,7 +420,7 @@ gat_layer_infer_kernel(trx_gat_layer_args a) {
 #pragma unroll
         for (int k = 0; k < KC; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int p = rp[i]; p < rp[i + 1]; ++p) {
-            const uint16_t* row = xs + cl[p] * HC;
+            const uint16_t* row = xs + cl[p] * XS;
             const float* alr = al + p * H;
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
@@ -839,7 +845,7 @@ size_t edge_head_infer_smem(const trx_edge_head_args& a) {
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a) {
     const int HC = a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
     const size_t alsz = (size_t)me * H;
-    size_t b = (size_t)n * HC * 2 + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 * 2 + (size_t)(n + 1) * 4 +
+    size_t b = (size_t)n * (HC + 8) * 2 + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 * 2 + (size_t)(n + 1) * 4 +
                (size_t)n * a.in_dim * 4;
     if (a.pool) b += (size_t)n * HC * 4;
     return b;

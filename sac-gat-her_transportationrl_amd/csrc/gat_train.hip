@@ -85,9 +85,12 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
     const int sbeg = a.sptr[node0];
     if (ne > a.max_graph_edges || ne < 0 || a.sptr[node0 + n] - sbeg != ne) return;  // host checks the topology
 
-    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);         // [n][HC] bf16 lin output
-    float* gv = reinterpret_cast<float*>(xs + n * HC);         // [n][HC] dL/d(aggregate + bias)
-    float* al = gv + n * HC;                                   // [me*H] attention weights
+    // rows padded by 16 B: phase C1 reads four pairs' rows per wave instruction,
+    // which unpadded 2 KB / 4 KB strides put on the same LDS banks
+    constexpr int XS = HC + 8, GS = HC + 4;
+    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);         // [n][XS] bf16 lin output
+    float* gv = reinterpret_cast<float*>(xs + n * XS);         // [n][GS] dL/d(aggregate + bias)
+    float* al = gv + n * GS;                                   // [me*H] attention weights
     float* ge = al + a.max_graph_edges * H;                    // [me*H] dL/dalpha, then dL/de
     float* asd = ge + a.max_graph_edges * H;                   // [n][2H] a_src | a_dst
     float* gas = asd + 2 * n * H;                              // [n][H] dL/da_src
@@ -122,8 +125,9 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
         }
     if (IN == 0) {
         const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.xh) + (size_t)node0 * HC);
-        uint4* dst = reinterpret_cast<uint4*>(xs);
-        for (int v = tid; v < n * HC / 8; v += kT) dst[v] = src[v];
+        constexpr int Q8 = HC / 8;
+        for (int v = tid; v < n * Q8; v += kT)
+            *reinterpret_cast<uint4*>(xs + (v / Q8) * XS + (v - (v / Q8) * Q8) * 8) = src[v];
     }
     __syncthreads();
     for (int i = tid; i < n; i += kT)
@@ -146,7 +150,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
                 uint2 u;
                 u.x = pkbf(acc[0], acc[1]);
                 u.y = pkbf(acc[2], acc[3]);
-                *reinterpret_cast<uint2*>(xs + i * HC + 4 * q) = u;
+                *reinterpret_cast<uint2*>(xs + i * XS + 4 * q) = u;
             }
         }
     }
@@ -232,7 +236,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             o.y = rstd * (gx[k][1] - m1 - xh_[k][1] * m2);
             o.z = rstd * (gx[k][2] - m1 - xh_[k][2] * m2);
             o.w = rstd * (gx[k][3] - m1 - xh_[k][3] * m2);
-            *reinterpret_cast<float4*>(gv + i * HC + f0) = o;
+            *reinterpret_cast<float4*>(gv + i * GS + f0) = o;
         }
         if (IN > 0 && a.residual == 2) {
 #pragma unroll
@@ -257,7 +261,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 #pragma unroll
             for (int j = 0; j < INR; ++j) pwp[r][j] = 0.0f;
         auto node_terms = [&](int i, const float4 t4, const float4 v4) {
-            const float4 g4 = *reinterpret_cast<const float4*>(gv + i * HC + 4 * q);
+            const float4 g4 = *reinterpret_cast<const float4*>(gv + i * GS + 4 * q);
             const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w},
                         vv[4] = {v4.x, v4.y, v4.z, v4.w};
             const float mean = st[2 * i], rstd = st[2 * i + 1];
@@ -314,8 +318,8 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             const int p = ok ? t / H : 0, h = ok ? t - (t / H) * H : 0;
             float s = 0.0f;
             if (ok) {
-                const float* gr = gv + dl[p] * HC + h * C;
-                const uint16_t* xr = xs + cl[p] * HC + h * C;
+                const float* gr = gv + dl[p] * GS + h * C;
+                const uint16_t* xr = xs + cl[p] * XS + h * C;
                 for (int c = 4 * sl; c < C; c += 64) {
                     const float4 g4 = *reinterpret_cast<const float4*>(gr + c);
                     const uint2 u = *reinterpret_cast<const uint2*>(xr + c);
@@ -366,7 +370,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             for (int r = 0; r < 4; ++r) acc[k][r] = 0.0f;
         for (int k2 = sp[j]; k2 < sp[j + 1]; ++k2) {
             const int p = spp[k2];
-            const float* gr = gv + dl[p] * HC;
+            const float* gr = gv + dl[p] * GS;
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
                 const int f0 = 4 * (lane + kW * k);
@@ -425,7 +429,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 #pragma unroll
             for (int j = 0; j < INR; ++j) pw0[r][j] = 0.0f;
         auto node_terms = [&](int j, const uint2 w) {
-            const uint2 u = *reinterpret_cast<const uint2*>(xs + j * HC + 4 * q);
+            const uint2 u = *reinterpret_cast<const uint2*>(xs + j * XS + 4 * q);
             const float xv[4] = {lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y)};
             const float gs = gas[j * H + h], gd = gad[j * H + h];
 #pragma unroll
@@ -470,7 +474,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 
 size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a) {
     const size_t HC = (size_t)a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
-    return n * HC * 2 + n * HC * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
+    return n * (HC + 8) * 2 + n * (HC + 4) * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
            (a.g_pool ? 2 * HC * 4 : 0) + (2 * me + 2 * (n + 1) + me) * 4;
 }
 
