@@ -89,12 +89,7 @@ constexpr int kQs = 4;
 constexpr uint64_t kUnreached = 0x7FF8000000000000ull;
 constexpr uint32_t kScannedHi = 0xFFF80000u;
 constexpr int kMaxDeg = 16;   // out-degree (out-slot rounds of 4: 1, 2, 4)
-#ifndef TRX_DS_PAD
-#define TRX_DS_PAD 0  // A/B knob: float padding of a node's out-slot cost row (2: rows of 10 floats)
-#endif
-#ifndef TRX_KEY_PAD
-#define TRX_KEY_PAD 0  // A/B knob: u64 padding of a tree's key row (2: the 16 rows of a wave start on distinct banks)
-#endif
+
 
 struct SmemS {
     uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [EPW*E] f32 (dprev: CFW only); aux: u32 AON link
@@ -132,9 +127,9 @@ __host__ __device__ inline SmemS smems_layout(int E, int N, int Z, int NP, int E
     o.t = take(el);
     o.aux = take(el);
     o.dprev = take(cfw ? el : 0u);
-    o.ocost = take((uint32_t)(EPW * NP * (DS + TRX_DS_PAD) * 4));
-    o.ov = take((uint32_t)(NP * (DS + TRX_DS_PAD)));
-    o.keys = take((uint32_t)(rows * (NP + TRX_KEY_PAD) * 8));
+    o.ocost = take((uint32_t)(EPW * NP * DS * 4));
+    o.ov = take((uint32_t)(NP * DS));
+    o.keys = take((uint32_t)(rows * NP * 8));
     o.pred = take((uint32_t)(EPW * Z * NP));
     o.ord = take((uint32_t)(EPW * Z * NP));
     o.eid = take((uint32_t)(NP * NP));
@@ -257,7 +252,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     float* const sunas = (float*)(smem_raw + O.unas);
     int* const sact = (int*)(smem_raw + O.act);
     double* const sred = (double*)(smem_raw + O.red);
-    const int DSP = DS + TRX_DS_PAD;  // row stride of the out-slot tables
+    const int DSP = DS;  // row stride of the out-slot tables (padded rows measured neutral, round 3)
     const int NDS = NP * DSP;
 #ifdef TRX_PHASE_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
@@ -367,7 +362,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     for (int it = 0; it < p.iters; ++it) {
         // ---------------- shortest-path tree per quad (Dijkstra, sparse relaxation)
         if (tree_on) {
-            uint64_t* const kt = skeys + tree * (NP + TRX_KEY_PAD);
+            uint64_t* const kt = skeys + tree * NP;
             uint32_t* const kt32 = reinterpret_cast<uint32_t*>(kt);
             const float* const oc = socost + lenv * NDS;
             uint8_t* const ol = sord + tree * NP;

@@ -130,12 +130,8 @@ extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
 
 // ------------------------------------------------------------- layer kernel
 // IN: 0 = xh given (layers >= 1), else the layer-0 input width (4).
-#ifndef TRX_L0_WAVES
-#define TRX_L0_WAVES 1  // A/B knob: waves-per-SIMD register budget of the layer-0 instances
-#endif
 template <int HC, int IN, int NT>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(IN > 0 ? TRX_L0_WAVES : 1)))
-gat_layer_infer_kernel(trx_gat_layer_args a) {
+__global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int kInferThreads = NT, kInferWaves = NT / kWave;  // this instance's workgroup
     constexpr int KC = HC / 256;  // float4 chunks per lane in a row

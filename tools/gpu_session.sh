@@ -27,6 +27,8 @@ for s in "$@"; do
         benchenv) step bench_env 400 python bench.py --workload env --steps 66 --warmup 22 --no-cpu ;;
         benchtorch) step bench_torch 400 python bench.py --sp torch --steps 44 --warmup 22 --no-cpu
                     step bench_env_torch 400 python bench.py --workload env --sp torch --steps 66 --warmup 22 --no-cpu ;;
+        benchgreedy) step bench_greedy 400 python bench.py --workload greedy --iters 60 --cpu-seconds 5 &&
+                     step bench_greedy30 400 python bench.py --workload greedy --iters 30 --cpu-seconds 5 ;;
         benchana) step bench_ana 600 python bench.py --network anaheim --steps 10 --warmup 3 --cpu-seconds 5 ;;
         benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
         wgrad) step wgrad 200 python tools/wgrad_probe.py ;;
