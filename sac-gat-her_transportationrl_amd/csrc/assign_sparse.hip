@@ -477,11 +477,18 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 wave_sync_s();
             }
             // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree
-            // demand sums S(v) per tree in reverse scan order (one lane per tree, plain
-            // LDS read-modify-write); once S(v) is final it is added to the load of
-            // v's predecessor link (u32 LDS atomics).  Integral demands: exact in any order.
+            // demand sums S(v) per tree in reverse scan order, once final added to
+            // the load of v's predecessor link (u32 LDS atomics; integral demands:
+            // exact in any order).  The quad's four lanes take the scan slots four
+            // at a time (group = one scan-order word, lane j slot 4G + 3 - j, so
+            // lane 0 is the latest scanned): each lane reads its S(v) -- complete
+            // but for children scanned in the same group -- adds those over three
+            // quad broadcasts (lane m's S is final after round m), then adds S(v)
+            // to v's link load and, unless v's predecessor is in the group (it has
+            // taken S(v) already), to the predecessor's S (u32 LDS atomic: two
+            // lanes may share a predecessor).
             const float* dm = gdem + zi * N;
-            float* const sa = reinterpret_cast<float*>(kt);
+            uint32_t* const sa = reinterpret_cast<uint32_t*>(kt);
             float un = 0.0f;
 #pragma unroll
             for (int i = 0; i < NPL; ++i) {
@@ -489,10 +496,10 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 const float dv = v < N ? dm[v] : 0.0f;
                 const bool load = v < N && pl[v] != kNoPred;  // reached, not the origin
                 un += (dv > 0.0f && !load) ? dv : 0.0f;      // intrazonal or unreachable (708)
-                sa[v] = load ? dv : 0.0f;
+                sa[v] = load ? (uint32_t)dv : 0u;             // exact: integral demands < 2^24
             }
             wave_sync_s();
-            if (j == 0) {
+            {
                 uint32_t* const ll = sload + lenv * E;
                 constexpr int QH = NP / 8;  // scan-order words per half: two halves keep 2*QH VGPRs live
 #pragma unroll
@@ -510,15 +517,31 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                         pw[q] = w;
                     }
 #pragma unroll
-                    for (int kk = 4 * QH - 1; kk >= 0; --kk) {
-                        const int k = half * 4 * QH + kk;
-                        if (k >= 1 && k < nscan) {  // quad-uniform
-                            const int v = (ow[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
-                            const int pv = (pw[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
-                            const int e = seid[pv * NP + v];  // read beside the sums, off the chain
-                            const float sv = sa[v];
-                            sa[pv] = sa[pv] + sv;
-                            atomicAdd(ll + e, (uint32_t)sv);
+                    for (int q = QH - 1; q >= 0; --q) {
+                        const int kb = 4 * (half * QH + q);  // the group's first scan slot
+                        if (kb >= nscan) continue;           // quad-uniform
+                        const int sh = 8 * (3 - j);          // my slot kb + 3 - j
+                        const bool valid = kb + 3 - j >= 1 && kb + 3 - j < nscan;
+                        const int v = (ow[q] >> sh) & 0xFF, pv = (pw[q] >> sh) & 0xFF;
+                        uint32_t S = valid ? sa[v] : 0u;
+                        const int e = valid ? seid[pv * NP + v] : 0;
+                        auto take = [&](const uint32_t Sm, const int m) {  // lane m's final S, to its parent
+                            const int km = kb + 3 - m, pvm = (pw[q] >> (8 * (3 - m))) & 0xFF;
+                            const bool vm = km >= 1 && km < nscan;
+                            S += (j > m && vm && valid && pvm == v) ? Sm : 0u;
+                        };
+                        take((uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x00, 0xf, 0xf, false), 0);
+                        take((uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0x55, 0xf, 0xf, false), 1);
+                        take((uint32_t)__builtin_amdgcn_update_dpp(0, (int)S, 0xAA, 0xf, 0xf, false), 2);
+                        bool parent_here = false;  // v's predecessor scanned in this group, after v
+#pragma unroll
+                        for (int m = 1; m < 4; ++m) {
+                            const int km = kb + 3 - m, vmn = (ow[q] >> (8 * (3 - m))) & 0xFF;
+                            parent_here |= m > j && km >= 1 && km < nscan && vmn == pv;
+                        }
+                        if (valid) {
+                            atomicAdd(ll + e, S);
+                            if (!parent_here) atomicAdd(sa + pv, S);
                         }
                     }
                 }
