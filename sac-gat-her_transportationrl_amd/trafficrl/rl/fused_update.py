@@ -350,16 +350,19 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     dev = reward.device
     nx, ex = node_x.float().contiguous(), edge_attr.float().contiguous()
     nnx, nex = next_node_x.float().contiguous(), next_edge_attr.float().contiguous()
-    # no-grad next-state passes (sac.py:184-191): next actor probs, two target critics
+    # the no-grad next-state passes (sac.py:184-191: next actor probs, two target
+    # critics) and the training forwards of the two critics and the actor (raw
+    # logits, with saves) are independent: six streams at once (each network's
+    # kernels fill a fraction of the GPU at batch 256)
     with torch.no_grad():
-        nprobs, qt1, qt2 = agent._concurrent([
+        outs = agent._concurrent([
             lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask)[0],
             lambda: net_forward(agent.target1, nnx, nex, topo, save=False)[0],
-            lambda: net_forward(agent.target2, nnx, nex, topo, save=False)[0]])
-        # training forwards of the two critics and the actor (raw logits), with saves
-        ctxs = agent._concurrent([lambda net=net: net_forward(net, nx, ex, topo, save=True)
-                                  for net in (agent.critic1, agent.critic2, agent.actor)])
-    (q1, c1), (q2, c2), (lg, ca) = ctxs
+            lambda: net_forward(agent.target2, nnx, nex, topo, save=False)[0]] +
+            [lambda net=net: net_forward(net, nx, ex, topo, save=True)
+             for net in (agent.critic1, agent.critic2, agent.actor)])
+    nprobs, qt1, qt2 = outs[:3]
+    (q1, c1), (q2, c2), (lg, ca) = outs[3:]
     L = _lib.load()
     la = agent.log_alpha.detach().reshape(1)
     act_local = action % E      # the batch tuple carries graph offsets (arange(B) * E + action)

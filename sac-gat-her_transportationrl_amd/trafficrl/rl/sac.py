@@ -547,8 +547,8 @@ class DiscreteSAC:
         if dev.type != "cuda" or not self.concurrent or not self._warm:
             return [fn() for fn in fns]
         main = torch.cuda.current_stream(dev)
-        if self._side is None:
-            self._side = [torch.cuda.Stream(dev) for _ in range(3)]
+        if self._side is None or len(self._side) < len(fns):
+            self._side = [torch.cuda.Stream(dev) for _ in range(max(3, len(fns)))]
         outs = []
         for st, fn in zip(self._side, fns):
             st.wait_stream(main)
