@@ -52,6 +52,17 @@ rng = np.random.default_rng(5)
 dmg = np.zeros((B, 76), np.float32)
 for b in range(B):
     dmg[b, rng.choice(76, 22, replace=False)] = 1.0
-env.reset(damaged=torch.from_numpy(dmg), observe=False)
+dmg_t = torch.from_numpy(dmg).cuda()
+rs = []
+for r in range(3):   # cold resets: per-env random damage, then the fixed damage of the timed steps
+    for dm in (dmg_t, dmg0):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        env.reset(damaged=dm, observe=False)
+        e.record()
+        torch.cuda.synchronize()
+        rs.append(s.elapsed_time(e))
+env.reset(damaged=dmg_t, observe=False)
 h.update(env.flow.cpu().numpy().tobytes() + env.tstt.cpu().numpy().tobytes())
-print(f"{os.path.basename(sys.argv[1])} [{sp}]: step kernel {sum(ms) / len(ms):.4f} ms (B={B}) sha {h.hexdigest()[:12]}")
+print(f"{os.path.basename(sys.argv[1])} [{sp}]: step kernel {sum(ms) / len(ms):.4f} ms (B={B}) sha {h.hexdigest()[:12]}"
+      f"  reset random {min(rs[0::2]):.2f} ms, fixed {min(rs[1::2]):.2f} ms")
