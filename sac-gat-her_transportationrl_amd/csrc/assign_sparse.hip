@@ -460,20 +460,15 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
 #ifdef TRX_PHASE_STAMPS
             if (tid == 0) atomicAdd(&trx_phase_cycles_s[7], (unsigned long long)__popcll(need));  // replayed trees (wave 0)
 #endif
-            if (need) {  // wave-uniform, rare: exact scipy-heap replays, one tree at a time
+            if (need) {  // wave-uniform: exact scipy-heap replays of the ambiguous trees
                 const float* const stl = st + lenv * E;
-                // the exact heap lives in the caller's workspace (global memory, one
-                // FibLane per wave): the key rows stay intact for the AON phase
+                // every ambiguous tree's quad leader replays its own tree at once, each
+                // with its own heap in the caller's workspace (global memory, one
+                // FibLane per tree): cold resets with random damage are tie-heavy
+                // (most trees of a wave ambiguous), so one tree at a time serialised them
                 FibLane* const h = reinterpret_cast<FibLane*>(
-                    ws + ((size_t)blockIdx.x * (size_t)(L >> 6) + (size_t)(tid >> 6)) * sizeof(FibLane));
-                uint64_t pending = need;
-                while (pending) {
-                    const int leader = __ffsll((unsigned long long)pending) - 1;
-                    if ((tid & 63) == leader) {
-                        replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
-                    }
-                    pending &= pending - 1;
-                }
+                    ws + ((size_t)blockIdx.x * (size_t)(L >> 2) + (size_t)(tid >> 2)) * sizeof(FibLane));
+                if ((need >> (tid & 63)) & 1ull) replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
                 wave_sync_s();
             }
             // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree
@@ -657,7 +652,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
 
 size_t sparse_workspace_bytes(const DevGraph& g, int num_envs) {
     const LaunchCfg c = sparse_launch_cfg(g, num_envs, TRX_METHOD_MSA);
-    return (size_t)c.blocks * (size_t)(c.threads / 64) * sizeof(FibLane);
+    return (size_t)c.blocks * (size_t)(c.threads / 4) * sizeof(FibLane);  // one exact heap per tree (quad)
 }
 
 LaunchCfg sparse_launch_cfg(const DevGraph& g, int num_envs, int method) {

@@ -473,7 +473,7 @@ int trx_graph_info(const trx_graph* g, int32_t* num_nodes, int32_t* num_edges, i
 int64_t trx_workspace_bytes(const trx_graph* g, int32_t num_envs) {
     if (!g || num_envs < 0) return fail(TRX_EINVAL, "bad arguments");
     // small graphs: per-env work lives in LDS; the sparse kernel's rare exact-heap
-    // replays use one FibLane per wave here
+    // replays use one FibLane per tree here
     if (g->dg.N <= trx::kSmallMaxNodes)
         return (int64_t)std::max<size_t>(256, trx::sparse_workspace_bytes(g->dg, num_envs));
     // large graphs: one exact-heap scratch slot per wave (rarely touched)

@@ -131,7 +131,7 @@ LaunchCfg sparse_launch_cfg(const DevGraph& g, int num_envs, int method);
 hipError_t launch_env_kernel_sparse(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs,
                                     int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                     const uint8_t* env_mask, void* workspace, hipStream_t stream);
-size_t sparse_workspace_bytes(const DevGraph& g, int num_envs);  // exact-heap scratch, one FibLane per wave
+size_t sparse_workspace_bytes(const DevGraph& g, int num_envs);  // exact-heap scratch, one FibLane per tree
 hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream);
