@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 7
+#define TRX_ABI_VERSION 8
 
 /* error codes */
 #define TRX_OK 0
@@ -276,6 +276,53 @@ typedef struct trx_edge_head_args {
     int64_t* action;            /* [B] drawn graph-local link (u != NULL) */
 } trx_edge_head_args;
 int trx_edge_head_infer(const trx_edge_head_args* a, void* stream);
+
+/* Fused tail of the Actor/Critic inference pass (ABI 8): the last GATConv of
+ * GATEncoder (src/models/gat_encoder.py:22-25, 47-53: heads 1, concat False,
+ * LayerNorm, ELU, global mean|max pool) followed by the edge scorer of
+ * trx_edge_head_infer (src/rl/sac.py:38-46, 69-78), four graphs per workgroup:
+ *   xh = bf16(x @ w_lin^T)                  (bf16 MFMA, fp32 accumulation)
+ *   attention / aggregation / bias / LayerNorm / ELU / pool as trx_gat_layer_infer
+ *   p  = bf16(bf16(y) @ w_nodes^T), c = bf16(bf16(ctx) @ w_ctx^T) + b1   (MFMA)
+ *   logits / masked softmax / draw as trx_edge_head_infer
+ * Replaces lin GEMM + trx_gat_layer_infer + two GEMMs + trx_edge_head_infer of
+ * the last layer; outputs equal theirs up to the GEMMs' accumulation order.
+ * channels == hidden == 256, in_dim % 128 == 0 (<= 8192), nodes_per_graph
+ * 1..32, edges_per_graph 1..128, max_graph_edges 1..256, edge_dim 1..8.     */
+typedef struct trx_gat_tail_args {
+    int32_t num_graphs, nodes_per_graph, edges_per_graph, in_dim, channels, hidden, edge_dim, max_graph_edges;
+    const void* x;              /* bf16 [N, in_dim] the previous layer's output */
+    const void* w_lin;          /* bf16 [channels, in_dim] lin.weight */
+    const int32_t* rowptr;      /* [N+1] CSR by destination (self loops included) */
+    const int32_t* col;         /* [Et] */
+    const float* a_edge;        /* [Et, a_edge_stride] edge logits in CSR order */
+    int32_t a_edge_stride, a_edge_offset;
+    const float* att_src;       /* [channels] */
+    const float* att_dst;       /* [channels] */
+    const float* bias;          /* [channels] */
+    float negative_slope;
+    const float* ln_weight;     /* [channels] */
+    const float* ln_bias;       /* [channels] */
+    float ln_eps;
+    const void* w_nodes;        /* bf16 [2*hidden, channels]: rows [0, hidden) src, [hidden, 2*hidden) dst */
+    const void* w_ctx;          /* bf16 [hidden, 2*channels] */
+    const float* b1;            /* [hidden] */
+    const int32_t* src;         /* [B*E] global node ids of the links */
+    const int32_t* dst;
+    const float* ea;            /* [B*E, edge_dim] normalised link features */
+    const float* we;            /* [hidden, edge_dim] bf16-representable */
+    const float* w2;            /* [hidden] bf16-representable */
+    const float* b2;            /* [1] bf16-representable */
+    const float* mask;          /* [B*E] (softmax only) */
+    int32_t softmax;            /* as trx_edge_head_args */
+    float* out;                 /* [B*E] probs (softmax) or logits */
+    float* logits;              /* [B*E] masked logits (softmax) or NULL */
+    const float* u;             /* [B] uniforms or NULL: draw one link per graph into action */
+    int64_t* action;            /* [B] */
+    void* emb_bf16;             /* [N, channels] bf16 node embeddings, or NULL */
+    float* pool;                /* [B, 2*channels] mean | max, or NULL */
+} trx_gat_tail_args;
+int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream);
 /* Backward of the edge scorer's logits (softmax = 0) for training, one
  * workgroup per graph (hidden <= 256): from grad_logits [B*E] float32 and the
  * same args (p, c, ea, we, w2, src, dst, nodes_per_graph) it writes grad_p

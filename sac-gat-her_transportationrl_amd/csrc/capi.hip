@@ -665,6 +665,35 @@ int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream) {
     return TRX_OK;
 }
 
+int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_tail_infer: NULL args");
+    if (a->num_graphs < 0) return fail(TRX_EINVAL, "gat_tail_infer: num_graphs < 0");
+    if (a->channels != 256 || a->hidden != 256)
+        return fail(TRX_EUNSUP, "gat_tail_infer: channels and hidden must be 256 (got %d, %d)", a->channels, a->hidden);
+    if (a->in_dim < 128 || a->in_dim > 8192 || a->in_dim % 128 != 0)
+        return fail(TRX_EUNSUP, "gat_tail_infer: in_dim must be a multiple of 128 in 128..8192 (got %d)", a->in_dim);
+    if (a->nodes_per_graph < 1 || a->nodes_per_graph > 32)
+        return fail(TRX_EUNSUP, "gat_tail_infer: nodes_per_graph must be 1..32 (got %d)", a->nodes_per_graph);
+    if (a->edges_per_graph < 1 || a->edges_per_graph > 128)
+        return fail(TRX_EUNSUP, "gat_tail_infer: edges_per_graph must be 1..128 (got %d)", a->edges_per_graph);
+    if (a->max_graph_edges < 1 || a->max_graph_edges > 256)
+        return fail(TRX_EUNSUP, "gat_tail_infer: max_graph_edges must be 1..256");
+    if (a->edge_dim < 1 || a->edge_dim > 8) return fail(TRX_EUNSUP, "gat_tail_infer: edge_dim must be 1..8");
+    if (!a->x || !a->w_lin || !a->rowptr || !a->col || !a->a_edge || !a->att_src || !a->att_dst || !a->bias ||
+        !a->ln_weight || !a->ln_bias || !a->w_nodes || !a->w_ctx || !a->b1 || !a->src || !a->dst || !a->ea ||
+        !a->we || !a->w2 || !a->b2 || !a->out)
+        return fail(TRX_EINVAL, "gat_tail_infer: NULL buffer");
+    if (a->softmax && !a->mask) return fail(TRX_EINVAL, "gat_tail_infer: softmax needs a mask");
+    if (a->u && (!a->softmax || !a->action)) return fail(TRX_EINVAL, "gat_tail_infer: a draw needs softmax and action");
+    if (a->a_edge_stride < a->a_edge_offset + 1 || a->a_edge_offset < 0)
+        return fail(TRX_EINVAL, "gat_tail_infer: a_edge stride/offset");
+    if (trx::gat_tail_smem(*a) > 160 * 1024) return fail(TRX_EUNSUP, "gat_tail_infer: LDS > 160 KB");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_gat_tail_infer(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_tail_infer launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
     if (!a) return fail(TRX_EINVAL, "edge_head_infer: NULL args");
     if (a->num_graphs < 0 || a->edges_per_graph < 1 || a->edges_per_graph > 4096)

@@ -169,6 +169,9 @@ size_t gat_layer_infer_smem(const trx_gat_layer_args& a);
 hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream);
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
 size_t edge_head_infer_smem(const trx_edge_head_args& a);
+size_t gat_tail_smem(const trx_gat_tail_args& a);
+int gat_tail_mtiles(int nodes_per_graph);
+hipError_t launch_gat_tail_infer(const trx_gat_tail_args& a, hipStream_t stream);
 size_t edge_head_bwd_smem(const trx_edge_head_args& a);
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
                                 void* grad_z, float* grad_w2_part, hipStream_t stream);

@@ -21,6 +21,8 @@ tests/test_gat_infer.py states the tolerances.
 """
 from __future__ import annotations
 
+import os
+import weakref
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
@@ -29,6 +31,7 @@ import torch.nn.functional as F
 
 from .. import _lib
 from .gat_encoder import GATEncoder, GraphCSR, _LoopMean, build_csr, is_regular_batch
+from .tensor_cache import TensorKeyed
 
 
 @dataclass
@@ -43,7 +46,7 @@ class Topology:
     pos_src: torch.Tensor   # [Et] int32 per CSR position: input link id, or -(node+1) for a self loop
 
 
-_topo_cache: Dict[Tuple, Optional[Topology]] = {}
+_topo_cache = TensorKeyed()
 
 
 def topology(edge_index: torch.Tensor, batch: torch.Tensor, B: int) -> Optional[Topology]:
@@ -73,9 +76,7 @@ def topology(edge_index: torch.Tensor, batch: torch.Tensor, B: int) -> Optional[
                 pos = torch.where(perm < ek, link, -(perm - ek) - 1).to(torch.int32).contiguous()
                 topo = Topology(B, n, e, g, mx, src.to(torch.int32).contiguous(), dst.to(torch.int32).contiguous(),
                                 pos)
-    if len(_topo_cache) > 64:
-        _topo_cache.clear()
-    _topo_cache[key] = topo
+    _topo_cache.put(key, (edge_index, batch), topo)
     return topo
 
 
@@ -168,13 +169,17 @@ def _prepared(owner, name: str, params, make):
     key = (_PREP_EPOCH[0],) + tuple((p.data_ptr(), p._version) for p in params)
     slot = (id(owner), name)
     hit = _prep_cache.get(slot)
+    if hit is not None and hit[3]() is not owner:
+        # a recycled id(owner): a new module whose parameters may sit at the dead
+        # one's addresses with the same versions -- never its slot
+        hit = None
     if hit is not None and hit[0] == key:
         return hit[1]
     if capturing:
         raise RuntimeError("prepared weights are stale inside a static-weight capture (call refresh_static first)")
-    sig = tuple((p.device, p.dtype, tuple(p.shape)) for p in params)   # a recycled id(owner) must not reuse a slot
+    sig = tuple((p.device, p.dtype, tuple(p.shape)) for p in params)
     val = make(hit[1] if hit is not None and hit[2] == sig else None)
-    _prep_cache[slot] = (key, val, sig)
+    _prep_cache[slot] = (key, val, sig, weakref.ref(owner))
     return val
 
 
@@ -290,11 +295,12 @@ def prologue_supported(model) -> bool:
 
 
 def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology,
-                  a_edge: Optional[torch.Tensor] = None):
+                  a_edge: Optional[torch.Tensor] = None, upto: Optional[int] = None):
     """GATEncoder.forward (gat_encoder.py) for a regular batch, no grad, bf16
     autocast semantics.  `a_edge`: every layer's edge logits in CSR order
     from `prologue` (else computed here with torch ops).  Returns (node_emb
-    bf16 [N, out], global ctx fp32 [B, 2*out])."""
+    bf16 [N, out], global ctx fp32 [B, 2*out]); with `upto` only layers
+    [0, upto) run and the bf16 output of layer upto-1 is returned."""
     L = _lib.load()
     g = topo.g
     dev = x.device
@@ -320,6 +326,8 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
     prev_f32, prev_bf16 = None, None
     emb = ctx = None
     for i, l in enumerate(layers):
+        if upto is not None and i >= upto:
+            return prev_bf16
         last = i == len(layers) - 1
         HC = l.heads * l.out_channels
         args = _lib.TrxGatLayerArgs()
@@ -399,6 +407,84 @@ def edge_head_infer(head, emb_bf16: torch.Tensor, ctx: torch.Tensor, edge_attr: 
         action = torch.empty(topo.B, device=dev, dtype=torch.int64)
         args.u, args.action = uu.data_ptr(), action.data_ptr()
     _lib.check(L.trx_edge_head_infer(args, _lib.stream_ptr(dev)), "trx_edge_head_infer")
+    if mask is None:
+        return out
+    if u is not None:
+        return logits, out, action
+    return logits, out
+
+
+TAIL = os.environ.get("TRX_TAIL", "0") == "1"   # fused MFMA tail: off until faster than the layer path (tests compare both)
+
+
+def tail_supported(model, topo: Topology) -> bool:
+    """trx_gat_tail_infer limits: the last layer heads 1 / concat False with 256
+    channels after a layer of a multiple of 128 channels, edge MLP hidden 256,
+    <= 128 links per graph."""
+    if not TAIL:
+        return False
+    layers = list(model.encoder.layers)
+    last, prev = layers[-1], layers[-2]
+    W1 = model.edge_mlp[0].weight
+    return (len(layers) >= 2 and last.heads == 1 and not last.concat and last.out_channels == 256
+            and model.embed == 256 and W1.shape[0] == 256 and (prev.heads * prev.out_channels) % 128 == 0
+            and prev.heads * prev.out_channels <= 8192 and 1 <= topo.e <= 128 and 1 <= model.edge_in <= 8
+            and topo.n <= 32)
+
+
+def tail_infer(model, x_prev: torch.Tensor, ea: torch.Tensor, a_all: torch.Tensor, topo: Topology,
+               mask: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None):
+    """Last GAT layer + edge head in one launch (trx_gat_tail_infer, bf16 MFMA):
+    the same returns as edge_head_infer."""
+    L = _lib.load()
+    dev = x_prev.device
+    enc = model.encoder
+    layers = list(enc.layers)
+    l, norm = layers[-1], enc.norms[-1]
+    wts = prepared_encoder(enc, layers)
+    wn, wct, we, w2, b2 = prepared_head(model)
+    wc = wct.t()
+    assert wc.is_contiguous() and wn.is_contiguous() and x_prev.is_contiguous()
+    b1 = model.edge_mlp[0].bias.detach().float().contiguous()
+    att_s = l.att_src.detach().float().reshape(-1).contiguous()
+    att_d = l.att_dst.detach().float().reshape(-1).contiguous()
+    bias = l.bias.detach().float().contiguous()
+    lw, lb = norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous()
+    keep = [b1, att_s, att_d, bias, lw, lb]
+    a = _lib.TrxGatTailArgs()
+    a.num_graphs, a.nodes_per_graph, a.edges_per_graph = topo.B, topo.n, topo.e
+    a.in_dim, a.channels, a.hidden, a.edge_dim = x_prev.shape[1], l.out_channels, wn.shape[0] // 2, ea.shape[1]
+    a.max_graph_edges = topo.max_graph_edges
+    a.x, a.w_lin = x_prev.data_ptr(), wts[-1].data_ptr()
+    g = topo.g
+    a.rowptr, a.col = g.rowptr.data_ptr(), g.col.data_ptr()
+    a.a_edge, a.a_edge_stride = a_all.data_ptr(), a_all.shape[1]
+    a.a_edge_offset = sum(x.heads for x in layers[:-1])
+    a.att_src, a.att_dst, a.bias = att_s.data_ptr(), att_d.data_ptr(), bias.data_ptr()
+    a.negative_slope = float(l.negative_slope)
+    a.ln_weight, a.ln_bias, a.ln_eps = lw.data_ptr(), lb.data_ptr(), float(norm.eps)
+    a.w_nodes, a.w_ctx, a.b1 = wn.data_ptr(), wc.data_ptr(), b1.data_ptr()
+    a.src, a.dst = topo.src32.data_ptr(), topo.dst32.data_ptr()
+    eac = ea.float().contiguous()
+    keep.append(eac)
+    a.ea, a.we, a.w2, a.b2 = eac.data_ptr(), we.data_ptr(), w2.data_ptr(), b2.data_ptr()
+    BE = topo.B * topo.e
+    out = torch.empty(BE, device=dev, dtype=torch.float32)
+    logits = None
+    if mask is not None:
+        m = mask.float().contiguous()
+        keep.append(m)
+        logits = torch.empty(BE, device=dev, dtype=torch.float32)
+        a.mask, a.softmax, a.logits = m.data_ptr(), 1, logits.data_ptr()
+    a.out = out.data_ptr()
+    action = None
+    if u is not None:
+        uu = u.float().contiguous()
+        keep.append(uu)
+        action = torch.empty(topo.B, device=dev, dtype=torch.int64)
+        a.u, a.action = uu.data_ptr(), action.data_ptr()
+    _lib.check(L.trx_gat_tail_infer(a, _lib.stream_ptr(dev)), "trx_gat_tail_infer")
+    del keep
     if mask is None:
         return out
     if u is not None:

@@ -34,6 +34,7 @@ import torch.nn.functional as F
 
 from .. import _lib
 from .skinny import perm_gather, skinny_linear, splitk_linear
+from .tensor_cache import TensorKeyed
 
 # in-feature widths up to which a projection's weight gradient takes the
 # split-K path (trafficrl/models/skinny.py)
@@ -60,7 +61,7 @@ class GraphCSR:
     inv_perm: torch.Tensor  # [Et] int64 inverse of perm (PyG-order edge id -> CSR position)
 
 
-_csr_cache: Dict[Tuple, GraphCSR] = {}
+_csr_cache = TensorKeyed()
 
 
 def build_csr(edge_index: torch.Tensor, num_nodes: int) -> GraphCSR:
@@ -106,9 +107,7 @@ def build_csr(edge_index: torch.Tensor, num_nodes: int) -> GraphCSR:
     g = GraphCSR(num_nodes, keep, src_all, dst_all, perm, rowptr.to(torch.int32), col.to(torch.int32),
                  sptr.to(torch.int32), sperm.to(torch.int32), sdst.to(torch.int32), deg_in, kept_idx, in_pad, dk,
                  inv_perm)
-    if len(_csr_cache) > 64:
-        _csr_cache.clear()
-    _csr_cache[key] = g
+    _csr_cache.put(key, (edge_index,), g)
     return g
 
 
@@ -404,7 +403,7 @@ class GATConv(nn.Module):
         return out
 
 
-_layout_cache: Dict[Tuple, bool] = {}
+_layout_cache = TensorKeyed()
 
 
 def is_regular_batch(batch: torch.Tensor, num_graphs: int) -> bool:
@@ -419,9 +418,7 @@ def is_regular_batch(batch: torch.Tensor, num_graphs: int) -> bool:
     if r is None:
         ref = torch.arange(num_graphs, device=batch.device).repeat_interleave(n_tot // num_graphs)
         r = bool(torch.equal(batch.long(), ref))
-        if len(_layout_cache) > 64:
-            _layout_cache.clear()
-        _layout_cache[key] = r
+        _layout_cache.put(key, (batch,), r)
     return r
 
 

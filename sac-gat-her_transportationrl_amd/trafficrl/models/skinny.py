@@ -24,6 +24,8 @@ from typing import Dict, Tuple
 
 import torch
 
+from .tensor_cache import TensorKeyed
+
 _SPLIT = 256
 
 
@@ -134,7 +136,7 @@ class _RegularGather(torch.autograd.Function):
         return torch.matmul(ctx.inc.to(g.dtype), g).reshape(B * n, -1), None, None, None
 
 
-_inc_cache: Dict[Tuple, torch.Tensor] = {}
+_inc_cache = TensorKeyed()
 
 
 def regular_gather(x: torch.Tensor, idx_local: torch.Tensor, B: int) -> torch.Tensor:
@@ -144,9 +146,7 @@ def regular_gather(x: torch.Tensor, idx_local: torch.Tensor, B: int) -> torch.Te
     if inc is None:
         inc = torch.zeros(n, idx_local.numel(), device=x.device)
         inc[idx_local, torch.arange(idx_local.numel(), device=x.device)] = 1.0
-        if len(_inc_cache) > 64:
-            _inc_cache.clear()
-        _inc_cache[key] = inc
+        _inc_cache.put(key, (idx_local,), inc)
     return _RegularGather.apply(x, idx_local, inc, B)
 
 

@@ -223,6 +223,9 @@ class _EdgeHead(nn.Module):
         if topo is None or not fused.prologue_supported(self):
             return None
         x0, ea, a_all = fused.prologue(self, node_x, edge_attr, topo)
+        if fused.tail_supported(self, topo):   # last layer + edge head as one MFMA kernel
+            x_prev = fused.encoder_infer(self.encoder, x0, ea, topo, a_edge=a_all, upto=len(self.encoder.layers) - 1)
+            return fused.tail_infer(self, x_prev, ea, a_all, topo, mask=mask, u=u)
         emb, ctx = fused.encoder_infer(self.encoder, x0, ea, topo, a_edge=a_all)
         return fused.edge_head_infer(self, emb, ctx, ea, topo, mask=mask, u=u)
 
