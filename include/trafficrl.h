@@ -457,6 +457,15 @@ typedef struct trx_gat_prologue_bwd_args {
     float* part;                /* [num_graphs, 8A + 32] */
 } trx_gat_prologue_bwd_args;
 int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream);
+/* Backward of every layer's edge-attention rows M (trx_gat_prologue_infer's
+ * M_l[h, :] = sum_c lin_edge_l.weight[h*C + c, :] * att_edge_l[h, c]; PyG
+ * GATConv's lin_edge + att_edge, src/models/gat_encoder.py:22-25) from
+ * g_m [sum heads, g_m_stride] (trx_gat_prologue_backward's summed rows):
+ * out holds, per layer in order, g_lin_edge [heads*channels, edge_dim] then
+ * g_att_edge [heads*channels] (ABI 8; reads num_layers, heads, channels,
+ * edge_dim, lin_edge_w, att_edge of the args).                             */
+int trx_edge_att_weights_backward(const trx_gat_prologue_args* a, const float* g_m, int32_t g_m_stride, float* out,
+                                  void* stream);
 
 /* trx_sac_loss: DiscreteSAC.update's losses (src/rl/sac.py:184-219) for B
  * graphs of e links (e <= 256) and their gradients: soft V target from the

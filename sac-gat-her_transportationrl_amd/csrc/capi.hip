@@ -960,6 +960,20 @@ int trx_partial_sum(const float* part, int32_t rows, int32_t width, int64_t stri
     return TRX_OK;
 }
 
+int trx_edge_att_weights_backward(const trx_gat_prologue_args* a, const float* g_m, int32_t g_m_stride, float* out,
+                                  void* stream) {
+    if (!a || !g_m || !out) return fail(TRX_EINVAL, "edge_att_weights_backward: NULL argument");
+    if (a->num_layers < 1 || a->num_layers > TRX_MAX_GAT_LAYERS || a->edge_dim < 1 || a->edge_dim > 8 ||
+        g_m_stride < a->edge_dim)
+        return fail(TRX_EUNSUP, "edge_att_weights_backward: layers 1..4, edge_dim 1..8, stride >= edge_dim");
+    for (int l = 0; l < a->num_layers; ++l)
+        if (a->heads[l] < 1 || a->channels[l] < 1 || !a->lin_edge_w[l] || !a->att_edge[l])
+            return fail(TRX_EINVAL, "edge_att_weights_backward: layer %d", l);
+    hipError_t e = trx::launch_edge_att_weights_bwd(*a, g_m, g_m_stride, out, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "edge_att_weights_backward launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream) {
     if (!a) return fail(TRX_EINVAL, "gat_prologue_backward: NULL args");
     if (a->num_graphs < 0 || a->nodes_per_graph < 1 || a->nodes_per_graph > 64 || a->edges_per_graph < 0 ||

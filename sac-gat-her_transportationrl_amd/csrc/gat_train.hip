@@ -559,6 +559,48 @@ hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t st
     return hipGetLastError();
 }
 
+// ------------------------------------------- edge-attention weight backward
+// Backward of every layer's M rows (edge_att_weights_kernel, gat_infer.hip:
+// M[h, j] = sum_c lin_edge.weight[h*C + c, j] * att_edge[h, c]) from gM [A, stride]:
+//   g_lin_edge[h*C + c, j] = gM[h, j] * att_edge[h, c]
+//   g_att_edge[h, c]       = sum_j lin_edge.weight[h*C + c, j] * gM[h, j]   (j ascending)
+// One thread per (layer, h, c); out holds per layer [g_lin_edge (H*C*D) | g_att_edge (H*C)].
+__global__ void __launch_bounds__(256) edge_att_weights_bwd_kernel(trx_gat_prologue_args a, const float* __restrict__ gm,
+                                                                   int gm_stride, float* __restrict__ out) {
+    int t = blockIdx.x * 256 + threadIdx.x;
+    const int D = a.edge_dim;
+    int l = 0, row0 = 0;
+    size_t o = 0;
+    while (l < a.num_layers && t >= a.heads[l] * a.channels[l]) {
+        const int hc = a.heads[l] * a.channels[l];
+        t -= hc;
+        o += (size_t)hc * (D + 1);
+        row0 += a.heads[l];
+        ++l;
+    }
+    if (l >= a.num_layers) return;
+    const int C = a.channels[l], HC = a.heads[l] * C;
+    const int h = t / C;
+    const float att = a.att_edge[l][t];
+    const float* w = a.lin_edge_w[l] + (size_t)t * D;
+    const float* g = gm + (size_t)(row0 + h) * gm_stride;
+    float s = 0.0f;
+    for (int j = 0; j < D; ++j) {
+        out[o + (size_t)t * D + j] = g[j] * att;
+        s += w[j] * g[j];
+    }
+    out[o + (size_t)HC * D + t] = s;
+}
+
+hipError_t launch_edge_att_weights_bwd(const trx_gat_prologue_args& a, const float* gm, int gm_stride, float* out,
+                                       hipStream_t stream) {
+    int n = 0;
+    for (int l = 0; l < a.num_layers; ++l) n += a.heads[l] * a.channels[l];
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(edge_att_weights_bwd_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, a, gm, gm_stride, out);
+    return hipGetLastError();
+}
+
 // --------------------------------------------------------- prologue backward
 // One 4-wave workgroup per graph.  Forward (gat_infer.hip gat_prologue_kernel): ea = LN(edge_x),
 // x0 = LN(node_x), loop[i] = mean of ea over i's kept in-links, a_edge[p, k] =

@@ -32,7 +32,7 @@ EXPORTS = (
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
     "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
     "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_gat_prologue_backward",
-    "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer",
+    "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
 )
 
 
@@ -287,6 +287,7 @@ def load():
     L.trx_gat_layer_infer.argtypes = [ctypes.POINTER(TrxGatLayerArgs), _vp]
     L.trx_edge_head_infer.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp]
     L.trx_gat_tail_infer.argtypes = [ctypes.POINTER(TrxGatTailArgs), _vp]
+    L.trx_edge_att_weights_backward.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp, _i32, _vp, _vp]
     L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
     L.trx_edge_head_backward.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_graph_pool_forward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp]
@@ -326,7 +327,7 @@ def load():
                  "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
                  "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
                  "trx_episode_step", "trx_gat_layer_backward", "trx_partial_sum", "trx_gat_prologue_backward",
-                 "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer"):
+                 "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

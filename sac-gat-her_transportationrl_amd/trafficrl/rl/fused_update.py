@@ -230,8 +230,8 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     torch.cat([g_wn[:Hd], g_wn[Hd:], g_we, g_wc], 1, out=gW1)
     _grad(W1, gW1)
     for prm, src in ((net.edge_mlp[0].bias, g_c), (net.edge_mlp[2].weight, gw2p)):
-        dst = sink.take(prm.numel())
-        torch.sum(src, 0, out=dst)
+        dst = sink.take(prm.numel())      # column sums over the graphs, fixed order
+        _lib.check(L.trx_partial_sum(_lib.ptr(src), B, Hd, Hd, _lib.ptr(dst), stream), "trx_partial_sum")
         _grad(prm, dst)
     gb2 = sink.take(1)
     torch.sum(gl.to(torch.bfloat16), 0, keepdim=True, dtype=torch.float32, out=gb2)
@@ -323,21 +323,27 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     _grad(net.edge_norm.bias, pp[8 * A + 8:8 * A + 8 + ed])
     _grad(net.node_norm.weight, pp[8 * A + 16:8 * A + 16 + nd])
     _grad(net.node_norm.bias, pp[8 * A + 24:8 * A + 24 + nd])
-    gM = pp[:8 * A].view(A, 8)[:, :ed]
+    # M[h, j] = sum_c W[h*C + c, j] * att[h, c] (fp32, then bf16-rounded in the forward):
+    # every layer's lin_edge / att_edge gradient from the summed M-row gradients, one launch
+    ea_args = _lib.TrxGatPrologueArgs()
+    ea_args.num_layers, ea_args.edge_dim = len(layers), ed
+    keep = []
+    for i, l in enumerate(layers):
+        w, at = l.lin_edge.weight.detach().contiguous(), l.att_edge.detach().contiguous()
+        keep += [w, at]
+        ea_args.heads[i], ea_args.channels[i] = l.heads, l.out_channels
+        ea_args.lin_edge_w[i], ea_args.att_edge[i] = w.data_ptr(), at.data_ptr()
+    tot = sum(l.heads * l.out_channels * (ed + 1) for l in layers)
+    gout = sink.take(tot)
+    _lib.check(L.trx_edge_att_weights_backward(ea_args, _lib.ptr(pp), 8, _lib.ptr(gout), stream),
+               "trx_edge_att_weights_backward")
+    del keep
     off = 0
     for l in layers:
-        H, C = l.heads, l.out_channels
-        gm = gM[off:off + H]                                           # [H, ed]
-        att = l.att_edge.detach().view(H, C, 1)
-        W = l.lin_edge.weight.detach().view(H, C, ed)
-        # M[h, j] = sum_c W[h*C + c, j] * att[h, c]  (fp32, then bf16-rounded in the forward)
-        gwe = sink.take(H * C * ed).view(H, C, ed)
-        torch.mul(gm.view(H, 1, ed), att, out=gwe)
-        _grad(l.lin_edge.weight, gwe.view(H * C, ed))
-        gae = sink.take(H * C).view(H, C)
-        torch.sum(W * gm.view(H, 1, ed), 2, out=gae)
-        _grad(l.att_edge, gae)
-        off += H
+        HC = l.heads * l.out_channels
+        _grad(l.lin_edge.weight, gout[off:off + HC * ed].view(HC, ed))
+        _grad(l.att_edge, gout[off + HC * ed:off + HC * (ed + 1)])
+        off += HC * (ed + 1)
 
 
 def compute_gradients_fused(agent, batch, weights, topo: Topology):

@@ -490,10 +490,16 @@ class DiscreteSAC:
                     return net(*args)
             return run
 
-        q1_all, q2_all, act_out = self._concurrent([
+        # The training forwards (autograd recording) run in order on the current
+        # stream: with the recorded graphs on side streams, repeated updates in one
+        # process came out different from the sequential ones now and then (an
+        # unsynchronised reuse somewhere between the side-stream forwards and the
+        # backward; tools/fused_vs_autograd_probe.py).  The fused update, whose
+        # kernels take their stream explicitly, keeps its side streams.
+        q1_all, q2_all, act_out = [fn() for fn in (
             train_pass(self.critic1, node_x, edge_index, edge_attr, batch_vec, B),
             train_pass(self.critic2, node_x, edge_index, edge_attr, batch_vec, B),
-            train_pass(self.actor, node_x, edge_index, edge_attr, action_mask, batch_vec, False, B)])
+            train_pass(self.actor, node_x, edge_index, edge_attr, action_mask, batch_vec, False, B))]
         logits, probs = act_out[0], act_out[1]
         q1 = q1_all[action]
         q2 = q2_all[action]
