@@ -427,8 +427,8 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
         mw = lane < q1 - q0 ? al[q0 + lane] : 0.0f;
     }
 #pragma unroll
-    for (int j = 0; j < kMaxHalf; ++j) {
-        if (j >= cnt) break;
+    for (int j = 0; j < kMaxHalf; ++j) {  // compile-time trip count: ysv stays in registers
+        if (j >= cnt) continue;
         const int node = nb + j;
         const int deg = min(__builtin_amdgcn_readlane(rpl, j + 1) - __builtin_amdgcn_readlane(rpl, j), kW);
         const int cc = mc;
@@ -523,7 +523,7 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
 #pragma unroll
     for (int j = 0; j < kMaxHalf; ++j) {
         const int i = i_lo + j;
-        if (!gon || i >= i_hi) break;
+        if (!gon || i >= i_hi) continue;
         const int node = gw * n + i;
         uint2 u;
         u.x = pk2(ysv[j][0], ysv[j][1]);
@@ -609,7 +609,6 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
                 w2_r[r] = w2s[k];
                 c_r[r] = cs[gw * kTC + k];
             }
-#pragma unroll 2
             for (int it = 0; it < nit; ++it) {
                 const int e = 8 * it + 4 * par + r4;
                 const int v = gw * E + (e < E ? e : E - 1);
