@@ -680,18 +680,23 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // mk[] written by every lane, read by lane 0
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane == 0) {  // one categorical draw per graph (inverse CDF over the same exp terms)
-            const float target = a.u[g] * ssum;
-            float acc = 0.0f;
-            int pick = -1, last = 0;
-            for (int e = 0; e < E; ++e) {
-                const float ex = mk[e];
-                if (ex > 0.0f) last = e;
+        // one categorical draw per graph (inverse CDF over the same exp terms, summed in
+        // link order): the terms come to the wave's registers 64 at a time and the
+        // serial scan reads them with readlane (no dependent LDS reads)
+        const float target = a.u[g] * ssum;
+        float acc = 0.0f;
+        int pick = -1, last = 0;
+        for (int e0 = 0; e0 < E; e0 += kWave) {
+            const float exl = e0 + lane < E ? mk[e0 + lane] : 0.0f;
+            const int cnt = E - e0 < kWave ? E - e0 : kWave;
+            for (int t = 0; t < cnt; ++t) {
+                const float ex = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(exl), t));
+                if (ex > 0.0f) last = e0 + t;
                 acc += ex;
-                if (pick < 0 && acc > target) pick = e;
+                if (pick < 0 && acc > target) pick = e0 + t;
             }
-            a.action[g] = pick >= 0 ? pick : last;  // u * total above the serial sum: last link with mass
         }
+        if (lane == 0) a.action[g] = pick >= 0 ? pick : last;  // u * total above the serial sum: last link with mass
     }
     TRX_ESTAMP(3);
 }
