@@ -218,7 +218,10 @@ class VecRepairEnv:
         (default all) from their own RNG streams, as RepairEnv.reset draws them."""
         ratio = self.damaged_ratio if damaged_ratio is None else damaged_ratio
         ids = list(range(self.num_envs)) if ids is None else ids
-        if self._fixed[0] or self._samplers is not None:
+        # numpy's choice for E > 10000 links is not the Floyd draw the native sampler
+        # restates (trx_damage_sample's limit): those graphs take the numpy samplers,
+        # which continue the same per-env streams
+        if self._fixed[0] or self._samplers is not None or self.num_edges > 10000:
             masks = np.stack([self.samplers[i].sample(ratio) for i in ids])
         else:   # every env's own default_rng(seed) stream, one native call for the batch
             if self._rng_states is None:

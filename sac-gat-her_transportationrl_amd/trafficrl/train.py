@@ -118,6 +118,7 @@ class GradAllReduce:
     def __init__(self, world: int, agent=None):
         import torch.distributed as dist
         self.dist, self.world, self.agent = dist, world, agent
+        self.calls = {"flat": 0, "bucket": 0}   # which path ran (tests)
 
     def _flat_of(self, grads):
         flat = getattr(self.agent, "grad_flat", None) if self.agent is not None else None
@@ -133,9 +134,11 @@ class GradAllReduce:
     def __call__(self, grads):
         flat = self._flat_of(grads)
         if flat is not None:
+            self.calls["flat"] += 1
             self.dist.all_reduce(flat)
             flat.div_(self.world)
             return
+        self.calls["bucket"] += 1
         flat = torch.cat([g.reshape(-1) for g in grads])
         self.dist.all_reduce(flat)
         flat.div_(self.world)

@@ -1,5 +1,7 @@
 """Worker for tests/test_dist_gpu.py: one rank of a data-parallel Trainer run
-on a shared GPU over gloo (TRX_DIST_BACKEND rehearsal of the RCCL path).
+on a shared GPU over gloo (TRX_DIST_BACKEND rehearsal of the RCCL path), or a
+single rank over nccl (RCCL) itself.  TRX_WORKER_HIDDEN sets hidden = embed
+(32: the autograd update path; 256: the fused update and its flat buffer).
 
 Each rank trains `iters` vector iterations with HIP-graph updates (3 eager
 warm-ups, then the update captured as two graphs around the eager gradient
@@ -20,23 +22,43 @@ import torch.distributed as dist  # noqa: E402
 def main():
     out, iters, sync, method = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo")
+    backend = os.environ.get("TRX_DIST_BACKEND", "gloo")
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend)
+    hid = int(os.environ.get("TRX_WORKER_HIDDEN", "32"))
     from trafficrl.train import Trainer, sf_config
     cfg = sf_config()
-    cfg.update(num_envs=64, batch_start=64, batch_size=32, hidden_dim=32, embed_dim=32, eval_every=0,
+    cfg.update(num_envs=64, batch_start=64, batch_size=32, hidden_dim=hid, embed_dim=hid, eval_every=0,
                output_dir=os.path.join(out, f"run{rank}"), update_every=1, update_unit="iterations",
                her_ratio=0.5, assignment_method=method, assignment_iters=10, fixed_damage=False,
                early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0)
     tr = Trainer(cfg, device="cuda:0", rank=rank, world=world if sync else 1, log=False)
     if not sync:
         tr.agent.grad_sync = None
+    elif world == 1:  # one rank: the all-reduce is the identity, but its code path (RCCL) runs
+        from trafficrl.train import GradAllReduce
+        tr.agent.grad_sync = GradAllReduce(1, tr.agent)
     hist = tr.run(max_iters=iters)
+    identity = None
+    if sync and world == 1 and tr.agent.grad_flat is not None:
+        # one more reduce of the last update's flat gradient buffer: on one rank it
+        # must hand every value back unchanged
+        before = tr.agent.grad_flat.clone()
+        tr.agent.grad_sync(tr.agent.gradients())
+        torch.cuda.synchronize()
+        identity = bool(torch.equal(before, tr.agent.grad_flat))
     sd = {f"{m}.{k}": v.detach().cpu() for m in ("actor", "critic1", "critic2", "target1", "target2")
           for k, v in getattr(tr.agent, m).state_dict().items()}
     sd["log_alpha"] = tr.agent.log_alpha.detach().cpu()
     torch.save({"params": sd, "episodes": tr.episodes_done, "history": len(hist),
                 "graphed": tr._graphed is not None and tr._graphed.g_grads is not None,
-                "split": tr._graphed is not None and tr._graphed.g_apply is not None}, os.path.join(out, f"rank{rank}.pt"))
+                "split": tr._graphed is not None and tr._graphed.g_apply is not None,
+                "reduce_calls": dict(tr.agent.grad_sync.calls) if tr.agent.grad_sync is not None else None,
+                "identity": identity},
+               os.path.join(out, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -28,12 +28,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(tmp, sync, method="fw", iters=12, world=2):
+def _run(tmp, sync, method="fw", iters=12, world=2, extra=None):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0", **(extra or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_trainer_worker.py"), str(tmp),
                                        str(iters), str(int(sync)), method], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT))
@@ -71,3 +71,21 @@ def test_two_ranks_diverge_without_allreduce(tmp_path):
     res = _run(tmp_path, sync=False, iters=8)
     p0, p1 = res[0]["params"], res[1]["params"]
     assert any(not torch.equal(p0[k], p1[k]) for k in p0)
+
+
+def test_rccl_single_rank_flat_all_reduce(tmp_path):
+    """The nccl (RCCL) branch itself, which two ranks on one GPU cannot take: one
+    rank trains with the fused update (hidden = embed = 256), its gradients
+    reduced in place in the flat buffer by RCCL (GradAllReduce's flat path,
+    never the bucket) between the two captured update graphs; a final reduce
+    of the last flat buffer hands every value back unchanged (one rank: the
+    identity).  Runs are not compared bit for bit with a run without the
+    reduce: training is not bitwise reproducible across processes (measured:
+    two identical runs ~3e-4 apart in parameters after 10 iterations)."""
+    extra = {"TRX_DIST_BACKEND": "nccl", "TRX_WORKER_HIDDEN": "256"}
+    a = _run(tmp_path, sync=True, iters=10, world=1, extra=extra)[0]
+    assert a["graphed"] and a["split"], (a["graphed"], a["split"])
+    assert a["reduce_calls"]["flat"] > 0 and a["reduce_calls"]["bucket"] == 0, a["reduce_calls"]
+    assert a["identity"] is True
+    for k, v in a["params"].items():
+        assert bool(torch.isfinite(v.float()).all()), k
