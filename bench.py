@@ -343,6 +343,9 @@ def main():
     ap.add_argument("--no-observe", action="store_true", help="skip get_state (assignment-only steps)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-gemm-tuning", action="store_true",
+                    help="train workload: torch's default GEMM kernels instead of the shipped TunableOp "
+                         "selection (trafficrl/gemm_tuning_gfx950.csv)")
     ap.add_argument("--workload", default=None, choices=["train", "env", "greedy"],
                     help="default train (sf) / env (anaheim); greedy = config #1 (one env, greedy baseline; "
                          "--iters 60 is configs/sioux_falls.yaml's K)")
@@ -400,12 +403,13 @@ def main():
         return out
 
     if args.workload == "train":
-        from trafficrl.train import Trainer, sf_config
+        from trafficrl.train import GEMM_TUNING_GFX950, Trainer, sf_config
         cfg = sf_config()
         cfg.update(num_envs=B, assignment_iters=args.iters, assignment_method=args.method, sp_backend=args.sp,
                    batch_start=256,
                    batch_size=256, update_every=4, updates_per_step=1, update_unit="iterations", eval_every=0, episodes=10 ** 9,
-                   output_dir=os.path.join("/tmp", f"trx_bench_{os.getpid()}"), amp="bf16")
+                   output_dir=os.path.join("/tmp", f"trx_bench_{os.getpid()}"), amp="bf16",
+                   gemm_tuning=None if args.no_gemm_tuning else GEMM_TUNING_GFX950)
         tr = Trainer(cfg, device=dev, rank=rank, world=world, log=False)
         env = tr.env
         raw_step, raw_act, raw_update = env.step, tr.act, tr.update
@@ -565,6 +569,8 @@ def main():
                 "envs_per_gpu": B, "global_envs": B * world, "network": NETWORKS[args.network][2],
                 "method": args.method, "assignment_iters": args.iters, "episode_len": ep_len,
                 "parallelism": f"env-sharded x{world}",
+                **({"gemm_kernels": ("TunableOp selection trafficrl/gemm_tuning_gfx950.csv (lookup only)"
+                                     if tr.tuned_gemms else "torch default")} if args.workload == "train" else {}),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

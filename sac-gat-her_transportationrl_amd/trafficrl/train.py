@@ -91,6 +91,28 @@ def load_config(path: Optional[str]) -> Dict:
     return cfg
 
 
+GEMM_TUNING_GFX950 = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tuning_gfx950.csv")
+
+
+def use_tuned_gemms(path: str) -> bool:
+    """Select the GEMM kernels of the acting pass and the SAC update from a
+    PyTorch TunableOp results file (hipBLASLt / rocBLAS solution per shape,
+    measured on MI355X with this image's ROCm, hipBLASLt and torch: the file's
+    validators must match or torch ignores it).  Lookup only -- no tuning at
+    run time, nothing written; shapes not in the file keep torch's default.
+    Same operands and fp32 accumulation: another kernel, not another precision.
+    Process-wide (TunableOp is global)."""
+    import torch.cuda.tunable as tunable
+    if not (torch.cuda.is_available() and os.path.exists(path)):
+        return False
+    import tempfile
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    # TunableOp's own output file (written at exit, if at all) goes to a scratch path
+    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"trx_tunableop_{os.getpid()}.csv"))
+    return bool(tunable.read_file(path))
+
+
 def sf_config() -> Dict:
     """The Sioux Falls GAT-SAC setup (trafficrl/sf_sac.yaml: the reference's
     configs/sioux_falls.yaml values plus num_envs / amp)."""
@@ -285,6 +307,9 @@ class Trainer:
     def __init__(self, cfg: Dict, device="cuda", rank: int = 0, world: int = 1, log: bool = True):
         self.cfg, self.rank, self.world = cfg, rank, world
         self.device = torch.device(device)
+        # opt-in (cfg gemm_tuning: a TunableOp results file, e.g. GEMM_TUNING_GFX950)
+        self.tuned_gemms = bool(cfg.get("gemm_tuning")) and self.device.type == "cuda" and \
+            use_tuned_gemms(cfg["gemm_tuning"])
         torch.manual_seed(int(cfg["seed"]) + rank)
         np.random.seed(int(cfg["seed"]) + rank)
         self.gen = torch.Generator(device=self.device).manual_seed(int(cfg["seed"]) * 1000 + rank)
