@@ -106,11 +106,17 @@ def use_tuned_gemms(path: str) -> bool:
     if not (torch.cuda.is_available() and os.path.exists(path)):
         return False
     import tempfile
-    tunable.enable(True)
-    tunable.tuning_enable(False)
-    # TunableOp's own output file (written at exit, if at all) goes to a scratch path
-    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"trx_tunableop_{os.getpid()}.csv"))
-    return bool(tunable.read_file(path))
+    try:
+        tunable.enable(True)
+        tunable.tuning_enable(False)
+        # TunableOp's own output file (written at exit, if at all) goes to a scratch path
+        tunable.set_filename(os.path.join(tempfile.gettempdir(), f"trx_tunableop_{os.getpid()}.csv"))
+        if tunable.read_file(path):
+            return True
+    except Exception:   # an unreadable file or another torch build: torch's default kernels
+        pass
+    tunable.enable(False)
+    return False
 
 
 def sf_config() -> Dict:
