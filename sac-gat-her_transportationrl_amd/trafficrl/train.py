@@ -181,9 +181,16 @@ def capture_graph(fn, pool=None):
     """torch.cuda.graph capture of fn() with the memset nodes rewritten into
     fill kernels before instantiation (trx_graph_patch_memsets: ROCm 7.2's
     packet-capture replay skips small memset nodes, which torch's multi-block
-    reductions use to clear their semaphores)."""
+    reductions use to clear their semaphores).
+
+    Capture mode thread_local: under data parallelism the process group's
+    watchdog thread polls the HIP events of finished RCCL work (hipEventQuery)
+    at any time; in the default global mode such a call from another thread
+    during a capture fails with hipErrorStreamCaptureUnsupported and the
+    watchdog aborts the rank (seen in tests/test_dist_gpu.py's RCCL test).
+    Only this thread's capture-unsafe calls are checked."""
     g = torch.cuda.CUDAGraph(keep_graph=True)
-    with torch.cuda.graph(g, pool=pool):
+    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
         out = fn()
     _lib.patch_graph_memsets(g)
     g.instantiate()
