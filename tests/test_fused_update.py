@@ -45,7 +45,7 @@ def _ref_grads(agent, batch, w, B):
     cl.backward()
     al.backward()
     aal.backward()
-    return _grads(agent), float(agent.log_alpha.grad), (float(cl), float(al), float(aal))
+    return _grads(agent), float(agent.log_alpha.grad), (float(cl.detach()), float(al.detach()), float(aal.detach()))
 
 
 def _worst(got, ref):
