@@ -522,6 +522,15 @@ def main():
     valu_frac = pmc.get("valu_busy_frac") if pmc else None
     lds_conf = pmc.get("lds_bank_conflict_frac") if pmc else None
     mfma = gemm_mfma(B * N, B) if (args.workload == "train" and rank == 0) else None
+    if mfma is not None and breakdown.get("act"):
+        # the live acting pass (one per step, HIP events around it in the timed loop):
+        # its GEMM FLOPs over its whole wall time -- GAT layer kernels, edge scorer,
+        # prologue included -- beside the GEMM-only figure above
+        act_ms = breakdown["act"]
+        mfma.update(act_pass_ms=act_ms, act_pass_achieved=mfma["flops_per_pass"] / (act_ms / 1e3) / 1e12,
+                    act_pass_frac=mfma["flops_per_pass"] / (act_ms / 1e3) / MFMA_PEAK_BF16,
+                    act_pass_note="frac / achieved: the acting GEMMs' shapes timed alone (torch.mm, HIP events); "
+                                  "act_pass_*: the same FLOPs over the timed acting pass of this run")
     upd_stats = None
     if args.workload == "train" and phase_ev.get("update"):
         # SAC update throughput (the timed updates are graph replays), and the env

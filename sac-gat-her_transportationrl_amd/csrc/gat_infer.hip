@@ -521,7 +521,10 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
 // registers), and a wave reduction of the 256->1 product.
 constexpr int kEdgeED = 8;  // edge_dim <= 8
 
-template <int MQ>  // hidden <= 256 * MQ, hidden % 4 == 0
+// DK: the link-feature count when fixed at compile time (the regular case, 6: no
+// per-term edge_dim test and no padding terms in the link-feature product), 0 = any
+// edge_dim <= kEdgeED.  The same terms in the same order either way.
+template <int MQ, int DK>  // hidden <= 256 * MQ, hidden % 4 == 0
 __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge_head_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int ED = kEdgeED;
@@ -588,7 +591,8 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         const int e = v / ED, j = v - (v / ED) * ED;
         eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
     }
-    float we_r[MQ][4][ED], w2_r[MQ][4], c_r[MQ][4];
+    constexpr int DC = DK > 0 ? DK : ED;
+    float we_r[MQ][4][DC], w2_r[MQ][4], c_r[MQ][4];
 #pragma unroll
     for (int m = 0; m < MQ; ++m)
 #pragma unroll
@@ -598,7 +602,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
             w2_r[m][r] = ok ? a.w2[k] : 0.0f;
             c_r[m][r] = ok ? a.c[(int64_t)g * Hd + k] : 0.0f;
 #pragma unroll
-            for (int j = 0; j < ED; ++j) we_r[m][r][j] = (ok && j < D) ? a.we[k * D + j] : 0.0f;
+            for (int j = 0; j < DC; ++j) we_r[m][r][j] = (ok && (DK > 0 || j < D)) ? a.we[k * D + j] : 0.0f;
         }
     const float b2 = a.b2[0];
     if (badf) *badl = 1;
@@ -612,7 +616,10 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
     }
 
     TRX_ESTAMP(0);
-    constexpr int EU = 2;  // links per wave iteration
+#ifndef TRX_EH_EU
+#define TRX_EH_EU 2
+#endif
+    constexpr int EU = TRX_EH_EU;  // links per wave iteration
     for (int e0 = wave * EU; e0 < E; e0 += kInferWaves * EU) {
         float part[EU];
 #pragma unroll
@@ -638,8 +645,8 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
                     for (int r = 0; r < 4; ++r) {
                         float ew = 0.0f;
 #pragma unroll
-                        for (int j = 0; j < ED; ++j)
-                            if (j < D) ew += ear[j] * we_r[m][r][j];
+                        for (int j = 0; j < DC; ++j)
+                            if (DK > 0 || j < D) ew += ear[j] * we_r[m][r][j];
                         const float z1 = bf16r(psv[r] + pdv[r]);
                         const float z2 = bf16r(z1 + bf16r(ew));
                         const float z3 = z2 + c_r[m][r];
@@ -920,6 +927,7 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 // grad_w2_part [B, H] (per-graph sums of bf16(g) * bf16(relu(z))).
 constexpr int kEhbThreads = 1024, kEhbParts = kEhbThreads / 256;
 
+template <int DK>  // compile-time link-feature count, 0 = any (as edge_head_infer_kernel)
 __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
                                                                     uint16_t* grad_p, float* grad_c,
                                                                     uint16_t* grad_z, float* grad_w2_part) {
@@ -958,9 +966,10 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
         eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
     }
     const bool on = k < Hd;
-    float we[ED];
+    constexpr int DC = DK > 0 ? DK : ED;
+    float we[DC];
 #pragma unroll
-    for (int j = 0; j < ED; ++j) we[j] = (on && j < D) ? a.we[k * D + j] : 0.0f;
+    for (int j = 0; j < DC; ++j) we[j] = (on && (DK > 0 || j < D)) ? a.we[k * D + j] : 0.0f;
     const float w2 = on ? a.w2[k] : 0.0f, ck = on ? a.c[(int64_t)g * Hd + k] : 0.0f;
     __syncthreads();
     if (tid < n) {  // per-node link lists (link order); counts first
@@ -993,8 +1002,8 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
             const int s = sl[e], d = dl[e];
             float ew = 0.0f;
 #pragma unroll
-            for (int j = 0; j < ED; ++j)
-                if (j < D) ew += eal[e * ED + j] * we[j];
+            for (int j = 0; j < DC; ++j)
+                if (DK > 0 || j < D) ew += eal[e * ED + j] * we[j];
             const float z1 = bf16r(bf2f(pr[s * 2 * Hd + k]) + bf2f(pr[d * 2 * Hd + Hd + k]));
             const float z2 = bf16r(z1 + bf16r(ew));
             const float z3 = z2 + ck;
@@ -1039,28 +1048,41 @@ size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
                                 void* grad_z, float* grad_w2_part, hipStream_t stream) {
     const size_t smem = edge_head_bwd_smem(a);
+    const bool d6 = a.edge_dim == 6;
+    const void* fn = d6 ? reinterpret_cast<const void*>(edge_head_bwd_kernel<6>)
+                        : reinterpret_cast<const void*>(edge_head_bwd_kernel<0>);
     if (smem > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(edge_head_bwd_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(edge_head_bwd_kernel, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
-                       static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
+    if (d6)
+        hipLaunchKernelGGL(edge_head_bwd_kernel<6>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
+                           static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
+    else
+        hipLaunchKernelGGL(edge_head_bwd_kernel<0>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
+                           static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
     return hipGetLastError();
 }
 
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream) {
     const size_t smem = edge_head_infer_smem(a);
-    const void* fn = a.hidden <= 256 ? reinterpret_cast<const void*>(edge_head_infer_kernel<1>)
-                                     : reinterpret_cast<const void*>(edge_head_infer_kernel<2>);
+    const bool d6 = a.edge_dim == 6;  // the networks' link features (repair_env.py:800-808)
+    const void* fn = a.hidden <= 256 ? (d6 ? reinterpret_cast<const void*>(edge_head_infer_kernel<1, 6>)
+                                           : reinterpret_cast<const void*>(edge_head_infer_kernel<1, 0>))
+                                     : (d6 ? reinterpret_cast<const void*>(edge_head_infer_kernel<2, 6>)
+                                           : reinterpret_cast<const void*>(edge_head_infer_kernel<2, 0>));
     if (smem > 64 * 1024) {  // opt in to more than 64 KB of dynamic LDS
         const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    if (a.hidden <= 256)
-        hipLaunchKernelGGL(edge_head_infer_kernel<1>, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
+    if (a.hidden <= 256 && d6)
+        hipLaunchKernelGGL((edge_head_infer_kernel<1, 6>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
+    else if (a.hidden <= 256)
+        hipLaunchKernelGGL((edge_head_infer_kernel<1, 0>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
+    else if (d6)
+        hipLaunchKernelGGL((edge_head_infer_kernel<2, 6>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
     else
-        hipLaunchKernelGGL(edge_head_infer_kernel<2>, dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
+        hipLaunchKernelGGL((edge_head_infer_kernel<2, 0>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
     return hipGetLastError();
 }
 
