@@ -927,7 +927,6 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 // grad_w2_part [B, H] (per-graph sums of bf16(g) * bf16(relu(z))).
 constexpr int kEhbThreads = 1024, kEhbParts = kEhbThreads / 256;
 
-template <int DK>  // compile-time link-feature count, 0 = any (as edge_head_infer_kernel)
 __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
                                                                     uint16_t* grad_p, float* grad_c,
                                                                     uint16_t* grad_z, float* grad_w2_part) {
@@ -966,10 +965,9 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
         eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
     }
     const bool on = k < Hd;
-    constexpr int DC = DK > 0 ? DK : ED;
-    float we[DC];
+    float we[ED];
 #pragma unroll
-    for (int j = 0; j < DC; ++j) we[j] = (on && (DK > 0 || j < D)) ? a.we[k * D + j] : 0.0f;
+    for (int j = 0; j < ED; ++j) we[j] = (on && j < D) ? a.we[k * D + j] : 0.0f;
     const float w2 = on ? a.w2[k] : 0.0f, ck = on ? a.c[(int64_t)g * Hd + k] : 0.0f;
     __syncthreads();
     if (tid < n) {  // per-node link lists (link order); counts first
@@ -1002,8 +1000,8 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
             const int s = sl[e], d = dl[e];
             float ew = 0.0f;
 #pragma unroll
-            for (int j = 0; j < DC; ++j)
-                if (DK > 0 || j < D) ew += eal[e * ED + j] * we[j];
+            for (int j = 0; j < ED; ++j)
+                if (j < D) ew += eal[e * ED + j] * we[j];
             const float z1 = bf16r(bf2f(pr[s * 2 * Hd + k]) + bf2f(pr[d * 2 * Hd + Hd + k]));
             const float z2 = bf16r(z1 + bf16r(ew));
             const float z3 = z2 + ck;
@@ -1048,19 +1046,13 @@ size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
                                 void* grad_z, float* grad_w2_part, hipStream_t stream) {
     const size_t smem = edge_head_bwd_smem(a);
-    const bool d6 = a.edge_dim == 6;
-    const void* fn = d6 ? reinterpret_cast<const void*>(edge_head_bwd_kernel<6>)
-                        : reinterpret_cast<const void*>(edge_head_bwd_kernel<0>);
     if (smem > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(edge_head_bwd_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    if (d6)
-        hipLaunchKernelGGL(edge_head_bwd_kernel<6>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
-                           static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
-    else
-        hipLaunchKernelGGL(edge_head_bwd_kernel<0>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
-                           static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
+    hipLaunchKernelGGL(edge_head_bwd_kernel, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
+                       static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
     return hipGetLastError();
 }
 
