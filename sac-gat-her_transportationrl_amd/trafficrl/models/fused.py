@@ -31,7 +31,7 @@ import torch.nn.functional as F
 
 from .. import _lib
 from .gat_encoder import GATEncoder, GraphCSR, _LoopMean, build_csr, is_regular_batch
-from .tensor_cache import TensorKeyed
+from .tensor_cache import TensorKeyed, pin
 
 
 @dataclass
@@ -503,7 +503,7 @@ def _idx32(t: torch.Tensor) -> torch.Tensor:
         if len(_idx32_cache) > 64:
             _idx32_cache.clear()
         _idx32_cache[key] = r
-    return r
+    return pin(r)
 
 
 def _edge_args(p, c, ea, we, w2, b2, src32, dst32, B: int, n: int, E: int):

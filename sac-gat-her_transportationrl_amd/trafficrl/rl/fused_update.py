@@ -387,7 +387,11 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
         sinks.append(gf)
         o += sz
     g_la = flat[o:o + 1]
-    w = torch.ones(B, device=dev) if weights is None else torch.as_tensor(weights, device=dev).float().reshape(B)
+    if weights is None:
+        w = torch.ones(B, device=dev)
+    else:   # a 0-dim weight applies to every sample, as in sac.py:180-181
+        w = torch.as_tensor(weights, device=dev).float()
+        w = (w.expand(B) if w.dim() == 0 else w.reshape(B)).contiguous()
     sa = _lib.TrxSacLossArgs()
     sa.num_graphs, sa.edges_per_graph = B, E
     npf = nprobs.contiguous()

@@ -39,6 +39,7 @@ import torch
 
 from .data.tntp_parser import load_graph_data, sioux_falls
 from .models import fused
+from .models.tensor_cache import pinning
 from .env.vec_env import VecRepairEnv
 from .rl.replay import DeviceReplay, her_relabel
 from . import _lib
@@ -190,8 +191,11 @@ def capture_graph(fn, pool=None):
     watchdog aborts the rank (seen in tests/test_dist_gpu.py's RCCL test).
     Only this thread's capture-unsafe calls are checked."""
     g = torch.cuda.CUDAGraph(keep_graph=True)
-    with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
+    with pinning() as pins, torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
         out = fn()
+    # cached tensors (topologies, CSR, int32 indices) the captured kernels read
+    # stay alive as long as the graph, whatever the caches evict later
+    g.trx_pins = pins
     _lib.patch_graph_memsets(g)
     g.instantiate()
     return g, out
@@ -394,6 +398,7 @@ class Trainer:
         self._graphed = GraphedUpdate(self) if self.use_graphs else None
         self._graphed_act = GraphedAct(self) if self.use_graphs and cfg.get("graph_act", True) else None
         self._transitions = 0   # env transitions added so far (update schedule)
+        self._due_carry = 0     # world > 1: summed due updates not yet dealt out
 
     # ------------------------------------------------------------ acting
     def act(self, obs, deterministic=False):
@@ -493,8 +498,21 @@ class Trainer:
         due = (self.ep_len % every) == 0
         ms = int(cfg["max_steps"])
         if ms > 0:
-            due &= ~((self.ep_len >= ms) & ~self.env.done)
-        return int(due.sum().item()) * ups
+            # env.done is uint8: ~ on it would be a bitwise not (255/254)
+            due &= ~((self.ep_len >= ms) & ~self.env.done.bool())
+        n = due.sum()
+        if self.world > 1:
+            # every rank must run the same number of updates (each one all-reduces
+            # its gradients): the ranks' due counts are summed and dealt out evenly,
+            # the remainder carried to the next iteration -- the same on every rank
+            import torch.distributed as dist
+            n = n.to(torch.int64).reshape(1)
+            dist.all_reduce(n)
+            self._due_carry += int(n.item()) * ups
+            k = self._due_carry // self.world
+            self._due_carry -= k * self.world
+            return k
+        return int(n.item()) * ups
 
     def prime_update(self):
         """Run the eager warm-up updates and the HIP-graph capture now, so that

@@ -40,18 +40,20 @@ def _fake(B, size, **cfg):
     import torch
     base = dict(batch_start=100, updates_per_step=1, update_every=4, update_unit="transitions", max_steps=0)
     base.update(cfg)
-    return SimpleNamespace(cfg=base, B=B, replay=SimpleNamespace(size=size), _transitions=0,
-                           ep_len=torch.zeros(B, dtype=torch.int64),
-                           env=SimpleNamespace(done=torch.zeros(B, dtype=torch.bool)))
+    # env.done is uint8, as VecRepairEnv keeps it (vec_env.py)
+    return SimpleNamespace(cfg=base, B=B, replay=SimpleNamespace(size=size), _transitions=0, world=1,
+                           _due_carry=0, ep_len=torch.zeros(B, dtype=torch.int64),
+                           env=SimpleNamespace(done=torch.zeros(B, dtype=torch.uint8)))
 
 
 def _episode(f, steps, done_at=None):
+    import torch
     """Drive updates_due through one episode per env (ep_len as trx_episode_step advances it)."""
     out = []
     for it in range(steps):
         f.ep_len += 1
         if done_at is not None:
-            f.env.done = f.ep_len >= done_at
+            f.env.done = (f.ep_len >= done_at).to(torch.uint8)
         out.append(Trainer.updates_due(f, it))
     return out
 
@@ -80,3 +82,48 @@ def test_update_schedule_transitions_follows_reference_episode_counter():
 def test_update_schedule_iterations():
     f = _fake(B=4096, size=10 ** 6, update_unit="iterations", updates_per_step=1, update_every=4)
     assert [Trainer.updates_due(f, it) for it in range(8)] == [1, 0, 0, 0, 1, 0, 0, 0]
+
+
+def _due_worker(rank, world, port, q):
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # uneven episode offsets per rank (random damage: different episode lengths)
+    f = _fake(B=3 + rank, size=1000, max_steps=7)
+    f.world = world
+    f.ep_len[:] = torch.arange(3 + rank) * (1 + rank)
+    got, own = [], 0
+    for it in range(12):
+        f.ep_len += 1
+        f.env.done = ((f.ep_len % (5 + rank)) == 0).to(torch.uint8)
+        due = ((f.ep_len % 4) == 0) & ~((f.ep_len >= 7) & ~f.env.done.bool())
+        own += int(due.sum())
+        got.append(Trainer.updates_due(f, it))
+        f.ep_len[(f.ep_len >= 7) | f.env.done.bool()] = 0
+    q.put((rank, got, own, f._due_carry))
+    dist.destroy_process_group()
+
+
+def test_update_schedule_transitions_world2_lockstep():
+    """world > 1: ranks with different episode states must still run the same
+    number of updates per iteration (each update all-reduces gradients)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_due_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(30)
+    (_, g0, o0, c0), (_, g1, o1, c1) = res
+    assert g0 == g1                                  # lockstep
+    assert o0 != o1                                  # the ranks' own schedules did differ
+    assert 2 * sum(g0) + c0 == o0 + o1 and c0 == c1  # every due update dealt out (carry < world)

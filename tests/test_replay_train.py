@@ -175,6 +175,31 @@ def test_short_training_run(tmp_path):
     assert np.isfinite(ev["tstt_last"])
 
 
+def test_training_run_transition_schedule(tmp_path):
+    """The reference's update schedule (update_unit "transitions", max_steps
+    truncation; sf_sac.yaml) past batch_start: env.done is the env's uint8
+    tensor, the per-env due counts reach the update loop, and the graph
+    capture keeps the topology it reads alive when the caches are cleared."""
+    from trafficrl.models import fused
+    from trafficrl.train import Trainer, batched_topology, sf_config
+    cfg = sf_config()
+    cfg.update(num_envs=16, batch_start=64, batch_size=16, hidden_dim=32, embed_dim=32, episodes=10 ** 6,
+               eval_every=0, output_dir=str(tmp_path), update_unit="transitions", update_every=4, max_steps=6)
+    tr = Trainer(cfg, device="cuda", log=False)
+    assert tr.env.done.dtype == torch.uint8
+    seen = []
+    orig = tr.update
+    tr.update = lambda: (seen.append(1), orig())[1]
+    tr.run(max_iters=14)
+    assert len(seen) > 0 and np.isfinite(float(tr.last_losses["critic_loss"]))
+    # evict every cached topology; the captured acting / update graphs keep theirs
+    fused._topo_cache.clear()
+    for _ in range(70):
+        fused.topology(*batched_topology(tr.env.edge_index, tr.N, 3), 3)
+    tr.run(max_iters=4)
+    assert np.isfinite(float(tr.last_losses["critic_loss"]))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("her,hidden,embed", [(0.0, 32, 32), (0.5, 32, 32), (0.0, 64, 256)])
 def test_graphed_update_matches_eager(tmp_path, her, hidden, embed):
