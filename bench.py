@@ -200,22 +200,35 @@ def lib_sha16():
         return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
-def measured_traffic(network, sha):
+PMC_SUMMARIES = {"sf": "r04_sf_pmc.json", "anaheim": "r04_ana_pmc.json"}
+
+
+def measured_traffic(network, kname):
     """HBM bytes per env-kernel launch and the VALU / LDS-conflict shares from
     the committed rocprofv3 PMC summary of this workload (tools/pmc_summary.py:
-    separate FETCH_SIZE / WRITE_SIZE / SQ passes).  Used only when the summary
-    was captured on the library this process loaded (lib_sha16 match);
+    separate FETCH_SIZE / WRITE_SIZE / SQ passes, one record per kernel and
+    grid).  Used only when the summary's record of this kernel was captured
+    on the same machine code as the kernel this process launches
+    (trafficrl.codeobj.kernel_code_hash of the loaded library: the kernel's
+    code bytes and descriptor), whatever else in the library changed since;
     otherwise (None, reason)."""
-    name = {"sf": "r03_sf_pmc.json", "anaheim": "r03_ana_pmc.json"}[network]
-    path = os.path.join(ROOT, "profiles", name)
+    from trafficrl import _lib, codeobj
+    path = os.path.join(ROOT, "profiles", PMC_SUMMARIES[network])
+    rel = os.path.relpath(path, ROOT)
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
-        return None, f"no PMC summary {os.path.relpath(path, ROOT)}"
-    if d.get("lib_sha16") != sha:
-        return None, (f"{os.path.relpath(path, ROOT)} was captured on libtrafficrl.so {d.get('lib_sha16')}, "
-                      f"this run loaded {sha}: counters omitted")
-    return d, os.path.relpath(path, ROOT)
+        return None, f"no PMC summary {rel}"
+    recs = [r for r in d.get("kernels", {}).values() if r.get("kernel") == kname]
+    if not recs:
+        return None, f"{rel} holds no record of {kname}"
+    # the workload's launches (the passes run the default workload only; bench checks that)
+    rec = max(recs, key=lambda r: max(r["dispatches"].values()))
+    live = codeobj.kernel_code_hash(_lib.LIB_PATH, rec["mangled_key"])
+    if live != rec.get("code_sha16"):
+        return None, (f"{rel} was captured on {kname} code {rec.get('code_sha16')}, this run launches code "
+                      f"{live}: counters omitted")
+    return rec, f"{rel} (kernel code {live})"
 
 
 def env_kernel_name(env, big):
@@ -514,9 +527,8 @@ def main():
     achieved = bpa * B / mean_kernel_s
     kname = env_kernel_name(env, big)
     sha = lib_sha16()
-    pmc, pmc_src = measured_traffic(args.network, sha)
-    if pmc is not None and (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")) \
-            or pmc is not None and pmc.get("kernel", "").split("(")[0] != kname:
+    pmc, pmc_src = measured_traffic(args.network, kname)
+    if pmc is not None and (args.envs, args.iters, args.method) != ((1024, 30, "fw") if big else (4096, 30, "msa")):
         pmc, pmc_src = None, "committed PMC passes cover the default workloads only"
     traffic = pmc.get("hbm_bytes_per_launch_raw") if pmc else None
     valu_frac = pmc.get("valu_busy_frac") if pmc else None
@@ -584,8 +596,8 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": traffic,
-                "traffic_note": (f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {pmc_src} (same libtrafficrl.so "
-                                 f"{sha}; raw; 4-byte loads, gfx950 x2 fetch correction not applied)") if traffic
+                "traffic_note": (f"rocprofv3 FETCH_SIZE+WRITE_SIZE per launch, {pmc_src}; raw: 4-byte loads, "
+                                 f"gfx950 x2 wide-read fetch correction not applied") if traffic
                 else pmc_src,
                 "lib_sha16": sha,
                 "kernel": kname, "kernel_mean_ms": mean_kernel_s * 1e3,

@@ -660,9 +660,10 @@ int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, con
 
 /* ------------------------------------------------ multi-tensor bf16 round
  * dst[k] = bf16(src[k]) for up to TRX_MAX_ROUND row-major blocks in one launch
- * (src rows x cols float32 with row stride src_stride; dst contiguous, bf16
- * bits when out_bf16[k], else the bf16-rounded value as float32).  Used to
- * prepare the small weight blocks of the fused inference passes.           */
+ * (src rows x cols float32 with row stride src_stride; dst contiguous;
+ * out_bf16[k] = 1: bf16 bits, 0: the bf16-rounded value as float32, 2: the
+ * float32 value unrounded -- a plain strided copy).  Used to prepare the
+ * small weight blocks of the fused inference passes.                       */
 #define TRX_MAX_ROUND 16
 typedef struct trx_round_list {
     int32_t count;

@@ -535,7 +535,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
     uint16_t* pr = reinterpret_cast<uint16_t*>(smem);               // [n][2*Hd] bf16
-    float* eal = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);  // [E][ED] bf16-rounded features
+    float* eal = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);  // [E][ED] link features (fp32)
     float* lg = eal + (size_t)E * ED;                                // [E] logits
     float* mk = lg + E;                                              // [E] mask
     int* sl = reinterpret_cast<int*>(mk + E);                        // [E] graph-local src
@@ -585,11 +585,11 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
 #pragma unroll
     for (int j = 0; j < kEaRegs; ++j) {
         const int v = tid + kInferThreads * j;
-        if (v < E * ED) eal[v] = bf16r(eav[j]);
+        if (v < E * ED) eal[v] = eav[j];
     }
     for (int v = tid + kInferThreads * kEaRegs; v < E * ED; v += kInferThreads) {
         const int e = v / ED, j = v - (v / ED) * ED;
-        eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
+        eal[v] = j < D ? a.ea[((int64_t)g * E + e) * D + j] : 0.0f;
     }
     constexpr int DC = DK > 0 ? DK : ED;
     float we_r[MQ][4][DC], w2_r[MQ][4], c_r[MQ][4];
@@ -647,10 +647,10 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
 #pragma unroll
                         for (int j = 0; j < DC; ++j)
                             if (DK > 0 || j < D) ew += ear[j] * we_r[m][r][j];
-                        const float z1 = bf16r(psv[r] + pdv[r]);
-                        const float z2 = bf16r(z1 + bf16r(ew));
-                        const float z3 = z2 + c_r[m][r];
-                        part[u] += bf16r(fmaxf(z3, 0.0f)) * w2_r[m][r];
+                        // fp32 from the bf16 GEMM outputs on: the link's hidden unit and
+                        // its share of the 256 -> 1 product
+                        const float z = ((psv[r] + pdv[r]) + ew) + c_r[m][r];
+                        part[u] += fmaxf(z, 0.0f) * w2_r[m][r];
                     }
                 }
             }
@@ -658,7 +658,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
 #pragma unroll
         for (int u = 0; u < EU; ++u) {
             const float t = wave_sum_f(part[u]);
-            if (lane == 0 && e0 + u < E) lg[e0 + u] = bf16r(t + b2);
+            if (lane == 0 && e0 + u < E) lg[e0 + u] = t + b2;
         }
     }
     __syncthreads();
@@ -910,21 +910,21 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 // ------------------------------------------------ edge scorer, backward
 // Training-path backward of the edge scorer (the logits of edge_head_infer
 // with softmax = 0), one workgroup per graph, thread k = hidden unit k
-// (hidden <= 256).  The forward is recomputed from the LDS-staged p rows; the
-// bf16 roundings are those of the autocast torch path: the incoming logit
-// gradient and d relu = bf16(g * w2) are bf16, relu backward on the fp32 z,
-// the gradient reaching the bf16 sum of the gathers and the link term is
-// rounded to bf16 (grad_z), p gradients are fp32 sums over the graph's links
-// (fixed link order) rounded to bf16 at the end.  Two passes, no LDS
-// read-modify-write chains, and four threads per hidden unit (1024 per graph:
-// the update's 256 graphs are one workgroup per CU): (1) per link (links
-// dealt to the four parts), thread k's gradient through unit k, stored bf16
-// in LDS (it is bf16-rounded anyway), with per-part grad_c / grad_w2 sums
-// added in part order; (2) per node (nodes dealt to the parts), the sums over
-// its out-links (p[:, :H]) and in-links (p[:, H:]) in link order.
+// (hidden <= 256).  The forward is recomputed from the LDS-staged p rows.
+// Everything after the bf16 p GEMM is fp32 (as in the forward): the incoming
+// logit gradient g, dz = g * w2 behind the ReLU, the per-graph sums of dz
+// (grad_c) and of g * relu(z) (grad_w2), and the p gradients as fp32 sums
+// over the graph's links in a fixed link order, rounded to bf16 once (they
+// feed the bf16 GEMM backward).  Two passes, no LDS read-modify-write chains,
+// and four threads per hidden unit (1024 per graph: the update's 256 graphs
+// are one workgroup per CU): (1) per link (links dealt to the four parts),
+// thread k's gradient through unit k, kept fp32 in LDS, with per-part
+// grad_c / grad_w2 sums added in part order; (2) per node (nodes dealt to the
+// parts), the sums over its out-links (p[:, :H]) and in-links (p[:, H:]) in
+// link order.
 // Outputs: grad_p [N, 2H] bf16, grad_c [B, H], grad_z [E_total, H] bf16 (for
-// the link-feature weight / input gradients, GEMMs on the host side) and
-// grad_w2_part [B, H] (per-graph sums of bf16(g) * bf16(relu(z))).
+// the link-feature weight / input gradients, bf16 GEMMs on the host side) and
+// grad_w2_part [B, H] (per-graph sums of g * relu(z)).
 constexpr int kEhbThreads = 1024, kEhbParts = kEhbThreads / 256;
 
 __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
@@ -935,9 +935,9 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
     const int g = blockIdx.x, tid = threadIdx.x, k = tid & 255, part = tid >> 8;
     const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
     uint16_t* pr = reinterpret_cast<uint16_t*>(smem);                   // [n][2*Hd] bf16
-    uint16_t* dzs = pr + (size_t)n * 2 * Hd;                            // [E][Hd] bf16 dL/dz
-    float* eal = reinterpret_cast<float*>(dzs + (size_t)E * Hd + ((E * Hd) & 1));  // [E][ED] link features
-    float* gl = eal + (size_t)E * ED;                                   // [E] bf16(grad logit)
+    float* dzs = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);     // [E][Hd] dL/dz (n*2*Hd even)
+    float* eal = dzs + (size_t)E * Hd;                                  // [E][ED] link features
+    float* gl = eal + (size_t)E * ED;                                   // [E] grad logit
     float* red = gl + E;                                                // [P][2][256] per-part sums
     int* sl = reinterpret_cast<int*>(red + P * 2 * 256);                // [E]
     int* dl = sl + E;                                                   // [E]
@@ -958,11 +958,11 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
         d = d < 0 ? 0 : (d >= n ? n - 1 : d);
         sl[e] = s;
         dl[e] = d;
-        gl[e] = bf16r(grad_logits[eg]);
+        gl[e] = grad_logits[eg];
     }
     for (int v = tid; v < E * ED; v += NT) {
         const int e = v / ED, j = v - (v / ED) * ED;
-        eal[v] = j < D ? bf16r(a.ea[((int64_t)g * E + e) * D + j]) : 0.0f;
+        eal[v] = j < D ? a.ea[((int64_t)g * E + e) * D + j] : 0.0f;
     }
     const bool on = k < Hd;
     float we[ED];
@@ -1002,16 +1002,13 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
 #pragma unroll
             for (int j = 0; j < ED; ++j)
                 if (j < D) ew += eal[e * ED + j] * we[j];
-            const float z1 = bf16r(bf2f(pr[s * 2 * Hd + k]) + bf2f(pr[d * 2 * Hd + Hd + k]));
-            const float z2 = bf16r(z1 + bf16r(ew));
-            const float z3 = z2 + ck;
+            const float z = ((bf2f(pr[s * 2 * Hd + k]) + bf2f(pr[d * 2 * Hd + Hd + k])) + ew) + ck;
             const float gb = gl[e];
-            gw2 += gb * bf16r(fmaxf(z3, 0.0f));
-            const float dz = z3 > 0.0f ? bf16r(gb * w2) : 0.0f;
+            gw2 += gb * fmaxf(z, 0.0f);
+            const float dz = z > 0.0f ? gb * w2 : 0.0f;
             gc += dz;
-            const uint16_t dzz = f2bf(bf16r(dz));
-            grad_z[((int64_t)g * E + e) * Hd + k] = dzz;
-            dzs[e * Hd + k] = dzz;
+            grad_z[((int64_t)g * E + e) * Hd + k] = f2bf(dz);
+            dzs[e * Hd + k] = dz;
         }
     }
     red[(part * 2 + 0) * 256 + k] = gc;
@@ -1030,8 +1027,8 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
     if (on)  // (2) per node: out-links feed p[:, :H], in-links p[:, H:]
         for (int i = part; i < n; i += P) {
             float so = 0.0f, si = 0.0f;
-            for (int q = op[i]; q < op[i + 1]; ++q) so += bf2f(dzs[lo[q] * Hd + k]);
-            for (int q = ip[i]; q < ip[i + 1]; ++q) si += bf2f(dzs[li[q] * Hd + k]);
+            for (int q = op[i]; q < op[i + 1]; ++q) so += dzs[lo[q] * Hd + k];
+            for (int q = ip[i]; q < ip[i + 1]; ++q) si += dzs[li[q] * Hd + k];
             grad_p[(node0 + i) * 2 * Hd + k] = f2bf(so);
             grad_p[(node0 + i) * 2 * Hd + Hd + k] = f2bf(si);
         }
@@ -1039,8 +1036,7 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
 
 size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
     const size_t n = a.nodes_per_graph, E = a.edges_per_graph, H = a.hidden;
-    return n * 2 * H * 2 + (E * H + ((E * H) & 1)) * 2 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * 2 * 256 * 4 +
-           2 * (n + 1) * 4;
+    return n * 2 * H * 2 + E * H * 4 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * 2 * 256 * 4 + 2 * (n + 1) * 4;
 }
 
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,

@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
     float* const lgs = reinterpret_cast<float*>(smem + O.lg);
     float* const mks = reinterpret_cast<float*>(smem + O.mk);
     int* const bad = reinterpret_cast<int*>(smem + O.bad);
-    float* const eal = reinterpret_cast<float*>(smem + O.eal);   // [kTG][E][kTED] bf16-rounded link features
+    float* const eal = reinterpret_cast<float*>(smem + O.eal);   // [kTG][E][kTED] link features (fp32)
     int* const lsd = reinterpret_cast<int*>(smem + O.lsd);       // [kTG][E][2] workgroup-local endpoints
     float* const tsum = reinterpret_cast<float*>(smem + O.tsum); // [kTG][E][4] 64-unit row sums
 
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
         lsd[2 * v] = okl ? gl * n + (int)s : 0;
         lsd[2 * v + 1] = okl ? gl * n + (int)d : 0;
 #pragma unroll
-        for (int j = 0; j < kTED; ++j) eal[kTED * v + j] = j < D ? bfr(a.ea[eg * D + j]) : 0.0f;
+        for (int j = 0; j < kTED; ++j) eal[kTED * v + j] = j < D ? a.ea[eg * D + j] : 0.0f;
     }
 
     TRX_TSTAMP(0);
@@ -627,10 +627,8 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
 #pragma unroll
                     for (int j = 0; j < kTED; ++j)
                         if (j < D) ew += ear[j] * we_r[r][j];
-                    const float z1 = bfr(psv[r] + pdv[r]);
-                    const float z2 = bfr(z1 + bfr(ew));
-                    const float z3 = z2 + c_r[r];
-                    part += bfr(fmaxf(z3, 0.0f)) * w2_r[r];
+                    const float z = ((psv[r] + pdv[r]) + ew) + c_r[r];   // fp32 after the p GEMM
+                    part += fmaxf(z, 0.0f) * w2_r[r];
                 }
                 part = t_row_sum16(part);
                 if (sl == 0 && e < E) tsum[4 * v + b] = part;
@@ -640,7 +638,7 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
     __syncthreads();
     for (int v = tid; v < G * E; v += kTThreads) {
         const float4 t = *reinterpret_cast<const float4*>(tsum + 4 * v);
-        lgs[v] = bfr(((t.x + t.y) + (t.z + t.w)) + a.b2[0]);
+        lgs[v] = ((t.x + t.y) + (t.z + t.w)) + a.b2[0];
     }
     __syncthreads();
 

@@ -78,7 +78,8 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     const uint32_t cols = (uint32_t)l.cols[k], n = (uint32_t)(l.rows[k] * l.cols[k]);
     const float* src = l.src[k];
     const int64_t ss = l.src_stride[k];
-    const bool bf = l.out_bf16[k] != 0;
+    const int mode = l.out_bf16[k];  // 0 bf16-rounded float32, 1 bf16 bits, 2 exact float32 copy
+    const bool bf = mode == 1;
     const uint32_t step = gridDim.x * 256u;
     if ((cols & 3u) == 0 && (ss & 3) == 0 && ((uintptr_t)src & 15) == 0) {
         for (uint32_t q = blockIdx.x * 256u + threadIdx.x; 4 * q < n; q += step) {
@@ -90,6 +91,8 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
                 u.x = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
                 u.y = (uint32_t)__builtin_bit_cast(uint16_t, h2) | ((uint32_t)__builtin_bit_cast(uint16_t, h3) << 16);
                 *reinterpret_cast<uint2*>(static_cast<uint16_t*>(l.dst[k]) + i) = u;
+            } else if (mode == 2) {
+                *reinterpret_cast<float4*>(static_cast<float*>(l.dst[k]) + i) = v;
             } else {
                 *reinterpret_cast<float4*>(static_cast<float*>(l.dst[k]) + i) =
                     make_float4((float)h0, (float)h1, (float)h2, (float)h3);
@@ -99,11 +102,12 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     }
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += step) {
         const uint32_t r = i / cols, c = i - r * cols;
-        const __bf16 h = (__bf16)src[r * ss + c];
+        const float x = src[r * ss + c];
+        const __bf16 h = (__bf16)x;
         if (bf)
             static_cast<uint16_t*>(l.dst[k])[i] = __builtin_bit_cast(uint16_t, h);
         else
-            static_cast<float*>(l.dst[k])[i] = (float)h;
+            static_cast<float*>(l.dst[k])[i] = mode == 2 ? x : (float)h;
     }
 }
 }  // namespace

@@ -129,16 +129,19 @@ _STATIC = [False]
 def _round_into(pairs):
     """One trx_bf16_round launch: for each (src float32 2-D/1-D view with unit
     column stride, dst contiguous float32 or bfloat16 tensor of the same
-    shape) write bf16(src) (as bf16 bits, or rounded float32)."""
+    shape[, exact]) write bf16(src) (as bf16 bits, or rounded float32), or with
+    exact=True the float32 value itself (a strided copy)."""
     L = _lib.load()
     lst = _lib.TrxRoundList()
     lst.count = len(pairs)
     dev = None
-    for k, (src, dst) in enumerate(pairs):
-        src = src.detach()
+    for k, item in enumerate(pairs):
+        src, dst = item[0].detach(), item[1]
+        exact = len(item) > 2 and item[2]
         src2 = src.reshape(1, -1) if src.dim() == 1 else src
         assert src2.dtype == torch.float32 and src2.stride(1) == 1 and dst.is_contiguous()
-        lst.out_bf16[k] = int(dst.dtype == torch.bfloat16)
+        assert not (exact and dst.dtype == torch.bfloat16)
+        lst.out_bf16[k] = 1 if dst.dtype == torch.bfloat16 else (2 if exact else 0)
         lst.rows[k], lst.cols[k] = src2.shape
         lst.src_stride[k] = src2.stride(0)
         lst.src[k], lst.dst[k] = src2.data_ptr(), dst.data_ptr()
@@ -224,8 +227,9 @@ def _encoder_weights(enc, layers, into=None):
 
 
 def _head_weights(head, into=None):
-    """(w_nodes bf16 [2H, d], W_ctx^T bf16 view, we, w2, b2 bf16-rounded
-    float32): one launch (into `into` when given)."""
+    """(w_nodes bf16 [2H, d], W_ctx^T bf16 view; we, w2, b2 float32 as they
+    are: the link-feature term and the 256 -> 1 product run in fp32 in the
+    kernels): one launch (into `into` when given)."""
     W1, b1 = head.edge_mlp[0].weight, head.edge_mlp[0].bias
     d, k = head.embed, head.edge_in
     hid = W1.shape[0]
@@ -240,8 +244,8 @@ def _head_weights(head, into=None):
         wn, wct, we, w2, b2 = into
         wc = wct.t()
     _round_into([(W1[:, :d], wn[:hid]), (W1[:, d:2 * d], wn[hid:]), (W1[:, 2 * d + k:], wc),
-                 (W1[:, 2 * d:2 * d + k], we), (head.edge_mlp[2].weight.reshape(-1), w2),
-                 (head.edge_mlp[2].bias.reshape(-1), b2)])
+                 (W1[:, 2 * d:2 * d + k], we, True), (head.edge_mlp[2].weight.reshape(-1), w2, True),
+                 (head.edge_mlp[2].bias.reshape(-1), b2, True)])
     return wn, wc.t(), we, w2, b2
 
 
@@ -520,8 +524,8 @@ class _EdgeScores(torch.autograd.Function):
     """Training-path edge scorer logits (the factored edge MLP of
     _EdgeHead.edge_scores for a regular batch): forward = the inference
     kernel with softmax off, backward = trx_edge_head_backward plus two
-    products for the link-feature block.  Same bf16 rounding points as the
-    autocast torch path."""
+    products for the link-feature block.  Same rounding points as
+    _EdgeHead.edge_scores' general path: bf16 p GEMM, fp32 from there on."""
 
     @staticmethod
     def forward(ctx, p, c, ea, W1e, W2, b2, src, dst, B: int, n: int):
@@ -530,7 +534,8 @@ class _EdgeScores(torch.autograd.Function):
         p = p.to(torch.bfloat16).contiguous()
         c = c.float().contiguous()
         eaf = ea.float().contiguous()
-        we, w2, b2r = _bf16r(W1e), _bf16r(W2.reshape(-1)), _bf16r(b2.reshape(-1))
+        we, w2, b2r = (W1e.detach().float().contiguous(), W2.detach().float().reshape(-1).contiguous(),
+                       b2.detach().float().reshape(-1).contiguous())
         src32, dst32 = _idx32(src), _idx32(dst)
         out = torch.empty(B * E, device=p.device, dtype=torch.float32)
         a = _edge_args(p, c, eaf, we, w2, b2r, src32, dst32, B, n, E)
@@ -558,7 +563,7 @@ class _EdgeScores(torch.autograd.Function):
         g_ea = (grad_z @ we.to(torch.bfloat16)).float()                     # skinny_linear's dx (bf16 GEMM)
         g_we = _splitk_wgrad(grad_z, ea.to(torch.bfloat16))                  # and its split-K fp32 dW
         g_w2 = gw2.sum(0).view(1, H)
-        g_b2 = g.to(torch.bfloat16).sum(0, dtype=torch.float32).view(1)
+        g_b2 = g.sum(0).view(1)
         return grad_p, grad_c, g_ea, g_we, g_w2, g_b2, None, None, None, None
 
 

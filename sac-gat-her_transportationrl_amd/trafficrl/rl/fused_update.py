@@ -234,7 +234,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         _lib.check(L.trx_partial_sum(_lib.ptr(src), B, Hd, Hd, _lib.ptr(dst), stream), "trx_partial_sum")
         _grad(prm, dst)
     gb2 = sink.take(1)
-    torch.sum(gl.to(torch.bfloat16), 0, keepdim=True, dtype=torch.float32, out=gb2)
+    torch.sum(gl, 0, keepdim=True, out=gb2)
     _grad(net.edge_mlp[2].bias, gb2)
     # ---- GAT layers, last to first
     a_all = cx.a_all

@@ -247,16 +247,24 @@ class _EdgeHead(nn.Module):
             # one kernel each way for the gathers, link term, context, ReLU and 256->1 product
             B = regular[0]
             return fused.edge_scores_train(p, c, edge_attr, w_e, W2, b2, src, dst, B, node_emb.shape[0] // B)
-        if regular is not None:
-            B, src_l, dst_l = regular
-            z = regular_gather(p[:, :hdim], src_l, B) + regular_gather(p[:, hdim:], dst_l, B)
-            z = z + skinny_linear(edge_attr, w_e)
-            z = z + c.unsqueeze(1).expand(B, src_l.numel(), hdim).reshape(-1, hdim)
-        else:
-            z = p[src, :hdim] + p[dst, hdim:]
-            z = z + skinny_linear(edge_attr, w_e)
-            z = z + c[edge_batch]
-        return skinny_linear(torch.relu(z), W2, b2).squeeze(-1)
+        # fp32 from the per-node GEMM's output on (the fused kernels' rounding
+        # points): the link's hidden units and the 256 -> 1 product.  Under bf16
+        # autocast the logits keep fp32 resolution (a graph's logits differ by
+        # ~1e-2 while bf16 resolves ~1e-3 at their magnitude)
+        up = lambda t: t.float() if t.dtype in (torch.bfloat16, torch.float16) else t  # noqa: E731
+        pf, c = up(p), up(c)
+        with torch.autocast("cuda", enabled=False):
+            ew = skinny_linear(up(edge_attr), w_e)
+            if regular is not None:
+                B, src_l, dst_l = regular
+                z = regular_gather(pf[:, :hdim], src_l, B) + regular_gather(pf[:, hdim:], dst_l, B)
+                z = z + ew
+                z = z + c.unsqueeze(1).expand(B, src_l.numel(), hdim).reshape(-1, hdim)
+            else:
+                z = pf[src, :hdim] + pf[dst, hdim:]
+                z = z + ew
+                z = z + c[edge_batch]
+            return skinny_linear(torch.relu(z), W2, b2).squeeze(-1)
 
 
 class Actor(_EdgeHead):

@@ -88,11 +88,13 @@ def _autograd_grads(agent, batch, w):
 
 
 def test_fused_update_vs_fp32_restatement():
-    """At the bench's sizes the bf16 actor gradient is ~9 % off the fp32 one
-    on BOTH bf16 paths: at random init a graph's logits span ~1e-2 while bf16
-    rounds logits of ~0.3 to ~1e-3, and the actor's gradient is made of the
-    centred logits (softmax backward).  So: critics within 6e-2 of fp32, the
-    actor within 1.2 x the autograd path's own error + 1e-2, losses 6e-2."""
+    """Absolute bounds against the fp32 restatement: actor gradients within
+    3e-2 per tensor, critics within 6e-2, losses within 6e-2.  The actor's
+    gradient is made of the centred logits (softmax backward) and a graph's
+    logits span only ~1e-2 at random init, so the edge scorer computes in
+    fp32 after its bf16 node-projection GEMM (round 3 rounded the hidden
+    units and the logits to bf16, ~1e-3 at their magnitude: 9 % actor error
+    on both bf16 paths)."""
     B = 256
     batch = _update_batch(B)
     agent = make_agent(hidden=256, embed=256)
@@ -107,7 +109,7 @@ def test_fused_update_vs_fp32_restatement():
         wf = _worst({k: got[k] for k in sub}, sub)
         wa = _worst({k: auto[k] for k in sub}, sub)
         print(f"{m}: fused {wf}, autograd {wa} (relative to fp32)")
-        assert wf[0] < (6e-2 if m != "actor" else 1.2 * wa[0] + 1e-2), (m, wf, wa)
+        assert wf[0] < (6e-2 if m != "actor" else 3e-2), (m, wf, wa)
     assert abs(got_alpha - ref_alpha) <= 6e-2 * max(1e-6, abs(ref_alpha))
     for k, r in zip(("critic_loss", "actor_loss", "alpha_loss"), losses):
         assert abs(float(out[k]) - r) <= 6e-2 * max(1e-3, abs(r)), (k, float(out[k]), r)
@@ -154,8 +156,9 @@ def test_fused_update_trajectory():
     (x 1.2 + 2e-2), and the two bf16 runs are no further apart than the
     autograd run is from fp32: Adam turns bf16 gradient noise into
     full-size sign-driven steps on small-gradient weights, so bf16 runs part
-    along the way (measured fused-autograd / autograd-fp32: actor 0.31 /
-    0.41, critic2 0.063 / 0.14).  Losses of every step within 6e-2 of fp32."""
+    along the way.  Absolute: every module's fused run within 0.15 of the
+    distance travelled from the fp32 run.  Losses of every step within 6e-2
+    of fp32."""
     from trafficrl.rl import sac
     B = 256
     batch = _update_batch(B)
@@ -187,3 +190,4 @@ def test_fused_update_trajectory():
         print(f"{m}: drift fused-autograd {dfa:.4f}, fused-fp32 {dfr:.4f}, autograd-fp32 {dar:.4f}")
         assert dfa <= dar, (m, dfa, dar)
         assert dfr <= 1.2 * dar + 2e-2, (m, dfr, dar)
+        assert dfr <= 0.15, (m, dfr)

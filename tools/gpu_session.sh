@@ -17,6 +17,18 @@ step() {  # step <name> <timeout-seconds> <cmd...>
     if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
     return 0
 }
+# four rocprofv3 --pmc passes (each within gfx950's per-pass slots: 8 SQ, 4 TCC, 2 GRBM)
+PMC_SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
+          "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
+          "FETCH_SIZE" "WRITE_SIZE")
+pmc4() {  # pmc4 <name> <cmd...>: passes gpurun_out/<name>_p1..p4
+    local name=$1; shift
+    local k=1
+    for set in "${PMC_SETS[@]}"; do
+        step ${name}_p$k 300 rocprofv3 --pmc $set --kernel-trace -d gpurun_out/${name}_p$k -o run --output-format csv -- "$@" || return 1
+        k=$((k + 1))
+    done
+}
 for s in "$@"; do
     case $s in
         tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
@@ -46,6 +58,9 @@ for s in "$@"; do
              step pmc2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc2 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu
              step pmc3 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc3 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu
              step pmc4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc4 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu ;;
+        pmcenv) pmc4 pmcenv python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu ;;
+        pmcact) pmc4 pmcact python3 tools/agent_profile.py 4096 act ;;
+        pmcupd) pmc4 pmcupd python3 tools/agent_profile.py 4096 update ;;
         stamps) step stamps 300 python tools/phase_stamps.py 4096 ;;
         epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --workload env --steps 44 --warmup 22 --no-cpu; done ;;
         gattests) step gat_tests 400 python -m pytest tests/test_gat_infer.py tests/test_gat.py tests/test_sac.py -x -q ;;
