@@ -404,7 +404,8 @@ def main():
     gd = load_network(args.network)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     observe = not args.no_observe
-    ev_pairs = []      # env_kernel launches (HIP events on the launch stream)
+    ev_pairs = []      # env_kernel step launches (HIP events on the launch stream)
+    reset_ev = []      # env_kernel reset launches (whole-batch cold resets, once per episode)
     phase_ev = {}      # per-phase events (train workload)
 
     def timed(fn, bucket):
@@ -442,7 +443,7 @@ def main():
         st = {"obs": env.observe(), "it": 0, "t": 0}
 
         def reset():
-            timed(lambda: env.reset_where(all_true, dmg_all), ev_pairs)
+            timed(lambda: env.reset_where(all_true, dmg_all), reset_ev)
             st["obs"] = env.observe()
             st["t"] = 0
             for acc in (tr.ep_reward, tr.ep_tstt_sum, tr.ep_auc, tr.ep_len):
@@ -466,10 +467,16 @@ def main():
         ep_len = int(dmg0.sum().item())     # max(1, int(E * 0.3)) damaged links either way
         st = {"t": 0}
 
+        if dmg_all is None:
+            # random damage: every env's next mask is drawn on a host thread while the
+            # device steps the current episode (pinned, copied asynchronously at reset)
+            env.enable_damage_prefetch(True)
+
         def reset():
-            # random: the host draws (one native call for all envs) stay outside the kernel events
-            dm = env.draw_damage() if dmg_all is None else dmg_all
-            timed(lambda: env.reset(damaged=dm, observe=False), ev_pairs)
+            if dmg_all is None:
+                timed(lambda: env.reset(observe=False), reset_ev)
+            else:
+                timed(lambda: env.reset(damaged=dmg_all, observe=False), reset_ev)
             if observe:
                 env.observe()
             st["t"] = 0
@@ -497,6 +504,7 @@ def main():
     if dist:
         dist.barrier()
     ev_pairs.clear()
+    reset_ev.clear()
     for v in phase_ev.values():
         v.clear()
     torch.cuda.synchronize()
@@ -509,7 +517,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     breakdown = {k: float(np.sum([s_.elapsed_time(e_) for s_, e_ in v])) / args.steps for k, v in phase_ev.items()}
-    kern_ms = [s.elapsed_time(e) for s, e in ev_pairs]
+    step_ms = [s.elapsed_time(e) for s, e in ev_pairs]
+    reset_ms = [s.elapsed_time(e) for s, e in reset_ev]
+    kern_ms = step_ms + reset_ms     # every assignment launch of the timed region
     mean_kernel_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -610,7 +620,14 @@ def main():
                 "mfma": mfma,
             },
             "cpu_baseline": cpu,
-            "breakdown_ms_per_step": dict(breakdown, env_kernel=mean_kernel_s * 1e3 * len(kern_ms) / args.steps),
+            "breakdown_ms_per_step": dict(breakdown, env_kernel=float(np.sum(kern_ms)) / args.steps,
+                                          env_step_kernel=float(np.sum(step_ms)) / args.steps,
+                                          env_reset_kernel=float(np.sum(reset_ms)) / args.steps),
+            "env_launches": {"step_mean_ms": float(np.mean(step_ms)) if step_ms else None,
+                             "reset_mean_ms": float(np.mean(reset_ms)) if reset_ms else None,
+                             "resets_timed": len(reset_ms), "steps_timed": len(step_ms),
+                             "note": "HIP events around trx_step / trx_reset (the reset's events include the "
+                                     "asynchronous copy of the prefetched damage masks when damage is random)"},
         }
         if args.workload == "train" and upd_stats is not None:
             out["sac_update"] = upd_stats

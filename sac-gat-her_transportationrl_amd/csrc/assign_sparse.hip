@@ -82,7 +82,8 @@ constexpr int kQs = 4;
 // the relaxation's atomic min):
 //   reached, unscanned: bits(label) | id -- a positive double, ordered by (label, id)
 //   unreached:          0x7FF8000000000000 | id -- a quiet NaN, the largest positive integer
-//   scanned:            high word 0xFFF80000, low word kept -- a quiet NaN, a negative integer
+//   scanned:            high word 0xFFF80000, low word = the scan step at which the node's
+//                       equal-label run began -- a quiet NaN, a negative integer
 //   padding node:       all ones -- a quiet NaN, a negative integer
 // v_min_f64 (IEEE minNum) ignores quiet NaNs, so the argmin sees only reached,
 // unscanned nodes; the signed min never improves a scanned key.
@@ -378,6 +379,11 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             wave_sync_s();
             int nscan = 0;
             int amb = 0;
+            // equal-label runs of the scan order: labels come out non-decreasing, so two
+            // scanned nodes have equal labels iff they belong to the same run (run = the
+            // scan step at which the run began, stored in the scanned key's low word)
+            int run = 0;
+            uint64_t prev_lb = ~0ull;
             uint64_t m[NPL];
             read_keys<NPL>(kt + NPL * j, m);
             for (int k = 0; k < N; ++k) {
@@ -394,13 +400,17 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                 if (!(bd < kInfD)) break;  // quad-uniform: the rest is unreachable (NaN or +inf: all ignored)
                 const uint64_t best = dbits_s(bd);
                 const uint32_t u = (uint32_t)best & 31u;
-                // one lane of the quad stores the scan order and the scanned mark
+                const uint64_t lb = best & ~31ull;
+                if (lb != prev_lb) {  // quad-uniform
+                    run = k;
+                    prev_lb = lb;
+                }
+                // one lane of the quad stores the scan order and the scanned mark (+ run)
                 if (j == 0) {
                     ol[k] = (uint8_t)u;
-                    kt32[2 * u + 1] = kScannedHi;
+                    kt[u] = ((uint64_t)kScannedHi << 32) | (uint32_t)run;
                 }
                 nscan = k + 1;
-                const uint64_t lb = best & ~31ull;
                 const double bl = bitsd_s(lb);
                 uint32_t v[R];
                 float c[R];
@@ -442,12 +452,12 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     // scipy's strict improvement: u becomes v's predecessor.  An equal key
-                    // means v already holds this label from the tail pl[v]; scipy's order
-                    // between the two is its heap's iff the tails' labels are equal.
+                    // means v already holds this label from the tail pl[v] (scanned before
+                    // u); scipy's order between the two is its heap's iff the tails' labels
+                    // are equal, i.e. iff pl[v] is in u's equal-label run (exact: no false
+                    // positives, so warm-started steps never replay on integral labels)
                     if (nk[r] < was[r]) pl[v[r]] = (uint8_t)u;
-                    // (scanned keys keep their low word: equal low label bits = maybe equal
-                    // labels; a false positive costs one exact replay, never a wrong tree)
-                    if (nk[r] == was[r]) amb |= ((kt32[2 * pl[v[r]]] ^ (uint32_t)lb) & ~31u) == 0u;
+                    if (nk[r] == was[r]) amb |= kt32[2 * pl[v[r]]] == (uint32_t)run;
                 }
             }
             wave_sync_s();

@@ -146,8 +146,26 @@ class VecRepairEnv:
         self._fixed = (fixed_damage, fixed_damage_seed)
         self._samplers = None
         self._rng_states = None   # PCG64 records of default_rng(seed_b), the non-fixed reset path
+        self._prefetch = None     # DamagePrefetch (enable_damage_prefetch)
         if reset:
             self.reset()
+
+    def enable_damage_prefetch(self, on: bool = True):
+        """Draw every env's NEXT damage mask on a host thread while the device
+        runs the current episode (native trx_damage_sample, GIL released),
+        into pinned memory, so a whole-batch reset costs an asynchronous copy
+        instead of a blocking host draw.  The masks and the generator states
+        are exactly those of drawing at reset time: a prefetched draw is
+        committed only when all envs reset together; any other reset discards
+        it and draws synchronously from the envs' true states."""
+        if self._prefetch is not None:
+            self._prefetch.close()
+            self._prefetch = None
+        if on and not self._fixed[0] and self._samplers is None and self.num_edges <= 10000:
+            if self._rng_states is None:
+                self._rng_states = pcg_states(self._seeds)
+            self._prefetch = DamagePrefetch(self)
+        return self._prefetch is not None
 
     @property
     def samplers(self):
@@ -198,7 +216,9 @@ class VecRepairEnv:
         ids = list(range(B)) if env_ids is None else [int(i) for i in (env_ids.tolist() if torch.is_tensor(env_ids)
                                                                        else env_ids)]
         if damaged is None:
-            damaged = self.draw_damage(ids, ratio)
+            damaged = self._take_prefetched(ids, ratio)
+            if damaged is None:
+                damaged = self.draw_damage(ids, ratio)
         damaged = damaged.to(device=self.device, dtype=torch.float32)
         env_mask = None
         if env_ids is None:
@@ -218,6 +238,9 @@ class VecRepairEnv:
         (default all) from their own RNG streams, as RepairEnv.reset draws them."""
         ratio = self.damaged_ratio if damaged_ratio is None else damaged_ratio
         ids = list(range(self.num_envs)) if ids is None else ids
+        got = self._take_prefetched(ids, ratio)
+        if got is not None:
+            return got.cpu()
         # numpy's choice for E > 10000 links is not the Floyd draw the native sampler
         # restates (trx_damage_sample's limit): those graphs take the numpy samplers,
         # which continue the same per-env streams
@@ -230,7 +253,26 @@ class VecRepairEnv:
             st = np.ascontiguousarray(self._rng_states[sel])
             masks = damage_sample_batch(self.num_nodes, self.graph.src, self.graph.dst, st, ratio)
             self._rng_states[sel] = st
+            if self._prefetch is not None:
+                self._prefetch.restart(ratio)   # from the advanced states
         return torch.from_numpy(masks)
+
+    def _take_prefetched(self, ids, ratio) -> Optional[torch.Tensor]:
+        """The prefetched masks already on the device (an asynchronous copy
+        from pinned memory) when every env resets at once; else None and the
+        prefetch is dropped (the caller draws from the envs' true states)."""
+        pf = self._prefetch
+        if pf is None:
+            return None
+        if self._fixed[0] or self._samplers is not None:   # the RNG record moved to the samplers
+            self.enable_damage_prefetch(False)
+            return None
+        return pf.take(ids, ratio)
+
+    def close(self):
+        if self._prefetch is not None:
+            self._prefetch.close()
+            self._prefetch = None
 
     def reset_where(self, env_mask: torch.Tensor, damaged: torch.Tensor, observe: bool = False):
         """Reset the envs where env_mask (bool/uint8 [B]) is set, with damage
@@ -332,3 +374,62 @@ class VecRepairEnv:
 
     def is_goal_complete(self) -> torch.Tensor:
         return (self.goal * self.damaged).sum(dim=1) == 0
+
+
+
+class DamagePrefetch:
+    """Background draw of every env's next damage mask (VecRepairEnv.
+    enable_damage_prefetch): one host thread, two pinned buffers.  The draw
+    for the next whole-batch reset runs while the current episode steps; a
+    buffer is rewritten only after the device copy that read it completed
+    (its HIP event, waited on by the worker thread)."""
+
+    def __init__(self, env: "VecRepairEnv"):
+        from concurrent.futures import ThreadPoolExecutor
+        self.env = env
+        B, E = env.num_envs, env.num_edges
+        self.bufs = [torch.empty(B, E, dtype=torch.float32).pin_memory() for _ in range(2)]
+        self.copied = [None, None]   # HIP event of the last device copy out of each buffer
+        self.which = 0
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="trx-damage")
+        self.job = None
+        self.restart(env.damaged_ratio)
+
+    def restart(self, ratio):
+        """(Re)start the draw of the next masks from the envs' current states."""
+        if self.job is not None:
+            self.job[2].result()     # never two draws into one buffer
+        env, k = self.env, self.which
+        states = np.ascontiguousarray(env._rng_states).copy()
+        ev = self.copied[k]
+        buf = self.bufs[k].numpy()
+
+        def work():
+            if ev is not None:
+                ev.synchronize()     # the previous copy out of this buffer has finished
+            damage_sample_batch(env.num_nodes, env.graph.src, env.graph.dst, states, ratio, out=buf)
+            return states
+
+        self.job = (k, ratio, self.pool.submit(work))
+
+    def take(self, ids, ratio) -> Optional[torch.Tensor]:
+        env = self.env
+        k, r, fut = self.job
+        states = fut.result()
+        if r != ratio or len(ids) != env.num_envs or list(ids) != list(range(env.num_envs)):
+            return None              # not committed: the caller's synchronous draw restarts us
+        env._rng_states[:] = states
+        dev = self.bufs[k].to(env.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.copied[k] = ev
+        self.which = 1 - k
+        self.job = None
+        self.restart(ratio)
+        return dev
+
+    def close(self):
+        if self.job is not None:
+            self.job[2].result()
+            self.job = None
+        self.pool.shutdown(wait=True)

@@ -117,10 +117,11 @@ def set_generator_state(rng: np.random.Generator, rec) -> None:
 
 
 def damage_sample_batch(num_nodes: int, src: np.ndarray, dst: np.ndarray, states: np.ndarray,
-                        damaged_ratio: float = 0.3, nthreads: int = 0) -> np.ndarray:
+                        damaged_ratio: float = 0.3, nthreads: int = 0, out: np.ndarray = None) -> np.ndarray:
     """RepairEnv.reset's damage draw for len(states) envs in one native call
-    (trx_damage_sample): float32 masks [n, E]; `states` (PCG64_DTYPE) advance
-    in place exactly as each env's numpy Generator would."""
+    (trx_damage_sample): float32 masks [n, E] (into `out` when given, e.g. a
+    view of pinned host memory); `states` (PCG64_DTYPE) advance in place
+    exactly as each env's numpy Generator would."""
     E = len(src)
     count = max(1, int(E * damaged_ratio))
     if E > 10000:   # numpy's choice leaves its Floyd branch above 10000 (not restated natively)
@@ -129,7 +130,10 @@ def damage_sample_batch(num_nodes: int, src: np.ndarray, dst: np.ndarray, states
         raise TypeError("states must be a C-contiguous PCG64_DTYPE array (pcg_states)")
     src = np.ascontiguousarray(src, np.int32)
     dst = np.ascontiguousarray(dst, np.int32)
-    out = np.zeros((len(states), E), np.float32)
+    if out is None:
+        out = np.zeros((len(states), E), np.float32)
+    elif out.shape != (len(states), E) or out.dtype != np.float32 or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous float32 array [n, E]")
     L = _lib.load()
     _lib.check(L.trx_damage_sample(int(num_nodes), E, src.ctypes.data, dst.ctypes.data, count, 50, len(states),
                                    states.ctypes.data, out.ctypes.data, int(nthreads)), "trx_damage_sample")

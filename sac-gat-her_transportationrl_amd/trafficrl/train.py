@@ -351,6 +351,8 @@ class Trainer:
             fixed_damage_seed=cfg["fixed_damage_seed"], seeds=seeds, reset=False, sp_backend=cfg["sp_backend"],
             force_gpu_sp=cfg["force_gpu_sp"], gp_step=cfg["gp_step"], gp_keep_paths=cfg["gp_keep_paths"])
         self.N, self.E = self.env.num_nodes, self.env.num_edges
+        if not cfg["fixed_damage"] and self.device.type == "cuda":
+            self.env.enable_damage_prefetch(True)   # next masks drawn on a host thread meanwhile
         amp = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(str(cfg.get("amp")).lower())
         self.use_graphs = bool(cfg.get("graph_update", True)) and self.device.type == "cuda"
         if self.use_graphs and not graph_memset_replays_ok(self.device):
@@ -426,7 +428,9 @@ class Trainer:
             env.reset_where(done_mask, self.fixed_mask.expand(self.B, -1))
         else:
             ids = torch.nonzero(done_mask).squeeze(1).tolist()
-            if ids:
+            if len(ids) == self.B:   # every env at once: the prefetched draw (enable_damage_prefetch)
+                env.reset(observe=False)
+            elif ids:
                 env.reset(env_ids=ids, observe=False)
         self.ep_prev_tstt = torch.where(done_mask, env.tstt, self.ep_prev_tstt)
 
