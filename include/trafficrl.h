@@ -249,9 +249,10 @@ int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
 
 /* Edge scorer of Actor/Critic (src/rl/sac.py:42-46, 69-78) for regular
  * batches, one workgroup per graph:
- *   z = bf16(bf16(p[src,:H] + p[dst,H:]) + bf16(bf16(ea) @ we^T)) + c[graph]
- *   logit = bf16(bf16(relu(z)) . w2 + b2)
- * p [N, 2H] bf16 = node_emb @ [W_src; W_dst]^T, c [B, H] fp32 = bf16(ctx @ W_ctx^T) + b1.
+ *   z = ((p[src,:H] + p[dst,H:]) + ea @ we^T) + c[graph]      (fp32)
+ *   logit = relu(z) . w2 + b2                                   (fp32)
+ * p [N, 2H] bf16 = node_emb @ [W_src; W_dst]^T (the bf16 GEMM), c [B, H] fp32 =
+ * bf16(ctx @ W_ctx^T) + b1; everything after those products is fp32.
  * softmax != 0: logits masked (mask <= 0 -> -1e9) and soft-maxed per graph
  * (Actor probs); else raw logits (Critic Q).  hidden <= 512, edge_dim <= 8,
  * nodes_per_graph * hidden <= 32768 (the graph's p rows are staged in LDS). */
@@ -262,9 +263,9 @@ typedef struct trx_edge_head_args {
     const void* p;              /* bf16 [N, 2*hidden] */
     const float* c;             /* [B, hidden] */
     const float* ea;            /* [B*E, edge_dim] normalised edge features */
-    const float* we;            /* [hidden, edge_dim] bf16-representable */
-    const float* w2;            /* [hidden] bf16-representable */
-    const float* b2;            /* [1] bf16-representable (device: no host read) */
+    const float* we;            /* [hidden, edge_dim] */
+    const float* w2;            /* [hidden] */
+    const float* b2;            /* [1] (device: no host read) */
     const float* mask;          /* [B*E] (softmax only) */
     int32_t softmax;
     float* out;                 /* [B*E] probs (softmax) or logits */
@@ -326,10 +327,12 @@ int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream);
 /* Backward of the edge scorer's logits (softmax = 0) for training, one
  * workgroup per graph (hidden <= 256): from grad_logits [B*E] float32 and the
  * same args (p, c, ea, we, w2, src, dst, nodes_per_graph) it writes grad_p
- * [N, 2H] bf16, grad_c [B, H] float32, grad_z [B*E, H] bf16 (the gradient at
- * the bf16 link pre-activation: the link-feature weight and input gradients
- * are GEMMs of it) and grad_w2_part [B, H] float32 (per-graph partial sums of
- * the 256->1 weight gradient).  bf16 roundings follow the autocast torch path. */
+ * [N, 2H] bf16 (fp32 sums over the graph's links, rounded once), grad_c [B, H]
+ * float32, grad_z [B*E, H] bf16 (the gradient at the link pre-activation: the
+ * link-feature weight and input gradients are bf16 GEMMs of it) and
+ * grad_w2_part [B, H] float32 (per-graph partial sums of the 256->1 weight
+ * gradient).  fp32 after the p GEMM, as the forward (and the general path of
+ * trafficrl/rl/sac.py _EdgeHead.edge_scores). */
 int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
                            void* grad_z, float* grad_w2_part, void* stream);
 
