@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 8
+#define TRX_ABI_VERSION 9   /* 9: fp32 edge scorer after its p GEMM; trx_gat_layer0_* */
 
 /* error codes */
 #define TRX_OK 0
@@ -246,6 +246,42 @@ typedef struct trx_gat_layer_args {
     float* save_stats;          /* [N, 2] LayerNorm mean, rstd                             */
 } trx_gat_layer_args;
 int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
+
+/* Layer 0 of GATEncoder for inference (no saved intermediates), in its linear
+ * form (gat_layer0.hip): 4 raw features per node, heads*channels = 256, 512 or
+ * 1024, concat, LayerNorm, relu(x + input_proj(x_in)); fp32 throughout.  The
+ * attention logits are 4-dots with u = W0_h^T att_h, the aggregate is
+ * W0_h (sum_j alpha_jh x_j) + b, the LayerNorm statistics are float64 forms
+ * of that per-head 4-vector (`stats`).  u and stats come from
+ * trx_gat_layer0_prepare whenever the weights change. */
+typedef struct trx_gat_layer0_args {
+    int32_t num_graphs, nodes_per_graph, heads, channels;  /* nodes_per_graph <= 32 */
+    int32_t max_graph_edges;    /* CSR positions per graph (self loops included), <= 256 */
+    const float* x0;            /* [N, 4] raw (normalised) node features */
+    const float* w0;            /* [heads*channels, 4] lin.weight */
+    const int32_t* rowptr;      /* [N+1] CSR by destination (self loops included) */
+    const int32_t* col;         /* [Et] */
+    const float* a_edge;        /* [Et, a_edge_stride] edge logits in CSR order */
+    int32_t a_edge_stride, a_edge_offset;
+    const float* bias;          /* [heads*channels] */
+    float negative_slope;
+    const float* ln_weight;     /* [heads*channels] */
+    const float* ln_bias;
+    float ln_eps;
+    const float* wp;            /* [heads*channels, 4] input_proj.weight */
+    const float* bp;            /* [heads*channels] input_proj.bias */
+    const float* u;             /* [2, heads, 4] W0_h^T att_src_h | W0_h^T att_dst_h */
+    const double* stats;        /* [heads*24 + 2] (trx_gat_layer0_prepare) */
+    float* out_f32;             /* [N, heads*channels] or NULL */
+    void* out_bf16;             /* [N, heads*channels] bf16 or NULL */
+} trx_gat_layer0_args;
+int trx_gat_layer0_infer(const trx_gat_layer0_args* a, void* stream);
+/* u [2*heads*4] float32 and stats [heads*24 + 2] float64 of one weight set:
+ * per head h (channels c of h, in order) s_h = sum W0[c], t_h = sum b_c W0[c],
+ * G_h = sum W0[c] W0[c]^T (4x4 row-major) at stats[24h + 0/4/8], then
+ * sum b_c and sum b_c^2.  One workgroup. */
+int trx_gat_layer0_prepare(int32_t heads, int32_t channels, const float* w0, const float* att_src,
+                           const float* att_dst, const float* bias, float* u, double* stats, void* stream);
 
 /* Edge scorer of Actor/Critic (src/rl/sac.py:42-46, 69-78) for regular
  * batches, one workgroup per graph:

@@ -633,6 +633,44 @@ int trx_per32_sample(const float* tree, int64_t capacity, const double* u, int32
     return TRX_OK;
 }
 
+int trx_gat_layer0_infer(const trx_gat_layer0_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_layer0_infer: NULL args");
+    const int HC = a->heads * a->channels;
+    if (a->num_graphs < 0) return fail(TRX_EINVAL, "gat_layer0_infer: num_graphs < 0");
+    if (a->nodes_per_graph < 1 || a->nodes_per_graph > 32)
+        return fail(TRX_EUNSUP, "gat_layer0_infer: nodes_per_graph must be 1..32 (got %d)", a->nodes_per_graph);
+    if (a->heads < 1 || a->heads > 8 || a->channels % 4 != 0 || (HC != 256 && HC != 512 && HC != 1024))
+        return fail(TRX_EUNSUP, "gat_layer0_infer: heads*channels must be 256, 512 or 1024 (got %d x %d)", a->heads,
+                    a->channels);
+    if (a->max_graph_edges < 1 || a->max_graph_edges > 256)
+        return fail(TRX_EUNSUP, "gat_layer0_infer: max_graph_edges must be 1..256");
+    if (!a->x0 || !a->w0 || !a->rowptr || !a->col || !a->a_edge || !a->bias || !a->ln_weight || !a->ln_bias ||
+        !a->wp || !a->bp || !a->u || !a->stats)
+        return fail(TRX_EINVAL, "gat_layer0_infer: NULL input or parameter buffer");
+    if (a->a_edge_stride < a->a_edge_offset + a->heads || a->a_edge_offset < 0)
+        return fail(TRX_EINVAL, "gat_layer0_infer: a_edge stride/offset");
+    if (!a->out_f32 && !a->out_bf16) return fail(TRX_EINVAL, "gat_layer0_infer: no output");
+    const uintptr_t al16 = (uintptr_t)a->w0 | (uintptr_t)a->wp | (uintptr_t)a->bias | (uintptr_t)a->ln_weight |
+                           (uintptr_t)a->ln_bias | (uintptr_t)a->bp | (uintptr_t)a->out_f32;
+    if ((al16 & 15) || ((uintptr_t)a->out_bf16 & 7))
+        return fail(TRX_EINVAL, "gat_layer0_infer: parameter / output buffers must be 16-byte aligned");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_gat_layer0(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_layer0_infer launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
+int trx_gat_layer0_prepare(int32_t heads, int32_t channels, const float* w0, const float* att_src,
+                           const float* att_dst, const float* bias, float* u, double* stats, void* stream) {
+    if (heads < 1 || heads > 8 || channels < 1) return fail(TRX_EINVAL, "gat_layer0_prepare: heads 1..8, channels");
+    if (!w0 || !att_src || !att_dst || !bias || !u || !stats)
+        return fail(TRX_EINVAL, "gat_layer0_prepare: NULL buffer");
+    hipError_t e = trx::launch_gat_layer0_prepare(heads, channels, w0, att_src, att_dst, bias, u, stats,
+                                                  static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_layer0_prepare launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream) {
     if (!a) return fail(TRX_EINVAL, "gat_layer_infer: NULL args");
     const int HC = a->heads * a->channels;

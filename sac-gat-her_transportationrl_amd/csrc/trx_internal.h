@@ -168,6 +168,10 @@ hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, cons
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a);
 hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream);
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
+size_t gat_layer0_smem(const trx_gat_layer0_args& a);
+hipError_t launch_gat_layer0(const trx_gat_layer0_args& a, hipStream_t stream);
+hipError_t launch_gat_layer0_prepare(int H, int C, const float* w0, const float* att_src, const float* att_dst,
+                                     const float* bias, float* u, double* stats, hipStream_t stream);
 size_t edge_head_infer_smem(const trx_edge_head_args& a);
 size_t gat_tail_smem(const trx_gat_tail_args& a);
 int gat_tail_mtiles(int nodes_per_graph);

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("TRX_LIB") or os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 8
+ABI_VERSION = 9
 SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
@@ -33,6 +33,7 @@ EXPORTS = (
     "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
     "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_gat_prologue_backward",
     "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
+    "trx_gat_layer0_infer", "trx_gat_layer0_prepare",
 )
 
 
@@ -89,6 +90,17 @@ class TrxGatLayerArgs(ctypes.Structure):
         ("activation", _i32),
         ("out_f32", _vp), ("out_bf16", _vp), ("pool", _vp),
         ("save_alpha", _vp), ("save_asd", _vp), ("save_v", _vp), ("save_stats", _vp),
+    ]
+
+
+class TrxGatLayer0Args(ctypes.Structure):
+    """trx_gat_layer0_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("nodes_per_graph", _i32), ("heads", _i32), ("channels", _i32),
+        ("max_graph_edges", _i32), ("x0", _vp), ("w0", _vp), ("rowptr", _vp), ("col", _vp),
+        ("a_edge", _vp), ("a_edge_stride", _i32), ("a_edge_offset", _i32), ("bias", _vp), ("negative_slope", _f32),
+        ("ln_weight", _vp), ("ln_bias", _vp), ("ln_eps", _f32), ("wp", _vp), ("bp", _vp), ("u", _vp),
+        ("stats", _vp), ("out_f32", _vp), ("out_bf16", _vp),
     ]
 
 
@@ -286,6 +298,8 @@ def load():
     L.trx_graph_patch_memsets.argtypes = [_vp, ctypes.POINTER(ctypes.c_int32)]
     L.trx_gat_layer_infer.argtypes = [ctypes.POINTER(TrxGatLayerArgs), _vp]
     L.trx_edge_head_infer.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp]
+    L.trx_gat_layer0_infer.argtypes = [ctypes.POINTER(TrxGatLayer0Args), _vp]
+    L.trx_gat_layer0_prepare.argtypes = [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_gat_tail_infer.argtypes = [ctypes.POINTER(TrxGatTailArgs), _vp]
     L.trx_edge_att_weights_backward.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp, _i32, _vp, _vp]
     L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
@@ -327,7 +341,8 @@ def load():
                  "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
                  "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
                  "trx_episode_step", "trx_gat_layer_backward", "trx_partial_sum", "trx_gat_prologue_backward",
-                 "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward"):
+                 "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
+                 "trx_gat_layer0_infer", "trx_gat_layer0_prepare"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

@@ -121,6 +121,7 @@ def _bf16r(t: torch.Tensor) -> torch.Tensor:
 # captures under static_weights() (slots read, never written, inside the
 # graph).  Any other capture (the SAC update) recomputes the copies inside the
 # graph on every replay.
+LAYER0_LINEAR = True   # inference layer 0 through trx_gat_layer0_infer (tests compare both kernels)
 _PREP_EPOCH = [0]
 _prep_cache: Dict[Tuple, Tuple] = {}
 _STATIC = [False]
@@ -206,7 +207,71 @@ def refresh_static(model):
     """Bring an Actor/Critic's prepared-weight slots up to date (in place)."""
     with torch.no_grad():
         prepared_encoder(model.encoder, list(model.encoder.layers))
+        prepared_layer0(model.encoder)
         prepared_head(model)
+
+
+def _layer0_params(enc):
+    l0, ip = enc.layers[0], enc.input_proj
+    return (l0.lin.weight, l0.att_src, l0.att_dst, l0.bias, ip.weight, ip.bias)
+
+
+def layer0_supported(enc) -> bool:
+    """trx_gat_layer0_infer limits (the linear-form layer 0)."""
+    l0 = enc.layers[0]
+    hc = l0.heads * l0.out_channels
+    return (l0.in_channels == 4 and l0.concat and l0.bias is not None and hc in (256, 512, 1024)
+            and l0.heads <= 8 and l0.out_channels % 4 == 0 and enc.norms[0].weight is not None)
+
+
+def prepared_layer0(enc):
+    return _prepared(enc, "enc0", _layer0_params(enc), lambda into: _layer0_consts(enc, into))
+
+
+def _layer0_consts(enc, into=None):
+    """Exact float32 copies of layer 0's lin / input_proj weights and bias
+    (one trx_bf16_round launch in copy mode) and the linear form's per-head
+    constants (trx_gat_layer0_prepare): (w0, wp, bp, u, stats)."""
+    l0, ip = enc.layers[0], enc.input_proj
+    H, C = l0.heads, l0.out_channels
+    dev = l0.lin.weight.device
+    if into is None:
+        w0, wp = torch.empty(H * C, 4, device=dev), torch.empty(H * C, 4, device=dev)
+        bp = torch.empty(H * C, device=dev)
+        u = torch.empty(2 * H * 4, device=dev)
+        stats = torch.empty(H * 24 + 2, device=dev, dtype=torch.float64)
+    else:
+        w0, wp, bp, u, stats = into
+    _round_into([(l0.lin.weight, w0, True), (ip.weight, wp, True), (ip.bias, bp, True)])
+    L = _lib.load()
+    att_s, att_d = l0.att_src.detach().reshape(-1), l0.att_dst.detach().reshape(-1)
+    _lib.check(L.trx_gat_layer0_prepare(H, C, _lib.ptr(w0), _lib.ptr(att_s), _lib.ptr(att_d),
+                                        _lib.ptr(l0.bias.detach()), _lib.ptr(u), _lib.ptr(stats),
+                                        _lib.stream_ptr(dev)), "trx_gat_layer0_prepare")
+    return w0, wp, bp, u, stats
+
+
+def layer0_infer(enc, x0: torch.Tensor, topo: Topology, a_all: torch.Tensor, offset: int,
+                 out_f32: Optional[torch.Tensor], out_bf16: Optional[torch.Tensor]):
+    """Layer 0 (GATConv 4 -> H*C + LayerNorm + relu(x + input_proj(x))) of a
+    regular batch without saved intermediates: trx_gat_layer0_infer, the
+    linear form (fp32 throughout; csrc/gat_layer0.hip)."""
+    L = _lib.load()
+    l0, norm = enc.layers[0], enc.norms[0]
+    w0, wp, bp, u, stats = prepared_layer0(enc)
+    a = _lib.TrxGatLayer0Args()
+    a.num_graphs, a.nodes_per_graph, a.heads, a.channels = topo.B, topo.n, l0.heads, l0.out_channels
+    a.max_graph_edges = topo.max_graph_edges
+    a.x0, a.w0 = x0.data_ptr(), w0.data_ptr()
+    a.rowptr, a.col = topo.g.rowptr.data_ptr(), topo.g.col.data_ptr()
+    a.a_edge, a.a_edge_stride, a.a_edge_offset = a_all.data_ptr(), a_all.shape[1], offset
+    bias, lw, lb = l0.bias.detach(), norm.weight.detach(), norm.bias.detach()
+    a.bias, a.negative_slope = bias.data_ptr(), float(l0.negative_slope)
+    a.ln_weight, a.ln_bias, a.ln_eps = lw.data_ptr(), lb.data_ptr(), float(norm.eps)
+    a.wp, a.bp, a.u, a.stats = wp.data_ptr(), bp.data_ptr(), u.data_ptr(), stats.data_ptr()
+    a.out_f32 = 0 if out_f32 is None else out_f32.data_ptr()
+    a.out_bf16 = 0 if out_bf16 is None else out_bf16.data_ptr()
+    _lib.check(L.trx_gat_layer0_infer(a, _lib.stream_ptr(x0.device)), "trx_gat_layer0_infer")
 
 
 def _encoder_weights(enc, layers, into=None):
@@ -327,6 +392,7 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
     stride = a_all.shape[1]
     stream = _lib.stream_ptr(dev)
     wts = prepared_encoder(enc, layers)
+    lin0 = LAYER0_LINEAR and layer0_supported(enc)
     prev_f32, prev_bf16 = None, None
     emb = ctx = None
     for i, l in enumerate(layers):
@@ -338,6 +404,13 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
         args.num_graphs, args.nodes_per_graph, args.heads, args.channels = topo.B, topo.n, l.heads, l.out_channels
         args.concat, args.max_graph_edges = int(l.concat), topo.max_graph_edges
         keep = []
+        if i == 0 and lin0:   # linear-form layer 0 (csrc/gat_layer0.hip)
+            out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if len(layers) > 2 else None
+            layer0_infer(enc, x, topo, a_all, offs[0], out_f32, out_bf16)
+            prev_f32, prev_bf16 = out_f32, out_bf16
+            emb = out_bf16
+            continue
         if i == 0:
             w0, wp, bp = wts[0]
             keep += [w0, wp, bp]

@@ -326,6 +326,11 @@ class _Lin(nn.Module):
         return splitk_linear(x, self.weight)
 
 
+def _f32up(t: torch.Tensor) -> torch.Tensor:
+    """At least float32 (half types up, float64 kept)."""
+    return t.float() if t.dtype in (torch.bfloat16, torch.float16) else t
+
+
 class GATConv(nn.Module):
     def __init__(self, in_channels: int, out_channels: int, heads: int = 1, concat: bool = True,
                  negative_slope: float = 0.2, dropout: float = 0.0, add_self_loops: bool = True,
@@ -362,7 +367,10 @@ class GATConv(nn.Module):
         N = x.size(0)
         g = build_csr(edge_index, N)
         if self.in_channels <= _SKINNY_IN:
-            xh = skinny_linear(x, self.lin.weight)         # [N, H*C]  (4 input features)
+            # 4 input features: kept in fp32 under autocast (the reference's precision;
+            # the fused inference kernel's linear form, csrc/gat_layer0.hip, does the same)
+            with torch.autocast("cuda", enabled=False):
+                xh = skinny_linear(_f32up(x), self.lin.weight)   # [N, H*C]
         else:
             xh = self.lin(x)                               # [N, H*C]  (MFMA GEMM)
         # per-head attention dot products <xh_h, att_h> for src and dst: one
@@ -495,8 +503,11 @@ class GATEncoder(nn.Module):
                 x = layer(x, edge_index, edge_attr=edge_attr, a_edge_csr=ae, skip_bias=tail)
                 if i == 0:
                     ip = self.input_proj
-                    x_in = (skinny_linear(x_in, ip.weight, ip.bias) if ip.in_features <= _SKINNY_IN
-                            else ip(x_in))
+                    if ip.in_features <= _SKINNY_IN:   # fp32, like layer 0's projection
+                        with torch.autocast("cuda", enabled=False):
+                            x_in = skinny_linear(_f32up(x_in), ip.weight, ip.bias)
+                    else:
+                        x_in = ip(x_in)
                 if tail:
                     x = layer_tail(x, layer.bias, norm, x_in)
                     continue

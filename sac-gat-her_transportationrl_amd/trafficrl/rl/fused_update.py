@@ -104,6 +104,15 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         norm = enc.norms[i]
         args = _layer_args(l, norm, topo, a_all, off, stride, i, last)
         rec = {"off": off, "heads": l.heads, "channels": l.out_channels}
+        if i == 0 and not save and fused.LAYER0_LINEAR and fused.layer0_supported(enc):
+            # no-grad passes: the linear-form layer 0 (csrc/gat_layer0.hip)
+            out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if len(layers) > 2 else None
+            fused.layer0_infer(enc, x0, topo, a_all, off, out_f32, out_bf16)
+            recs.append(rec)
+            prev_f32, prev_bf16 = out_f32, out_bf16
+            off += l.heads
+            continue
         if i == 0:
             w0, wp, bp = wts[0]
             args.in_dim, args.x0, args.w0 = x0.shape[1], x0.data_ptr(), w0.data_ptr()

@@ -35,7 +35,7 @@ def test_exports_every_declared_symbol():
     assert set(syms) == set(_lib.EXPORTS)
     for s in syms:
         assert hasattr(L, s), s
-    assert L.trx_abi_version() == _lib.ABI_VERSION == 8
+    assert L.trx_abi_version() == _lib.ABI_VERSION == 9
 
 
 def test_struct_layout_matches_header(tmp_path):
@@ -169,7 +169,7 @@ def test_fused_args_layout_matches_header(tmp_path):
     from trafficrl import _lib
     lines = []
     structs = (("trx_gat_layer_args", _lib.TrxGatLayerArgs), ("trx_edge_head_args", _lib.TrxEdgeHeadArgs),
-               ("trx_gat_prologue_args", _lib.TrxGatPrologueArgs))
+               ("trx_gat_prologue_args", _lib.TrxGatPrologueArgs), ("trx_gat_layer0_args", _lib.TrxGatLayer0Args))
     for cname, cls in structs:
         lines.append(f'printf("%zu\\n", sizeof({cname}));')
         for f, _ in cls._fields_:

@@ -245,3 +245,79 @@ def test_prepared_weights_follow_updates():
     assert not torch.allclose(after[valid], before[valid])
     # to bf16 precision of the logits' magnitude (the span can be tiny here)
     assert (after[valid] - ref[valid]).abs().max().item() <= 1e-2 * ref[valid].abs().max().item() + 1e-3
+
+
+def test_layer0_linear_form_matches_fp32_restatement():
+    """trx_gat_layer0_infer (csrc/gat_layer0.hip: attention logits as 4-dots,
+    aggregate of the raw features, LayerNorm moments as float64 forms)
+    against layer 0 restated in plain fp32 torch ops from the same inputs
+    (the prologue's normalised features and edge logits in CSR order):
+    GATConv lin, per-head <xh, att> logits, leaky ReLU 0.2, softmax over each
+    node's in-edges (+1e-16), aggregate + bias, LayerNorm, + input_proj,
+    ReLU (src/models/gat_encoder.py:36-47).  Both outputs (fp32 residual,
+    bf16 GEMM input) within 2e-5 relative to the row scale / one bf16 ulp."""
+    from trafficrl.models import fused
+    from trafficrl.rl.sac import Actor
+    torch.manual_seed(11)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    with torch.no_grad():   # non-trivial LayerNorm / bias parameters
+        for p in (actor.encoder.layers[0].bias, actor.encoder.norms[0].weight, actor.encoder.norms[0].bias):
+            p.add_(0.1 * torch.randn_like(p))
+    enc = actor.encoder
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=13)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        topo = fused.topology(ei, bv, B)
+        x0, eaf, a_all = fused.prologue(actor, node_x, ea, topo)
+        N = x0.shape[0]
+        out32 = torch.empty(N, 1024, device="cuda")
+        out16 = torch.empty(N, 1024, device="cuda", dtype=torch.bfloat16)
+        fused.layer0_infer(enc, x0, topo, a_all, 0, out32, out16)
+    torch.cuda.synchronize()
+    l0, ln, ip = enc.layers[0], enc.norms[0], enc.input_proj
+    H, C = l0.heads, l0.out_channels
+    with torch.no_grad():
+        x = x0.double()
+        xh = x @ l0.lin.weight.double().t()
+        a_s = (xh.view(N, H, C) * l0.att_src.double().view(1, H, C)).sum(-1)
+        a_d = (xh.view(N, H, C) * l0.att_dst.double().view(1, H, C)).sum(-1)
+        rp, col = topo.g.rowptr.long(), topo.g.col.long()
+        dst = torch.repeat_interleave(torch.arange(N, device="cuda"), rp.diff())
+        logit = torch.nn.functional.leaky_relu(a_s[col] + a_d[dst] + a_all[:, :H].double(), 0.2)
+        mx = torch.full((N, H), -1e300, device="cuda", dtype=torch.float64).scatter_reduce(
+            0, dst[:, None].expand(-1, H), logit, "amax")
+        ex = torch.exp(logit - mx[dst])
+        den = torch.zeros(N, H, device="cuda", dtype=torch.float64).index_add_(0, dst, ex) + 1e-16
+        alpha = ex / den[dst]
+        agg = torch.zeros(N, H, C, device="cuda", dtype=torch.float64).index_add_(
+            0, dst, alpha[:, :, None] * xh.view(N, H, C)[col]).reshape(N, H * C)
+        v = agg + l0.bias.double()
+        y = torch.nn.functional.layer_norm(v, (H * C,), ln.weight.double(), ln.bias.double(), ln.eps)
+        ref = torch.relu(y + x @ ip.weight.double().t() + ip.bias.double())
+    scale = ref.abs().amax(1, keepdim=True).clamp(min=1e-3)
+    err = ((out32.double() - ref).abs() / scale).max().item()
+    print(f"layer0 linear form: max error / row scale {err:.2e}")
+    assert err < 2e-5
+    torch.testing.assert_close(out16, out32.to(torch.bfloat16), rtol=0, atol=0)   # one rounding of the same row
+
+
+def test_actor_layer0_kernels_agree():
+    """The acting pass with the linear-form layer 0 and with the round-3
+    layer kernel (bf16 projection) agree to bf16 precision."""
+    from trafficrl.models import fused
+    from trafficrl.rl.sac import Actor
+    torch.manual_seed(4)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=21)
+    outs = []
+    for lin in (False, True):
+        fused.LAYER0_LINEAR = lin
+        try:
+            with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+                outs.append(actor(node_x, ei, ea, mask, bv, num_graphs=B))
+        finally:
+            fused.LAYER0_LINEAR = True
+    (l0, p0, _), (l1, p1, _) = outs
+    valid = mask > 0
+    span = (l0[valid].max() - l0[valid].min()).item()
+    assert (l1[valid] - l0[valid]).abs().max().item() <= 0.02 * span + 1e-3
+    assert (p1 - p0).abs().max().item() < 1e-2
