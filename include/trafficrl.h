@@ -274,8 +274,42 @@ typedef struct trx_gat_layer0_args {
     const double* stats;        /* [heads*24 + 2] (trx_gat_layer0_prepare) */
     float* out_f32;             /* [N, heads*channels] or NULL */
     void* out_bf16;             /* [N, heads*channels] bf16 or NULL */
+    float* desc;                /* [N, 4*heads + 8] per-node descriptor (xbar [heads][4], x [4], mean,
+                                   rstd, 0, 0) for trx_gat_mid_infer, or NULL */
 } trx_gat_layer0_args;
 int trx_gat_layer0_infer(const trx_gat_layer0_args* a, void* stream);
+/* The middle GAT layer whose residual input is layer 0's output (GATEncoder
+ * layer 1), for inference: xh = bf16(x_in @ lin.weight^T) given, channels
+ * == 256, heads*channels = layer 0's; the residual rows are regenerated from
+ * layer 0's descriptor (trx_gat_layer0_infer's desc) and parameters with the
+ * expression that kernel evaluates (bit-identical), not read from HBM. */
+typedef struct trx_gat_mid_args {
+    int32_t num_graphs, nodes_per_graph, heads, channels;
+    int32_t max_graph_edges;
+    const void* xh;             /* bf16 [N, heads*channels] */
+    const int32_t* rowptr;
+    const int32_t* col;
+    const float* a_edge;
+    int32_t a_edge_stride, a_edge_offset;
+    const float* att_src;       /* [heads*channels] */
+    const float* att_dst;
+    const float* bias;
+    float negative_slope;
+    const float* ln_weight;
+    const float* ln_bias;
+    float ln_eps;
+    const float* desc;          /* [N, 4*l0_heads + 8] */
+    int32_t l0_heads;
+    const float* l0_w0;         /* layer 0: [heads*channels, 4] lin.weight (the same float32 buffers */
+    const float* l0_bias;       /*   trx_gat_layer0_infer read)                                      */
+    const float* l0_ln_weight;
+    const float* l0_ln_bias;
+    const float* l0_wp;         /* [heads*channels, 4] input_proj.weight */
+    const float* l0_bp;
+    float* out_f32;             /* [N, heads*channels] or NULL */
+    void* out_bf16;             /* [N, heads*channels] bf16 or NULL */
+} trx_gat_mid_args;
+int trx_gat_mid_infer(const trx_gat_mid_args* a, void* stream);
 /* u [2*heads*4] float32 and stats [heads*24 + 2] float64 of one weight set:
  * per head h (channels c of h, in order) s_h = sum W0[c], t_h = sum b_c W0[c],
  * G_h = sum W0[c] W0[c]^T (4x4 row-major) at stats[24h + 0/4/8], then

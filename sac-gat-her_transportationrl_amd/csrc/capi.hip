@@ -660,6 +660,39 @@ int trx_gat_layer0_infer(const trx_gat_layer0_args* a, void* stream) {
     return TRX_OK;
 }
 
+int trx_gat_mid_infer(const trx_gat_mid_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_mid_infer: NULL args");
+    const int HC = a->heads * a->channels;
+    if (a->num_graphs < 0) return fail(TRX_EINVAL, "gat_mid_infer: num_graphs < 0");
+    if (a->nodes_per_graph < 1 || a->nodes_per_graph > 32)
+        return fail(TRX_EUNSUP, "gat_mid_infer: nodes_per_graph must be 1..32 (got %d)", a->nodes_per_graph);
+    if (a->channels != 256 || a->heads < 1 || a->heads > 4)
+        return fail(TRX_EUNSUP, "gat_mid_infer: channels must be 256 and heads 1..4 (got %d x %d)", a->heads,
+                    a->channels);
+    if (a->l0_heads < 1 || a->l0_heads > 8 || HC % a->l0_heads != 0 || (HC / a->l0_heads) % 4 != 0)
+        return fail(TRX_EUNSUP, "gat_mid_infer: layer-0 heads must divide heads*channels into multiples of 4");
+    if (a->max_graph_edges < 1 || a->max_graph_edges > 256)
+        return fail(TRX_EUNSUP, "gat_mid_infer: max_graph_edges must be 1..256");
+    if (!a->xh || !a->rowptr || !a->col || !a->a_edge || !a->att_src || !a->att_dst || !a->bias || !a->ln_weight ||
+        !a->ln_bias || !a->desc || !a->l0_w0 || !a->l0_bias || !a->l0_ln_weight || !a->l0_ln_bias || !a->l0_wp ||
+        !a->l0_bp)
+        return fail(TRX_EINVAL, "gat_mid_infer: NULL input or parameter buffer");
+    if (a->a_edge_stride < a->a_edge_offset + a->heads || a->a_edge_offset < 0)
+        return fail(TRX_EINVAL, "gat_mid_infer: a_edge stride/offset");
+    if (!a->out_f32 && !a->out_bf16) return fail(TRX_EINVAL, "gat_mid_infer: no output");
+    const uintptr_t al16 = (uintptr_t)a->xh | (uintptr_t)a->att_src | (uintptr_t)a->att_dst | (uintptr_t)a->bias |
+                           (uintptr_t)a->ln_weight | (uintptr_t)a->ln_bias | (uintptr_t)a->l0_w0 |
+                           (uintptr_t)a->l0_bias | (uintptr_t)a->l0_ln_weight | (uintptr_t)a->l0_ln_bias |
+                           (uintptr_t)a->l0_wp | (uintptr_t)a->l0_bp | (uintptr_t)a->out_f32;
+    if ((al16 & 15) || ((uintptr_t)a->out_bf16 & 7))
+        return fail(TRX_EINVAL, "gat_mid_infer: buffers must be 16-byte aligned");
+    if (trx::gat_mid_smem(*a) > 160 * 1024) return fail(TRX_EUNSUP, "gat_mid_infer: LDS > 160 KB");
+    if (a->num_graphs == 0) return TRX_OK;
+    hipError_t e = trx::launch_gat_mid(*a, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "gat_mid_infer launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_gat_layer0_prepare(int32_t heads, int32_t channels, const float* w0, const float* att_src,
                            const float* att_dst, const float* bias, float* u, double* stats, void* stream) {
     if (heads < 1 || heads > 8 || channels < 1) return fail(TRX_EINVAL, "gat_layer0_prepare: heads 1..8, channels");

@@ -37,6 +37,21 @@ __device__ __forceinline__ uint32_t pk_bf16_l0(float lo, float hi) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, l0_b2));
 }
 
+// wave-wide sum on DPP + readlane: quad butterflies, row mirrors, then the four
+// 16-lane row totals (every lane gets the total)
+#define L0_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, false))
+__device__ __forceinline__ float wave_sum_l0(float v) {
+    v = v + L0_DPP(v, 0xB1);
+    v = v + L0_DPP(v, 0x4E);
+    v = v + L0_DPP(v, 0x141);
+    v = v + L0_DPP(v, 0x140);
+    return (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+           (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
+}
+#undef L0_DPP
+
 // 4-term dot product in a fixed order (no contraction: -ffp-contract=off)
 __device__ __forceinline__ float dot4(const float (&x)[4], float a0, float a1, float a2, float a3) {
     return (x[0] * a0 + x[1] * a1) + (x[2] * a2 + x[3] * a3);
@@ -179,6 +194,20 @@ __global__ void __launch_bounds__(HC / 4) gat_layer0_lin_kernel(trx_gat_layer0_a
         st[2 * i + 1] = (float)(1.0 / sqrt(var + (double)a.ln_eps));
     }
     __syncthreads();
+    if (a.desc) {  // per-node descriptor: xbar [H][4], x [4], mean, rstd (trx_gat_mid_infer regenerates the row)
+        const int DS = 4 * H + 8;
+        for (int v = tid; v < n * DS; v += NT) {
+            const int i = v / DS, q = v - i * DS;
+            float val = 0.0f;
+            if (q < 4 * H)
+                val = xb[i * H * 4 + q];
+            else if (q < 4 * H + 4)
+                val = xs[4 * i + q - 4 * H];
+            else if (q < 4 * H + 6)
+                val = st[2 * i + q - 4 * H - 4];
+            a.desc[(size_t)(node0 + i) * DS + q] = val;
+        }
+    }
 
     // output rows: v = W0 xbar + b, y = relu(LN(v) + (Wp x + bp)), float32 + bf16
     for (int i = 0; i < n; ++i) {
@@ -200,6 +229,210 @@ __global__ void __launch_bounds__(HC / 4) gat_layer0_lin_kernel(trx_gat_layer0_a
         if (a.out_bf16)
             *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.out_bf16) + o) =
                 make_uint2(pk_bf16_l0(y[0], y[1]), pk_bf16_l0(y[2], y[3]));
+    }
+}
+
+// ------------------------------------------------------------------ layer 1
+// The middle GAT layer (gat_encoder.py:41-47 for 0 < i < L-1, residual x_in =
+// layer 0's output) with the residual regenerated from layer 0's per-node
+// descriptor (xbar, x, mean, rstd) and layer 0's parameters, with the very
+// expression trx_gat_layer0_infer evaluates (bit-identical rows), instead of
+// reading a float32 [N, H*C] residual from HBM.  Layout: thread t owns
+// channels 4t..4t+3 of every row (channels == 256: wave w = head w), the
+// graph's xh rows (bf16) staged in LDS; attention dots are wave sums; the
+// LayerNorm moments of NB nodes at a time are combined across the waves
+// through LDS (two barriers per batch).  Output bf16 (the last layer's GEMM
+// input) and optionally float32.
+template <int HC, int NB>
+__global__ void __launch_bounds__(HC / 4) gat_mid_gen_kernel(trx_gat_mid_args a) {
+    constexpr int NT = HC / 4, NW = NT / 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = a.nodes_per_graph, H = a.heads;  // H == NW (channels 256)
+    const int H0 = a.l0_heads, C0 = HC / H0, DS = 4 * H0 + 8;
+    const int node0 = g * n;
+    const int ebeg = a.rowptr[node0];
+    const int ne = a.rowptr[node0 + n] - ebeg;
+    const int me = a.max_graph_edges;
+    const int f0 = 4 * tid, h0 = f0 / C0;
+
+    // xh rows of the graph (n * HC bf16, contiguous in HBM and in LDS): LDS-DMA,
+    // 1 KB per wave instruction, no VGPRs; all in flight before the constants load
+    const int nq = n * HC / 8;
+    {
+        const uint4* xsrc = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.xh) + (size_t)node0 * HC);
+        for (int base = wave * 64; base < nq; base += NT) {
+            const int v = base + lane;
+            if (v < nq)
+                __builtin_amdgcn_global_load_lds(xsrc + v, (__attribute__((address_space(3))) void*)(smem + (size_t)base * 16),
+                                                 16, 0, 0);
+        }
+    }
+    // constants of this thread's four channels: layer 1 (attention, bias, norm) and layer 0
+    float as_r[4], ad_r[4], b1[4], g1[4], e1[4], w0[4][4], wp[4][4], b0[4], g0[4], e0[4], bp[4];
+    {
+        const float4 x = *reinterpret_cast<const float4*>(a.att_src + f0), y = *reinterpret_cast<const float4*>(a.att_dst + f0);
+        const float4 p = *reinterpret_cast<const float4*>(a.bias + f0), q = *reinterpret_cast<const float4*>(a.ln_weight + f0);
+        const float4 r = *reinterpret_cast<const float4*>(a.ln_bias + f0);
+        as_r[0] = x.x, as_r[1] = x.y, as_r[2] = x.z, as_r[3] = x.w;
+        ad_r[0] = y.x, ad_r[1] = y.y, ad_r[2] = y.z, ad_r[3] = y.w;
+        b1[0] = p.x, b1[1] = p.y, b1[2] = p.z, b1[3] = p.w;
+        g1[0] = q.x, g1[1] = q.y, g1[2] = q.z, g1[3] = q.w;
+        e1[0] = r.x, e1[1] = r.y, e1[2] = r.z, e1[3] = r.w;
+        const float4* w4 = reinterpret_cast<const float4*>(a.l0_w0 + (size_t)f0 * 4);
+        const float4* p4 = reinterpret_cast<const float4*>(a.l0_wp + (size_t)f0 * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 u = w4[k], v = p4[k];
+            w0[k][0] = u.x, w0[k][1] = u.y, w0[k][2] = u.z, w0[k][3] = u.w;
+            wp[k][0] = v.x, wp[k][1] = v.y, wp[k][2] = v.z, wp[k][3] = v.w;
+        }
+        const float4 c = *reinterpret_cast<const float4*>(a.l0_bias + f0), d = *reinterpret_cast<const float4*>(a.l0_ln_weight + f0);
+        const float4 e = *reinterpret_cast<const float4*>(a.l0_ln_bias + f0), f = *reinterpret_cast<const float4*>(a.l0_bp + f0);
+        b0[0] = c.x, b0[1] = c.y, b0[2] = c.z, b0[3] = c.w;
+        g0[0] = d.x, g0[1] = d.y, g0[2] = d.z, g0[3] = d.w;
+        e0[0] = e.x, e0[1] = e.y, e0[2] = e.z, e0[3] = e.w;
+        bp[0] = f.x, bp[1] = f.y, bp[2] = f.z, bp[3] = f.w;
+    }
+    if (ne > me || ne < 0) {  // LDS was sized for max_graph_edges: poison, do not overrun
+        for (int i = 0; i < n; ++i) {
+            const size_t o = (size_t)(node0 + i) * HC + f0;
+            if (a.out_f32)
+                *reinterpret_cast<float4*>(a.out_f32 + o) =
+                    make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+            if (a.out_bf16) *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.out_bf16) + o) = make_uint2(0x7fc07fc0u, 0x7fc07fc0u);
+        }
+        return;
+    }
+    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);                 // [n][HC] bf16
+    float* dsc = reinterpret_cast<float*>(xs + (size_t)n * HC);       // [n][DS] layer-0 descriptors
+    float* as_ = dsc + n * DS;                                        // [n*H]
+    float* ad_ = as_ + n * H;                                         // [n*H] then softmax denominators
+    float* red = ad_ + n * H;                                         // [2][NW][NB] LayerNorm partials
+    float* al = red + 2 * NW * NB;                                    // [me*H]
+    int* cl = reinterpret_cast<int*>(al + me * H);                    // [me]
+    int* dlc = cl + me;                                               // [me]
+    int* rp = dlc + me;                                               // [n+1]
+    if (tid <= n) rp[tid] = a.rowptr[node0 + tid] - ebeg;
+    for (int p = tid; p < ne; p += NT) cl[p] = a.col[ebeg + p] - node0;
+    for (int v = tid; v < ne * H; v += NT) {
+        const int p = v / H, h = v - p * H;
+        al[v] = a.a_edge[(size_t)(ebeg + p) * a.a_edge_stride + a.a_edge_offset + h];
+    }
+    for (int v = tid; v < n * DS; v += NT) dsc[v] = a.desc[(size_t)node0 * DS + v];
+    __syncthreads();   // (waits for the LDS-DMA: vmcnt(0) before the barrier)
+    for (int i = tid; i < n; i += NT)
+        for (int p = rp[i]; p < rp[i + 1]; ++p) dlc[p] = i;
+    // attention dots: wave w = head w, each node's 256-channel dot as a wave sum
+    for (int i = 0; i < n; ++i) {
+        const uint2 u = *reinterpret_cast<const uint2*>(xs + (size_t)i * HC + f0);
+        const float x0v = __uint_as_float(u.x << 16), x1v = __uint_as_float(u.x & 0xffff0000u);
+        const float x2v = __uint_as_float(u.y << 16), x3v = __uint_as_float(u.y & 0xffff0000u);
+        float s1 = (x0v * as_r[0] + x1v * as_r[1]) + (x2v * as_r[2] + x3v * as_r[3]);
+        float s2 = (x0v * ad_r[0] + x1v * ad_r[1]) + (x2v * ad_r[2] + x3v * ad_r[3]);
+        s1 = wave_sum_l0(s1);
+        s2 = wave_sum_l0(s2);
+        if (lane == 0) {
+            as_[i * H + wave] = s1;
+            ad_[i * H + wave] = s2;
+        }
+    }
+    __syncthreads();
+    for (int v = tid; v < ne * H; v += NT) {
+        const int p = v / H, h = v - p * H;
+        al[v] = leaky0(as_[cl[p] * H + h] + ad_[dlc[p] * H + h] + al[v], a.negative_slope);
+    }
+    __syncthreads();
+    for (int t = tid; t < n * H; t += NT) {
+        const int i = t / H, h = t - i * H;
+        const int p0 = rp[i], p1 = rp[i + 1];
+        float m = -__builtin_huge_valf();
+        for (int p = p0; p < p1; ++p) m = fmaxf(m, al[p * H + h]);
+        float ssum = 0.0f;
+        for (int p = p0; p < p1; ++p) {
+            const float ex = __expf(al[p * H + h] - m);
+            al[p * H + h] = ex;
+            ssum += ex;
+        }
+        ad_[t] = ssum + 1e-16f;
+    }
+    __syncthreads();
+    for (int v = tid; v < ne * H; v += NT) {
+        const int p = v / H, h = v - p * H;
+        al[v] = al[v] / ad_[dlc[p] * H + h];
+    }
+    __syncthreads();
+    // aggregation + bias + LayerNorm + regenerated residual + ReLU, NB nodes per round
+    for (int i0 = 0; i0 < n; i0 += NB) {
+        float v[NB][4];
+        float s[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int i = i0 + b;
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            if (i < n)
+                for (int p = rp[i]; p < rp[i + 1]; ++p) {
+                    const float w = al[p * H + wave];
+                    const uint2 u = *reinterpret_cast<const uint2*>(xs + (size_t)cl[p] * HC + f0);
+                    acc[0] += w * __uint_as_float(u.x << 16);
+                    acc[1] += w * __uint_as_float(u.x & 0xffff0000u);
+                    acc[2] += w * __uint_as_float(u.y << 16);
+                    acc[3] += w * __uint_as_float(u.y & 0xffff0000u);
+                }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[b][r] = acc[r] + b1[r];
+            s[b] = wave_sum_l0((v[b][0] + v[b][1]) + (v[b][2] + v[b][3]));
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) red[wave * NB + b] = s[b];
+        __syncthreads();
+        float mean[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            float t = 0.0f;
+            for (int w = 0; w < NW; ++w) t += red[w * NB + b];
+            mean[b] = t / (float)HC;
+            float q = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = v[b][r] - mean[b];
+                q += d * d;
+            }
+            s[b] = wave_sum_l0(q);
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int b = 0; b < NB; ++b) red[(NW + wave) * NB + b] = s[b];
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int i = i0 + b;
+            if (i >= n) break;
+            float t = 0.0f;
+            for (int w = 0; w < NW; ++w) t += red[(NW + w) * NB + b];
+            const float rstd = rsqrtf(t / (float)HC + a.ln_eps);
+            // layer 0's row i, channels f0..f0+3 (trx_gat_layer0_infer's expression)
+            const float* d = dsc + i * DS;
+            const float xbr[4] = {d[4 * h0], d[4 * h0 + 1], d[4 * h0 + 2], d[4 * h0 + 3]};
+            const float xr[4] = {d[4 * H0], d[4 * H0 + 1], d[4 * H0 + 2], d[4 * H0 + 3]};
+            const float mean0 = d[4 * H0 + 4], rstd0 = d[4 * H0 + 5];
+            float y[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v0 = dot4(xbr, w0[r][0], w0[r][1], w0[r][2], w0[r][3]) + b0[r];
+                const float res = dot4(xr, wp[r][0], wp[r][1], wp[r][2], wp[r][3]) + bp[r];
+                const float yy0 = (g0[r] * (rstd0 * (v0 - mean0)) + e0[r]) + res;
+                const float y0 = yy0 > 0.0f ? yy0 : 0.0f;
+                const float yy = (g1[r] * (rstd * (v[b][r] - mean[b])) + e1[r]) + y0;
+                y[r] = yy > 0.0f ? yy : 0.0f;
+            }
+            const size_t o = (size_t)(node0 + i) * HC + f0;
+            if (a.out_f32) *reinterpret_cast<float4*>(a.out_f32 + o) = make_float4(y[0], y[1], y[2], y[3]);
+            if (a.out_bf16)
+                *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.out_bf16) + o) =
+                    make_uint2(pk_bf16_l0(y[0], y[1]), pk_bf16_l0(y[2], y[3]));
+        }
     }
 }
 
@@ -266,6 +499,38 @@ hipError_t launch_gat_layer0(const trx_gat_layer0_args& a, hipStream_t stream) {
             break;
         default:
             hipLaunchKernelGGL((gat_layer0_lin_kernel<1024>), grid, dim3(256), smem, stream, a);
+            break;
+    }
+    return hipGetLastError();
+}
+
+constexpr int kMidNB = 8;
+
+size_t gat_mid_smem(const trx_gat_mid_args& a) {
+    const size_t n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges, HC = (size_t)a.heads * a.channels;
+    const size_t DS = 4 * (size_t)a.l0_heads + 8;
+    return n * HC * 2 + (n * DS + 2 * n * H + 2 * (HC / 256) * kMidNB + me * H) * 4 + (2 * me + n + 1) * 4;
+}
+
+hipError_t launch_gat_mid(const trx_gat_mid_args& a, hipStream_t stream) {
+    const int HC = a.heads * a.channels;
+    const size_t smem = gat_mid_smem(a);
+    static bool attr_set = false;
+    if (!attr_set) {  // > 64 KB of dynamic LDS at n = 32
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_mid_gen_kernel<1024, kMidNB>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    const dim3 grid(a.num_graphs);
+    switch (HC) {
+        case 256:
+            hipLaunchKernelGGL((gat_mid_gen_kernel<256, kMidNB>), grid, dim3(64), smem, stream, a);
+            break;
+        case 512:
+            hipLaunchKernelGGL((gat_mid_gen_kernel<512, kMidNB>), grid, dim3(128), smem, stream, a);
+            break;
+        default:
+            hipLaunchKernelGGL((gat_mid_gen_kernel<1024, kMidNB>), grid, dim3(256), smem, stream, a);
             break;
     }
     return hipGetLastError();

@@ -170,6 +170,8 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
 size_t gat_layer0_smem(const trx_gat_layer0_args& a);
 hipError_t launch_gat_layer0(const trx_gat_layer0_args& a, hipStream_t stream);
+size_t gat_mid_smem(const trx_gat_mid_args& a);
+hipError_t launch_gat_mid(const trx_gat_mid_args& a, hipStream_t stream);
 hipError_t launch_gat_layer0_prepare(int H, int C, const float* w0, const float* att_src, const float* att_dst,
                                      const float* bias, float* u, double* stats, hipStream_t stream);
 size_t edge_head_infer_smem(const trx_edge_head_args& a);

@@ -33,7 +33,7 @@ EXPORTS = (
     "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
     "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_gat_prologue_backward",
     "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
-    "trx_gat_layer0_infer", "trx_gat_layer0_prepare",
+    "trx_gat_layer0_infer", "trx_gat_layer0_prepare", "trx_gat_mid_infer",
 )
 
 
@@ -100,7 +100,19 @@ class TrxGatLayer0Args(ctypes.Structure):
         ("max_graph_edges", _i32), ("x0", _vp), ("w0", _vp), ("rowptr", _vp), ("col", _vp),
         ("a_edge", _vp), ("a_edge_stride", _i32), ("a_edge_offset", _i32), ("bias", _vp), ("negative_slope", _f32),
         ("ln_weight", _vp), ("ln_bias", _vp), ("ln_eps", _f32), ("wp", _vp), ("bp", _vp), ("u", _vp),
-        ("stats", _vp), ("out_f32", _vp), ("out_bf16", _vp),
+        ("stats", _vp), ("out_f32", _vp), ("out_bf16", _vp), ("desc", _vp),
+    ]
+
+
+class TrxGatMidArgs(ctypes.Structure):
+    """trx_gat_mid_args (include/trafficrl.h)."""
+    _fields_ = [
+        ("num_graphs", _i32), ("nodes_per_graph", _i32), ("heads", _i32), ("channels", _i32),
+        ("max_graph_edges", _i32), ("xh", _vp), ("rowptr", _vp), ("col", _vp),
+        ("a_edge", _vp), ("a_edge_stride", _i32), ("a_edge_offset", _i32), ("att_src", _vp), ("att_dst", _vp),
+        ("bias", _vp), ("negative_slope", _f32), ("ln_weight", _vp), ("ln_bias", _vp), ("ln_eps", _f32),
+        ("desc", _vp), ("l0_heads", _i32), ("l0_w0", _vp), ("l0_bias", _vp), ("l0_ln_weight", _vp),
+        ("l0_ln_bias", _vp), ("l0_wp", _vp), ("l0_bp", _vp), ("out_f32", _vp), ("out_bf16", _vp),
     ]
 
 
@@ -300,6 +312,7 @@ def load():
     L.trx_edge_head_infer.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp]
     L.trx_gat_layer0_infer.argtypes = [ctypes.POINTER(TrxGatLayer0Args), _vp]
     L.trx_gat_layer0_prepare.argtypes = [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.trx_gat_mid_infer.argtypes = [ctypes.POINTER(TrxGatMidArgs), _vp]
     L.trx_gat_tail_infer.argtypes = [ctypes.POINTER(TrxGatTailArgs), _vp]
     L.trx_edge_att_weights_backward.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp, _i32, _vp, _vp]
     L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
@@ -342,7 +355,7 @@ def load():
                  "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
                  "trx_episode_step", "trx_gat_layer_backward", "trx_partial_sum", "trx_gat_prologue_backward",
                  "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
-                 "trx_gat_layer0_infer", "trx_gat_layer0_prepare"):
+                 "trx_gat_layer0_infer", "trx_gat_layer0_prepare", "trx_gat_mid_infer"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

@@ -252,10 +252,13 @@ def _layer0_consts(enc, into=None):
 
 
 def layer0_infer(enc, x0: torch.Tensor, topo: Topology, a_all: torch.Tensor, offset: int,
-                 out_f32: Optional[torch.Tensor], out_bf16: Optional[torch.Tensor]):
+                 out_f32: Optional[torch.Tensor], out_bf16: Optional[torch.Tensor],
+                 desc: Optional[torch.Tensor] = None):
     """Layer 0 (GATConv 4 -> H*C + LayerNorm + relu(x + input_proj(x))) of a
     regular batch without saved intermediates: trx_gat_layer0_infer, the
-    linear form (fp32 throughout; csrc/gat_layer0.hip)."""
+    linear form (fp32 throughout; csrc/gat_layer0.hip).  `desc` [N, 4H+8]:
+    the per-node descriptor layer 1 regenerates its residual from
+    (mid_infer)."""
     L = _lib.load()
     l0, norm = enc.layers[0], enc.norms[0]
     w0, wp, bp, u, stats = prepared_layer0(enc)
@@ -271,7 +274,44 @@ def layer0_infer(enc, x0: torch.Tensor, topo: Topology, a_all: torch.Tensor, off
     a.wp, a.bp, a.u, a.stats = wp.data_ptr(), bp.data_ptr(), u.data_ptr(), stats.data_ptr()
     a.out_f32 = 0 if out_f32 is None else out_f32.data_ptr()
     a.out_bf16 = 0 if out_bf16 is None else out_bf16.data_ptr()
+    a.desc = 0 if desc is None else desc.data_ptr()
     _lib.check(L.trx_gat_layer0_infer(a, _lib.stream_ptr(x0.device)), "trx_gat_layer0_infer")
+
+
+def mid_supported(enc) -> bool:
+    """trx_gat_mid_infer limits: layer 1 a middle layer of 256-channel heads
+    (<= 4) over layer 0's width."""
+    if len(enc.layers) < 3 or not layer0_supported(enc):
+        return False
+    l0, l1 = enc.layers[0], enc.layers[1]
+    hc = l1.heads * l1.out_channels
+    return (l1.concat and l1.out_channels == 256 and l1.heads <= 4 and l1.bias is not None
+            and hc == l0.heads * l0.out_channels and (hc // l0.heads) % 4 == 0)
+
+
+def mid_infer(enc, xh: torch.Tensor, desc: torch.Tensor, topo: Topology, a_all: torch.Tensor, offset: int,
+              out_f32: Optional[torch.Tensor], out_bf16: Optional[torch.Tensor]):
+    """Layer 1 with its residual (layer 0's output) regenerated from layer 0's
+    per-node descriptor: trx_gat_mid_infer (csrc/gat_layer0.hip)."""
+    L = _lib.load()
+    l0, l1, n0, n1 = enc.layers[0], enc.layers[1], enc.norms[0], enc.norms[1]
+    w0, wp, bp, _, _ = prepared_layer0(enc)
+    a = _lib.TrxGatMidArgs()
+    a.num_graphs, a.nodes_per_graph, a.heads, a.channels = topo.B, topo.n, l1.heads, l1.out_channels
+    a.max_graph_edges = topo.max_graph_edges
+    a.xh, a.rowptr, a.col = xh.data_ptr(), topo.g.rowptr.data_ptr(), topo.g.col.data_ptr()
+    a.a_edge, a.a_edge_stride, a.a_edge_offset = a_all.data_ptr(), a_all.shape[1], offset
+    att_s, att_d = l1.att_src.detach().reshape(-1), l1.att_dst.detach().reshape(-1)
+    a.att_src, a.att_dst, a.bias = att_s.data_ptr(), att_d.data_ptr(), l1.bias.detach().data_ptr()
+    a.negative_slope = float(l1.negative_slope)
+    a.ln_weight, a.ln_bias, a.ln_eps = n1.weight.detach().data_ptr(), n1.bias.detach().data_ptr(), float(n1.eps)
+    a.desc, a.l0_heads = desc.data_ptr(), l0.heads
+    a.l0_w0, a.l0_bias = w0.data_ptr(), l0.bias.detach().data_ptr()
+    a.l0_ln_weight, a.l0_ln_bias = n0.weight.detach().data_ptr(), n0.bias.detach().data_ptr()
+    a.l0_wp, a.l0_bp = wp.data_ptr(), bp.data_ptr()
+    a.out_f32 = 0 if out_f32 is None else out_f32.data_ptr()
+    a.out_bf16 = 0 if out_bf16 is None else out_bf16.data_ptr()
+    _lib.check(L.trx_gat_mid_infer(a, _lib.stream_ptr(xh.device)), "trx_gat_mid_infer")
 
 
 def _encoder_weights(enc, layers, into=None):
@@ -393,6 +433,7 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
     stream = _lib.stream_ptr(dev)
     wts = prepared_encoder(enc, layers)
     lin0 = LAYER0_LINEAR and layer0_supported(enc)
+    mid = lin0 and mid_supported(enc)
     prev_f32, prev_bf16 = None, None
     emb = ctx = None
     for i, l in enumerate(layers):
@@ -406,8 +447,17 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
         keep = []
         if i == 0 and lin0:   # linear-form layer 0 (csrc/gat_layer0.hip)
             out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
-            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if len(layers) > 2 else None
-            layer0_infer(enc, x, topo, a_all, offs[0], out_f32, out_bf16)
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if len(layers) > 2 and not mid else None
+            desc = torch.empty(N, 4 * l.heads + 8, device=dev, dtype=torch.float32) if mid else None
+            layer0_infer(enc, x, topo, a_all, offs[0], out_f32, out_bf16, desc)
+            prev_f32, prev_bf16 = out_f32, out_bf16
+            emb = out_bf16
+            continue
+        if i == 1 and mid:    # layer 1, residual regenerated from layer 0's descriptor
+            xh = F.linear(prev_bf16, wts[1])
+            out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if i + 1 < len(layers) - 1 else None
+            mid_infer(enc, xh, desc, topo, a_all, offs[1], out_f32, out_bf16)
             prev_f32, prev_bf16 = out_f32, out_bf16
             emb = out_bf16
             continue

@@ -93,6 +93,8 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     N = x0.shape[0]
     stride = a_all.shape[1]
     wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
+    lin0 = not save and fused.LAYER0_LINEAR and fused.layer0_supported(enc)
+    mid = lin0 and fused.mid_supported(enc)
     keep = []
     recs = []
     prev_f32 = prev_bf16 = None
@@ -104,11 +106,21 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         norm = enc.norms[i]
         args = _layer_args(l, norm, topo, a_all, off, stride, i, last)
         rec = {"off": off, "heads": l.heads, "channels": l.out_channels}
-        if i == 0 and not save and fused.LAYER0_LINEAR and fused.layer0_supported(enc):
+        if i == 0 and lin0:
             # no-grad passes: the linear-form layer 0 (csrc/gat_layer0.hip)
             out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
-            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if len(layers) > 2 else None
-            fused.layer0_infer(enc, x0, topo, a_all, off, out_f32, out_bf16)
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if len(layers) > 2 and not mid else None
+            desc = torch.empty(N, 4 * l.heads + 8, device=dev, dtype=torch.float32) if mid else None
+            fused.layer0_infer(enc, x0, topo, a_all, off, out_f32, out_bf16, desc)
+            recs.append(rec)
+            prev_f32, prev_bf16 = out_f32, out_bf16
+            off += l.heads
+            continue
+        if i == 1 and mid:   # layer 1 with the regenerated residual
+            xh = F.linear(prev_bf16, wts[i])
+            out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+            out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32) if i + 1 < len(layers) - 1 else None
+            fused.mid_infer(enc, xh, desc, topo, a_all, off, out_f32, out_bf16)
             recs.append(rec)
             prev_f32, prev_bf16 = out_f32, out_bf16
             off += l.heads

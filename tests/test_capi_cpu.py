@@ -169,7 +169,8 @@ def test_fused_args_layout_matches_header(tmp_path):
     from trafficrl import _lib
     lines = []
     structs = (("trx_gat_layer_args", _lib.TrxGatLayerArgs), ("trx_edge_head_args", _lib.TrxEdgeHeadArgs),
-               ("trx_gat_prologue_args", _lib.TrxGatPrologueArgs), ("trx_gat_layer0_args", _lib.TrxGatLayer0Args))
+               ("trx_gat_prologue_args", _lib.TrxGatPrologueArgs), ("trx_gat_layer0_args", _lib.TrxGatLayer0Args),
+               ("trx_gat_mid_args", _lib.TrxGatMidArgs))
     for cname, cls in structs:
         lines.append(f'printf("%zu\\n", sizeof({cname}));')
         for f, _ in cls._fields_:

@@ -321,3 +321,55 @@ def test_actor_layer0_kernels_agree():
     span = (l0[valid].max() - l0[valid].min()).item()
     assert (l1[valid] - l0[valid]).abs().max().item() <= 0.02 * span + 1e-3
     assert (p1 - p0).abs().max().item() < 1e-2
+
+
+def test_mid_layer_regenerated_residual_matches_stored_residual():
+    """trx_gat_mid_infer (layer 1 with layer 0's output regenerated from the
+    per-node descriptor) against trx_gat_layer_infer fed with layer 0's
+    float32 rows from HBM: the same function, the LayerNorm sums taken in
+    another order -- within 1e-5 of the row scale (bf16 outputs within one
+    bf16 ulp)."""
+    import torch.nn.functional as F
+    from trafficrl import _lib
+    from trafficrl.models import fused
+    from trafficrl.rl.sac import Actor
+    torch.manual_seed(17)
+    actor = Actor(4, 6, 256, 256, 3).cuda()
+    enc = actor.encoder
+    assert fused.mid_supported(enc)
+    node_x, ei, ea, mask, bv, B, E = _obs_batch(seed=23)
+    L = _lib.load()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        topo = fused.topology(ei, bv, B)
+        x0, eaf, a_all = fused.prologue(actor, node_x, ea, topo)
+        N = x0.shape[0]
+        y0 = torch.empty(N, 1024, device="cuda")
+        y0b = torch.empty(N, 1024, device="cuda", dtype=torch.bfloat16)
+        desc = torch.empty(N, 24, device="cuda")
+        fused.layer0_infer(enc, x0, topo, a_all, 0, y0, y0b, desc)
+        w1 = fused.prepared_encoder(enc, list(enc.layers))[1]
+        xh = F.linear(y0b, w1)
+        got32 = torch.empty(N, 1024, device="cuda")
+        got16 = torch.empty(N, 1024, device="cuda", dtype=torch.bfloat16)
+        fused.mid_infer(enc, xh, desc, topo, a_all, 4, got32, got16)
+        # the round-3 layer kernel with the stored float32 residual
+        l1, n1 = enc.layers[1], enc.norms[1]
+        args = _lib.TrxGatLayerArgs()
+        args.num_graphs, args.nodes_per_graph, args.heads, args.channels = B, topo.n, l1.heads, l1.out_channels
+        args.concat, args.max_graph_edges, args.in_dim, args.xh = 1, topo.max_graph_edges, 0, xh.data_ptr()
+        args.rowptr, args.col = topo.g.rowptr.data_ptr(), topo.g.col.data_ptr()
+        args.a_edge, args.a_edge_stride, args.a_edge_offset = a_all.data_ptr(), a_all.shape[1], 4
+        keep = [l1.att_src.detach().reshape(-1).contiguous(), l1.att_dst.detach().reshape(-1).contiguous()]
+        args.att_src, args.att_dst, args.bias = keep[0].data_ptr(), keep[1].data_ptr(), l1.bias.detach().data_ptr()
+        args.negative_slope = float(l1.negative_slope)
+        args.ln_weight, args.ln_bias, args.ln_eps = n1.weight.detach().data_ptr(), n1.bias.detach().data_ptr(), n1.eps
+        args.residual, args.res, args.activation = 1, y0.data_ptr(), 0
+        ref32 = torch.empty(N, 1024, device="cuda")
+        args.out_f32 = ref32.data_ptr()
+        _lib.check(L.trx_gat_layer_infer(args, _lib.stream_ptr(y0.device)), "trx_gat_layer_infer")
+    torch.cuda.synchronize()
+    scale = ref32.abs().amax(1, keepdim=True).clamp(min=1e-3)
+    err = ((got32 - ref32).abs() / scale).max().item()
+    print(f"mid layer: max error / row scale {err:.2e}")
+    assert err < 1e-5
+    torch.testing.assert_close(got16, got32.to(torch.bfloat16), rtol=0, atol=0)
