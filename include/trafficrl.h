@@ -397,14 +397,16 @@ int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream);
 /* Backward of the edge scorer's logits (softmax = 0) for training, one
  * workgroup per graph (hidden <= 256): from grad_logits [B*E] float32 and the
  * same args (p, c, ea, we, w2, src, dst, nodes_per_graph) it writes grad_p
- * [N, 2H] bf16 (fp32 sums over the graph's links, rounded once), grad_c [B, H]
- * float32, grad_z [B*E, H] bf16 (the gradient at the link pre-activation: the
- * link-feature weight and input gradients are bf16 GEMMs of it) and
- * grad_w2_part [B, H] float32 (per-graph partial sums of the 256->1 weight
- * gradient).  fp32 after the p GEMM, as the forward (and the general path of
- * trafficrl/rl/sac.py _EdgeHead.edge_scores). */
+ * [N, 2H] bf16 (fp32 sums over the graph's links, rounded once), grad_c
+ * [B, H] float32, grad_w2_part [B, H] float32 (per-graph partial sums of the
+ * 256->1 weight gradient), grad_we_part [B, H, edge_dim] float32 (per-graph
+ * partial sums of the link-feature weight gradient) and grad_ea [B*E,
+ * edge_dim] float32 (the link features' gradient); grad_z [B*E, H] bf16 (the
+ * gradient at the link pre-activation) only when non-NULL.  fp32 after the p
+ * GEMM, as the forward (and the general path of trafficrl/rl/sac.py
+ * _EdgeHead.edge_scores). */
 int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
-                           void* grad_z, float* grad_w2_part, void* stream);
+                           void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea, void* stream);
 
 /* Input stage of Actor/Critic (src/rl/sac.py:36-37) plus every layer's edge
  * attention logits (src/models/gat_encoder.py:36-52: PyG GATConv with

@@ -786,7 +786,7 @@ int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
 }
 
 int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
-                           void* grad_z, float* grad_w2_part, void* stream) {
+                           void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea, void* stream) {
     if (!a) return fail(TRX_EINVAL, "edge_head_backward: NULL args");
     if (a->num_graphs < 0 || a->edges_per_graph < 1 || a->edges_per_graph > 4096)
         return fail(TRX_EUNSUP, "edge_head_backward: edges_per_graph must be 1..4096");
@@ -795,11 +795,11 @@ int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits
     if (a->nodes_per_graph < 1 || trx::edge_head_bwd_smem(*a) > 160 * 1024)
         return fail(TRX_EUNSUP, "edge_head_backward: graph too large for LDS (nodes_per_graph, edges_per_graph)");
     if (!a->src || !a->dst || !a->p || !a->c || !a->ea || !a->we || !a->w2 || !grad_logits || !grad_p || !grad_c ||
-        !grad_z || !grad_w2_part)
+        !grad_w2_part || !grad_we_part || !grad_ea)
         return fail(TRX_EINVAL, "edge_head_backward: NULL buffer");
     if (a->num_graphs == 0) return TRX_OK;
-    hipError_t e = trx::launch_edge_head_bwd(*a, grad_logits, grad_p, grad_c, grad_z, grad_w2_part,
-                                             static_cast<hipStream_t>(stream));
+    hipError_t e = trx::launch_edge_head_bwd(*a, grad_logits, grad_p, grad_c, grad_z, grad_w2_part, grad_we_part,
+                                             grad_ea, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "edge_head_backward launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }

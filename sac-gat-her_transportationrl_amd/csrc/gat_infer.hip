@@ -922,14 +922,17 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 // grad_c / grad_w2 sums added in part order; (2) per node (nodes dealt to the
 // parts), the sums over its out-links (p[:, :H]) and in-links (p[:, H:]) in
 // link order.
-// Outputs: grad_p [N, 2H] bf16, grad_c [B, H], grad_z [E_total, H] bf16 (for
-// the link-feature weight / input gradients, bf16 GEMMs on the host side) and
-// grad_w2_part [B, H] (per-graph sums of g * relu(z)).
+// Outputs: grad_p [N, 2H] bf16, grad_c [B, H], grad_w2_part [B, H] (per-graph
+// sums of g * relu(z)), and the link-feature block in fp32 like its forward:
+// grad_we_part [B, H, D] (per-graph sums of dz * ea, links in order) and
+// grad_ea [E_total, D] (dz . we per link: (3), one wave per link, wave sums);
+// grad_z [E_total, H] bf16 (dz) only when asked for.
 constexpr int kEhbThreads = 1024, kEhbParts = kEhbThreads / 256;
 
 __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
                                                                     uint16_t* grad_p, float* grad_c,
-                                                                    uint16_t* grad_z, float* grad_w2_part) {
+                                                                    uint16_t* grad_z, float* grad_w2_part,
+                                                                    float* grad_we_part, float* grad_ea) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int ED = kEdgeED, NT = kEhbThreads, P = kEhbParts;
     const int g = blockIdx.x, tid = threadIdx.x, k = tid & 255, part = tid >> 8;
@@ -938,8 +941,9 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
     float* dzs = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);     // [E][Hd] dL/dz (n*2*Hd even)
     float* eal = dzs + (size_t)E * Hd;                                  // [E][ED] link features
     float* gl = eal + (size_t)E * ED;                                   // [E] grad logit
-    float* red = gl + E;                                                // [P][2][256] per-part sums
-    int* sl = reinterpret_cast<int*>(red + P * 2 * 256);                // [E]
+    float* red = gl + E;                                                // [P][2 + ED][256] per-part sums
+    float* wes = red + P * (2 + ED) * 256;                              // [256][ED] link-feature weights
+    int* sl = reinterpret_cast<int*>(wes + 256 * ED);                   // [E]
     int* dl = sl + E;                                                   // [E]
     int* lo = dl + E;                                                   // [E] links by source node, link order
     int* li = lo + E;                                                   // [E] links by destination node
@@ -968,6 +972,9 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
     float we[ED];
 #pragma unroll
     for (int j = 0; j < ED; ++j) we[j] = (on && j < D) ? a.we[k * D + j] : 0.0f;
+    if (part == 0)
+#pragma unroll
+        for (int j = 0; j < ED; ++j) wes[k * ED + j] = we[j];
     const float w2 = on ? a.w2[k] : 0.0f, ck = on ? a.c[(int64_t)g * Hd + k] : 0.0f;
     __syncthreads();
     if (tid < n) {  // per-node link lists (link order); counts first
@@ -994,7 +1001,9 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
             if (dl[e] == tid) li[wi++] = e;
         }
     }
-    float gc = 0.0f, gw2 = 0.0f;
+    float gc = 0.0f, gw2 = 0.0f, gwe[ED];
+#pragma unroll
+    for (int j = 0; j < ED; ++j) gwe[j] = 0.0f;
     if (on) {  // (1) per link
         for (int e = part; e < E; e += P) {
             const int s = sl[e], d = dl[e];
@@ -1007,22 +1016,48 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
             gw2 += gb * fmaxf(z, 0.0f);
             const float dz = z > 0.0f ? gb * w2 : 0.0f;
             gc += dz;
-            grad_z[((int64_t)g * E + e) * Hd + k] = f2bf(dz);
+#pragma unroll
+            for (int j = 0; j < ED; ++j) gwe[j] += dz * eal[e * ED + j];
+            if (grad_z) grad_z[((int64_t)g * E + e) * Hd + k] = f2bf(dz);
             dzs[e * Hd + k] = dz;
         }
     }
-    red[(part * 2 + 0) * 256 + k] = gc;
-    red[(part * 2 + 1) * 256 + k] = gw2;
+    constexpr int RS = 2 + ED;  // per-part rows: grad_c, grad_w2, grad_we[ED]
+    red[(part * RS + 0) * 256 + k] = gc;
+    red[(part * RS + 1) * 256 + k] = gw2;
+#pragma unroll
+    for (int j = 0; j < ED; ++j) red[(part * RS + 2 + j) * 256 + k] = gwe[j];
     __syncthreads();
     if (on && part == 0) {
-        float tc = red[k], tw = red[256 + k];
+        float t[RS];
 #pragma unroll
-        for (int q = 1; q < P; ++q) {
-            tc += red[(q * 2) * 256 + k];
-            tw += red[(q * 2 + 1) * 256 + k];
+        for (int r = 0; r < RS; ++r) t[r] = red[r * 256 + k];
+#pragma unroll
+        for (int q = 1; q < P; ++q)
+#pragma unroll
+            for (int r = 0; r < RS; ++r) t[r] += red[(q * RS + r) * 256 + k];
+        grad_c[(int64_t)g * Hd + k] = t[0];
+        grad_w2_part[(int64_t)g * Hd + k] = t[1];
+        for (int j = 0; j < D; ++j) grad_we_part[((int64_t)g * Hd + k) * D + j] = t[2 + j];
+    }
+    // (3) per link: grad_ea[e, j] = sum_k dz[e, k] we[k, j], one wave per link
+    {
+        const int wv = tid >> 6, ln = tid & 63;
+        for (int e = wv; e < E; e += NT / 64) {
+            float s[ED];
+#pragma unroll
+            for (int j = 0; j < ED; ++j) s[j] = 0.0f;
+            for (int kk = ln; kk < Hd; kk += 64) {
+                const float dz = dzs[e * Hd + kk];
+#pragma unroll
+                for (int j = 0; j < ED; ++j) s[j] += dz * wes[kk * ED + j];
+            }
+#pragma unroll
+            for (int j = 0; j < ED; ++j) {
+                const float t = wave_sum_f(s[j]);
+                if (ln == 0 && j < D) grad_ea[((int64_t)g * E + e) * D + j] = t;
+            }
         }
-        grad_c[(int64_t)g * Hd + k] = tc;
-        grad_w2_part[(int64_t)g * Hd + k] = tw;
     }
     if (on)  // (2) per node: out-links feed p[:, :H], in-links p[:, H:]
         for (int i = part; i < n; i += P) {
@@ -1036,11 +1071,13 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
 
 size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
     const size_t n = a.nodes_per_graph, E = a.edges_per_graph, H = a.hidden;
-    return n * 2 * H * 2 + E * H * 4 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * 2 * 256 * 4 + 2 * (n + 1) * 4;
+    return n * 2 * H * 2 + E * H * 4 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * (2 + kEdgeED) * 256 * 4 +
+           256 * kEdgeED * 4 + 2 * (n + 1) * 4;
 }
 
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
-                                void* grad_z, float* grad_w2_part, hipStream_t stream) {
+                                void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea,
+                                hipStream_t stream) {
     const size_t smem = edge_head_bwd_smem(a);
     if (smem > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(edge_head_bwd_kernel),
@@ -1048,7 +1085,8 @@ hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_l
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(edge_head_bwd_kernel, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
-                       static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part);
+                       static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part,
+                       grad_we_part, grad_ea);
     return hipGetLastError();
 }
 

@@ -180,7 +180,8 @@ int gat_tail_mtiles(int nodes_per_graph);
 hipError_t launch_gat_tail_infer(const trx_gat_tail_args& a, hipStream_t stream);
 size_t edge_head_bwd_smem(const trx_edge_head_args& a);
 hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
-                                void* grad_z, float* grad_w2_part, hipStream_t stream);
+                                void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea,
+                                hipStream_t stream);
 int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
 int small_ln_blocks(int N);

@@ -316,7 +316,7 @@ def load():
     L.trx_gat_tail_infer.argtypes = [ctypes.POINTER(TrxGatTailArgs), _vp]
     L.trx_edge_att_weights_backward.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp, _i32, _vp, _vp]
     L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
-    L.trx_edge_head_backward.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp, _vp, _vp, _vp, _vp, _vp]
+    L.trx_edge_head_backward.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.trx_graph_pool_forward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp]
     L.trx_bf16_round.argtypes = [ctypes.POINTER(TrxRoundList), _vp]
     L.trx_multi_copy.argtypes = [ctypes.POINTER(TrxCopyList), _vp]

@@ -675,16 +675,17 @@ class _EdgeScores(torch.autograd.Function):
         B, n, E = ctx.dims
         H = we.shape[0]
         g = g.float().contiguous()
+        D = we.shape[1]
         grad_p = torch.empty_like(p)
         grad_c = torch.empty(B, H, device=p.device, dtype=torch.float32)
-        grad_z = torch.empty(B * E, H, device=p.device, dtype=torch.bfloat16)
         gw2 = torch.empty(B, H, device=p.device, dtype=torch.float32)
+        gwe = torch.empty(B, H, D, device=p.device, dtype=torch.float32)
+        g_ea = torch.empty(B * E, D, device=p.device, dtype=torch.float32)   # the link features' gradient
         a = _edge_args(p, c, ea, we, w2, b2r, src32, dst32, B, n, E)
-        _lib.check(L.trx_edge_head_backward(a, _lib.ptr(g), _lib.ptr(grad_p), _lib.ptr(grad_c), _lib.ptr(grad_z),
-                                            _lib.ptr(gw2), _lib.stream_ptr(p.device)), "trx_edge_head_backward")
-        from .skinny import _splitk_wgrad
-        g_ea = (grad_z @ we.to(torch.bfloat16)).float()                     # skinny_linear's dx (bf16 GEMM)
-        g_we = _splitk_wgrad(grad_z, ea.to(torch.bfloat16))                  # and its split-K fp32 dW
+        _lib.check(L.trx_edge_head_backward(a, _lib.ptr(g), _lib.ptr(grad_p), _lib.ptr(grad_c), None,
+                                            _lib.ptr(gw2), _lib.ptr(gwe), _lib.ptr(g_ea),
+                                            _lib.stream_ptr(p.device)), "trx_edge_head_backward")
+        g_we = gwe.sum(0)                                                    # fp32 link-feature weight gradient
         g_w2 = gw2.sum(0).view(1, H)
         g_b2 = g.sum(0).view(1)
         return grad_p, grad_c, g_ea, g_we, g_w2, g_b2, None, None, None, None

@@ -230,16 +230,17 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     Hd = wn.shape[0] // 2
     # ---- edge scorer (sac.py:42-44 factored): kernel + link-feature / weight products
     a = fused._edge_args(cx.p, cx.c, cx.ea, we, w2, b2, topo.src32, topo.dst32, B, n, e)
+    k = we.shape[1]
     g_p = torch.empty_like(cx.p)
     g_c = torch.empty(B, Hd, device=dev, dtype=torch.float32)
-    g_z = torch.empty(B * e, Hd, device=dev, dtype=torch.bfloat16)
     gw2p = torch.empty(B, Hd, device=dev, dtype=torch.float32)
+    gwep = torch.empty(B, Hd * k, device=dev, dtype=torch.float32)      # per-graph link-feature weight partials
+    g_ea_head = torch.empty(B * e, k, device=dev, dtype=torch.float32)   # link features' gradient (fp32)
     gl = g_logits.contiguous()
-    _lib.check(L.trx_edge_head_backward(a, _lib.ptr(gl), _lib.ptr(g_p), _lib.ptr(g_c), _lib.ptr(g_z),
-                                        _lib.ptr(gw2p), stream), "trx_edge_head_backward")
-    ea_b = cx.ea.to(torch.bfloat16)
-    g_we = _splitk_wgrad(g_z, ea_b)                                     # [H, k] fp32
-    g_ea_head = (g_z @ we.to(torch.bfloat16)).float()                   # [B*e, k]
+    _lib.check(L.trx_edge_head_backward(a, _lib.ptr(gl), _lib.ptr(g_p), _lib.ptr(g_c), None, _lib.ptr(gw2p),
+                                        _lib.ptr(gwep), _lib.ptr(g_ea_head), stream), "trx_edge_head_backward")
+    g_we = torch.empty(Hd, k, device=dev, dtype=torch.float32)
+    _lib.check(L.trx_partial_sum(_lib.ptr(gwep), B, Hd * k, Hd * k, _lib.ptr(g_we), stream), "trx_partial_sum")
     g_wn = _splitk_wgrad(g_p, cx.emb)                                   # [2H, embed] fp32
     g_emb = g_p @ wn                                                    # bf16 [N, embed]
     g_cb = g_c.to(torch.bfloat16)
