@@ -313,7 +313,7 @@ int trx_gat_mid_infer(const trx_gat_mid_args* a, void* stream);
 /* u [2*heads*4] float32 and stats [heads*24 + 2] float64 of one weight set:
  * per head h (channels c of h, in order) s_h = sum W0[c], t_h = sum b_c W0[c],
  * G_h = sum W0[c] W0[c]^T (4x4 row-major) at stats[24h + 0/4/8], then
- * sum b_c and sum b_c^2.  One workgroup. */
+ * sum b_c and sum b_c^2.  heads + 1 workgroups, fixed-order float64 sums. */
 int trx_gat_layer0_prepare(int32_t heads, int32_t channels, const float* w0, const float* att_src,
                            const float* att_dst, const float* bias, float* u, double* stats, void* stream);
 

@@ -438,44 +438,68 @@ __global__ void __launch_bounds__(HC / 4) gat_mid_gen_kernel(trx_gat_mid_args a)
 
 // Per-weight-set constants: u = [W0_h^T att_src_h ; W0_h^T att_dst_h] (float32
 // [2, H, 4], from float64 sums) and the LayerNorm forms (float64, layout above).
-// One workgroup of 256 threads; thread (h, q) sums one quantity over the head's
-// C channels in channel order.
+// One workgroup per head (+ one for the bias sums): each thread forms its
+// channels' 32 products (4 u_src, 4 u_dst, 4 s, 4 t, 16 G) in float64, then
+// a fixed-order tree reduction over the workgroup (deterministic).
 __global__ void __launch_bounds__(256) gat_layer0_prepare_kernel(int H, int C, const float* __restrict__ w0,
                                                                   const float* __restrict__ att_src,
                                                                   const float* __restrict__ att_dst,
                                                                   const float* __restrict__ bias, float* __restrict__ u,
                                                                   double* __restrict__ stats) {
-    // quantities per head: 4 u_src + 4 u_dst + 4 s + 4 t + 16 G = 32
-    for (int t = threadIdx.x; t < H * 32 + 2; t += blockDim.x) {
-        double acc = 0.0;
-        if (t >= H * 32) {
-            for (int c = 0; c < H * C; ++c) {
+    __shared__ double red[256];
+    const int tid = threadIdx.x, h = blockIdx.x;
+    if (h == H) {  // sum b, sum b^2 over all channels
+        for (int q = 0; q < 2; ++q) {
+            double acc = 0.0;
+            for (int c = tid; c < H * C; c += 256) {
                 const double b = bias[c];
-                acc += t == H * 32 ? b : b * b;
+                acc += q == 0 ? b : b * b;
             }
-            stats[H * 24 + (t - H * 32)] = acc;
-            continue;
+            red[tid] = acc;
+            __syncthreads();
+            for (int w = 128; w > 0; w >>= 1) {
+                if (tid < w) red[tid] += red[tid + w];
+                __syncthreads();
+            }
+            if (tid == 0) stats[H * 24 + q] = red[0];
+            __syncthreads();
         }
-        const int h = t / 32, q = t - h * 32;
-        for (int c = h * C; c < (h + 1) * C; ++c) {
-            const float* wr = w0 + (size_t)c * 4;
+        return;
+    }
+    double acc[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) acc[q] = 0.0;
+    for (int c = h * C + tid; c < (h + 1) * C; c += 256) {
+        const float4 wv = *reinterpret_cast<const float4*>(w0 + (size_t)c * 4);
+        const double w[4] = {wv.x, wv.y, wv.z, wv.w};
+        const double as = att_src[c], ad = att_dst[c], b = bias[c];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            acc[k] += w[k] * as;
+            acc[4 + k] += w[k] * ad;
+            acc[8 + k] += w[k];
+            acc[12 + k] += b * w[k];
+#pragma unroll
+            for (int l = 0; l < 4; ++l) acc[16 + 4 * k + l] += w[k] * w[l];
+        }
+    }
+    for (int q = 0; q < 32; ++q) {
+        red[tid] = acc[q];
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (tid < w) red[tid] += red[tid + w];
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const double v = red[0];
             if (q < 4)
-                acc += (double)wr[q] * (double)att_src[c];
+                u[4 * h + q] = (float)v;
             else if (q < 8)
-                acc += (double)wr[q - 4] * (double)att_dst[c];
-            else if (q < 12)
-                acc += (double)wr[q - 8];
-            else if (q < 16)
-                acc += (double)bias[c] * (double)wr[q - 12];
+                u[4 * (H + h) + q - 4] = (float)v;
             else
-                acc += (double)wr[(q - 16) >> 2] * (double)wr[(q - 16) & 3];
+                stats[24 * h + (q - 8)] = v;
         }
-        if (q < 4)
-            u[4 * h + q] = (float)acc;
-        else if (q < 8)
-            u[4 * (H + h) + q - 4] = (float)acc;
-        else
-            stats[24 * h + (q - 8)] = acc;
+        __syncthreads();
     }
 }
 
@@ -538,8 +562,8 @@ hipError_t launch_gat_mid(const trx_gat_mid_args& a, hipStream_t stream) {
 
 hipError_t launch_gat_layer0_prepare(int H, int C, const float* w0, const float* att_src, const float* att_dst,
                                      const float* bias, float* u, double* stats, hipStream_t stream) {
-    hipLaunchKernelGGL(gat_layer0_prepare_kernel, dim3(1), dim3(256), 0, stream, H, C, w0, att_src, att_dst, bias, u,
-                       stats);
+    hipLaunchKernelGGL(gat_layer0_prepare_kernel, dim3(H + 1), dim3(256), 0, stream, H, C, w0, att_src, att_dst, bias,
+                       u, stats);
     return hipGetLastError();
 }
 

@@ -65,12 +65,15 @@ for s in "$@"; do
                 python tools/pmc_summary.py r04_sf "pmcenv_p*" env_kernel > gpurun_out/pmcenv_summary.log 2>&1
                 cp profiles/r04_sf_pmc.json gpurun_out/; rm -rf gpurun_out/pmcenv_p* ;;
         pmcact) pmc4 pmcact python3 tools/agent_profile.py 4096 act &&
-                python tools/pmc_summary.py r04_act "pmcact_p*" gat_layer_infer edge_head gat_prologue Cijk > gpurun_out/pmcact_summary.log 2>&1
+                python tools/pmc_summary.py r04_act "pmcact_p*" gat_layer gat_mid edge_head gat_prologue Cijk > gpurun_out/pmcact_summary.log 2>&1
                 cp profiles/r04_act_pmc.json gpurun_out/; rm -rf gpurun_out/pmcact_p* ;;
         pmcupd) pmc4 pmcupd python3 tools/agent_profile.py 4096 update &&
                 python tools/pmc_summary.py r04_upd "pmcupd_p*" trx:: Cijk > gpurun_out/pmcupd_summary.log 2>&1
                 cp profiles/r04_upd_pmc.json gpurun_out/; rm -rf gpurun_out/pmcupd_p* ;;
         stamps) step stamps 300 python tools/phase_stamps.py 4096 ;;
+        stampsrand)
+                    step stamps_rand 300 env TRX_DAMAGE=random python tools/phase_stamps.py 4096 &&
+                    step stamps_rand_reset 300 env TRX_DAMAGE=random TRX_STAMP_RESET=1 python tools/phase_stamps.py 4096 ;;
         epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --workload env --steps 44 --warmup 22 --no-cpu; done ;;
         gattests) step gat_tests 400 python -m pytest tests/test_gat_infer.py tests/test_gat.py tests/test_sac.py -x -q ;;
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;

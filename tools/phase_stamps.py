@@ -27,7 +27,16 @@ from trafficrl.data import sioux_falls  # noqa: E402
 from trafficrl.env import VecRepairEnv  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=True, fixed_damage_seed=42)
+RANDOM = os.environ.get("TRX_DAMAGE", "fixed") == "random"   # per-env default_rng(1000 + i) damage
+env = VecRepairEnv(sioux_falls(), B, assignment_iters=30, fixed_damage=not RANDOM, fixed_damage_seed=42,
+                   seeds=[1000 + i for i in range(B)])
+if os.environ.get("TRX_STAMP_RESET"):   # time the cold reset instead of warm-started steps
+    L.trx_debug_phase_cycles(buf := (ctypes.c_ulonglong * 8)(), 1)
+    env.reset(observe=False)
+    torch.cuda.synchronize()
+    L.trx_debug_phase_cycles(buf, 1)
+    print("reset: replayed trees (wave 0 of each workgroup):", buf[7], "of", (B // 2) * 30 * 16, "tree-iterations")
+    print("reset cycles by phase:", [buf[i] for i in range(7)])
 buf = (ctypes.c_ulonglong * 8)()
 L.trx_debug_phase_cycles(buf, 1)
 gen = torch.Generator(device="cuda").manual_seed(0)

@@ -50,7 +50,7 @@ def short_name(kernel_name):
 def mangled_key(short):
     """Mangled-name substring of a trx:: kernel: 'trx::k<24, 2>' -> '1kILi24ELi2EE'
     (length-prefixed identifier + integer template arguments)."""
-    m = re.match(r"(?:trx::)?(\w+)(?:<(.*)>)?$", short)
+    m = re.match(r"(?:trx::)?(?:\(anonymous namespace\)::)?(\w+)(?:<(.*)>)?$", short)
     if not m:
         return None
     name, targs = m.group(1), m.group(2)
