@@ -178,12 +178,23 @@ __device__ __forceinline__ void read_keys(const uint64_t* row, uint64_t (&m)[NPL
     }
 }
 
+// Fibonacci-heap storage of one replay sized for NP nodes, carved from the
+// wave's key rows in LDS (dead between the Dijkstra and the subtree pass).
+template <int NPX>
+struct FibSmall {
+    using idx_t = int8_t;
+    double val[NPX];
+    int8_t parent[NPX], left[NPX], right[NPX], child[NPX];
+    uint8_t rank[NPX], state[NPX];
+    int8_t roots[32];
+};
+
 // The exact scipy-heap replay of one ambiguous tree (rare: out of line so the
 // Dijkstra loop's registers are not sized for it); writes scan order and preds.
 template <int NP>
 __device__ __noinline__ void replay_tree_s(int N, const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-                                           const int16_t* __restrict__ eid_of, const float* stl, int origin, FibLane* h,
-                                           uint8_t* ol, uint8_t* pl) {
+                                           const int16_t* __restrict__ eid_of, const float* stl, int origin,
+                                           FibSmall<NP>* h, uint8_t* ol, uint8_t* pl) {
     exact_sssp(N, indptr, indices, [stl, eid_of](int a_, int b_) { return stl[eid_of[a_ * NP + b_]]; }, origin, h, ol,
                pl, 1, 0);
 }
@@ -472,14 +483,32 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
 #endif
             if (need) {  // wave-uniform: exact scipy-heap replays of the ambiguous trees
                 const float* const stl = st + lenv * E;
-                // every ambiguous tree's quad leader replays its own tree at once, each
-                // with its own heap in the caller's workspace (global memory, one
-                // FibLane per tree): cold resets with random damage are tie-heavy
-                // (most trees of a wave ambiguous), so one tree at a time serialised them
-                FibLane* const h = reinterpret_cast<FibLane*>(
-                    ws + ((size_t)blockIdx.x * (size_t)(L >> 2) + (size_t)(tid >> 2)) * sizeof(FibLane));
-                if ((need >> (tid & 63)) & 1ull) replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
-                wave_sync_s();
+                // the ambiguous trees' quad leaders replay their trees concurrently, each with
+                // its own heap in LDS: the wave's 16 key rows (16 * NP * 8 bytes, dead until the
+                // subtree pass re-initialises them) hold kSlots heaps, so up to kSlots trees per
+                // round.  (A heap in global memory cost ~1 ms of dependent misses per replay,
+                // and a single replay held the whole launch.)
+                constexpr int kHeapBytes = (int)((sizeof(FibSmall<NP>) + 7) & ~(size_t)7);
+                constexpr int kSlots = (16 * NP * 8) / kHeapBytes;
+                static_assert(kSlots >= 1, "replay heap does not fit the wave's key rows");
+                unsigned char* const area = reinterpret_cast<unsigned char*>(skeys + (size_t)(tid >> 6) * 16 * NP);
+                const int lane = tid & 63;
+                uint64_t pend = need;
+                while (pend) {  // wave-uniform
+                    uint64_t batch = 0, m = pend;
+                    for (int c = 0; c < kSlots && m; ++c) {
+                        const uint64_t b = m & (~m + 1);
+                        batch |= b;
+                        m ^= b;
+                    }
+                    pend &= ~batch;
+                    if ((batch >> lane) & 1ull) {
+                        const int slot = __popcll(batch & ((1ull << lane) - 1ull));
+                        FibSmall<NP>* const h = reinterpret_cast<FibSmall<NP>*>(area + slot * kHeapBytes);
+                        replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
+                    }
+                    wave_sync_s();
+                }
             }
             // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree
             // demand sums S(v) per tree in reverse scan order, once final added to

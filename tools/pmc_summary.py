@@ -35,7 +35,7 @@ LIB = os.path.join(ROOT, "sac-gat-her_transportationrl_amd", "trafficrl", "libtr
 
 def short_name(kernel_name):
     """'void trx::env_kernel_s<24, 2>(trx::DevGraph, ...)' -> 'trx::env_kernel_s<24, 2>'."""
-    s = kernel_name.replace("void ", "", 1)
+    s = kernel_name.replace("void ", "", 1).replace("(anonymous namespace)::", "")
     depth = 0
     for i, ch in enumerate(s):
         if ch == "<":
@@ -50,7 +50,7 @@ def short_name(kernel_name):
 def mangled_key(short):
     """Mangled-name substring of a trx:: kernel: 'trx::k<24, 2>' -> '1kILi24ELi2EE'
     (length-prefixed identifier + integer template arguments)."""
-    m = re.match(r"(?:trx::)?(?:\(anonymous namespace\)::)?(\w+)(?:<(.*)>)?$", short)
+    m = re.match(r"(?:trx::)?(\w+)(?:<(.*)>)?$", short)
     if not m:
         return None
     name, targs = m.group(1), m.group(2)
