@@ -191,12 +191,49 @@ struct FibSmall {
 
 // The exact scipy-heap replay of one ambiguous tree (rare: out of line so the
 // Dijkstra loop's registers are not sized for it); writes scan order and preds.
-template <int NP>
-__device__ __noinline__ void replay_tree_s(int N, const int32_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-                                           const int16_t* __restrict__ eid_of, const float* stl, int origin,
-                                           FibSmall<NP>* h, uint8_t* ol, uint8_t* pl) {
-    exact_sssp(N, indptr, indices, [stl, eid_of](int a_, int b_) { return stl[eid_of[a_ * NP + b_]]; }, origin, h, ol,
-               pl, 1, 0);
+// device_common.h exact_sssp's loop, with the adjacency and the costs read from
+// the workgroup's LDS tables instead of the graph in global memory: u's k-th
+// out-link (scipy CSR order) sits in slot (k % 4) * R + k / 4 of row u of the
+// sparse tables (head node in `ov`, cost in `oc`; empty slots name u itself and
+// come after the real ones).
+template <int NP, int R>
+__device__ __noinline__ void replay_tree_s(int N, const uint8_t* ov, const float* oc, int origin, FibSmall<NP>* h,
+                                           uint8_t* ol, uint8_t* pl) {
+    constexpr int DS = 4 * R;
+    for (int k = 0; k < N; ++k) {
+        h->val[k] = 0.0;
+        h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
+        h->rank[k] = 0;
+        h->state[k] = 0;
+        pl[k] = kNoPred;
+    }
+    Heap<FibSmall<NP>> H{h, -1};
+    fh_insert(H, origin);
+    int k = 0;
+    while (H.min >= 0) {
+        const int v = fh_remove_min(H);
+        h->state[v] = 2;
+        ol[k++] = (uint8_t)v;
+        const double vv = h->val[v];
+        for (int q = 0; q < DS; ++q) {
+            const int slot = v * DS + (q & 3) * R + (q >> 2);
+            const int jc = ov[slot];
+            if (jc == v) break;  // no more out-links
+            const int st = h->state[jc];
+            if (st != 2) {
+                const double nv = vv + (double)oc[slot];
+                if (st == 0) {
+                    h->state[jc] = 1;
+                    h->val[jc] = nv;
+                    fh_insert(H, jc);
+                    pl[jc] = (uint8_t)v;
+                } else if (h->val[jc] > nv) {
+                    fh_decrease(H, jc, nv);
+                    pl[jc] = (uint8_t)v;
+                }
+            }
+        }
+    }
 }
 
 // out-slot rounds of 4 (the kernel is instantiated for 1, 2 and 4)
@@ -482,7 +519,6 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
             if (tid == 0) atomicAdd(&trx_phase_cycles_s[7], (unsigned long long)__popcll(need));  // replayed trees (wave 0)
 #endif
             if (need) {  // wave-uniform: exact scipy-heap replays of the ambiguous trees
-                const float* const stl = st + lenv * E;
                 // the ambiguous trees' quad leaders replay their trees concurrently, each with
                 // its own heap in LDS: the wave's 16 key rows (16 * NP * 8 bytes, dead until the
                 // subtree pass re-initialises them) hold kSlots heaps, so up to kSlots trees per
@@ -505,7 +541,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
                     if ((batch >> lane) & 1ull) {
                         const int slot = __popcll(batch & ((1ull << lane) - 1ull));
                         FibSmall<NP>* const h = reinterpret_cast<FibSmall<NP>*>(area + slot * kHeapBytes);
-                        replay_tree_s<NP>(N, g.indptr, g.indices, g.eid_of, stl, origin, h, ol, pl);
+                        replay_tree_s<NP, R>(N, sov, oc, origin, h, ol, pl);
                     }
                     wave_sync_s();
                 }
