@@ -50,6 +50,15 @@ __device__ unsigned long long trx_phase_cycles_s[8];
             stamp_prev_ = now_;                                             \
         }                                                                   \
     } while (0)
+// per-workgroup wall cycles (thread 0, kernel start -> end) of the last launch
+__device__ unsigned long long trx_wg_cycles_s[1 << 16];
+extern "C" int trx_debug_wg_cycles_s(unsigned long long* out, int n) {
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (n > (1 << 16)) n = 1 << 16;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_wg_cycles_s), sizeof(unsigned long long) * n) != hipSuccess)
+        return -2;
+    return 0;
+}
 extern "C" int trx_debug_phase_cycles_s(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -2;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_phase_cycles_s), sizeof(unsigned long long) * 8) != hipSuccess)
@@ -305,6 +314,7 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
     const int NDS = NP * DSP;
 #ifdef TRX_PHASE_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+    const unsigned long long wg_start_ = stamp_prev_;
 #endif
 
     // ------------------------------------------------ per-env activation
@@ -723,6 +733,9 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
         }
     }
     TRX_SSTAMP(6);
+#ifdef TRX_PHASE_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) trx_wg_cycles_s[blockIdx.x] = __builtin_amdgcn_s_memtime() - wg_start_;
+#endif
 }
 
 size_t sparse_workspace_bytes(const DevGraph& g, int num_envs) {

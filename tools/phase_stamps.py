@@ -54,3 +54,15 @@ if KIND == "sparse":
           f"x 16 trees = {buf[7] / (5 * (B // 2) * 30 * 16) * 100:.3f} %")
 for i, n in enumerate(names):
     print(f"{n:>14}: {buf[i] / tot * 100:6.2f} %  ({buf[i] / 5 / (B / 4) / 30:.0f} cycles/WG/iter)")
+
+# per-workgroup wall cycles of the last step launch: the launch lasts as long as its slowest workgroup
+import numpy as np  # noqa: E402
+L.trx_debug_wg_cycles_s.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+nb = B // 2
+wg = (ctypes.c_ulonglong * nb)()
+L.trx_debug_wg_cycles_s(wg, nb)
+w = np.array(wg[:nb], dtype=np.float64)
+print("per-WG cycles of the last launch: mean %.0f  p50 %.0f  p90 %.0f  p99 %.0f  max %.0f" %
+      (w.mean(), np.percentile(w, 50), np.percentile(w, 90), np.percentile(w, 99), w.max()))
+slow = np.argsort(w)[-8:]
+print("slowest workgroups (envs 2k, 2k+1):", [(int(i), int(w[i])) for i in slow])
