@@ -362,26 +362,46 @@ __global__ void __launch_bounds__(HC / 4) gat_mid_gen_kernel(trx_gat_mid_args a)
         al[v] = al[v] / ad_[dlc[p] * H + h];
     }
     __syncthreads();
-    // aggregation + bias + LayerNorm + regenerated residual + ReLU, NB nodes per round
+    // aggregation + bias + LayerNorm + regenerated residual + ReLU, NB nodes per round.
+    // The four channels as two packed pairs (v_pk_mul_f32 / v_pk_add_f32: each lane of a
+    // pair is the scalar operation, so the regenerated residual keeps layer 0's values)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 w0p[4][2], wpp[4][2], b0p[2], g0p[2], e0p[2], bpp[2], b1p[2], g1p[2], e1p[2];
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            w0p[k][P] = f2{w0[2 * P][k], w0[2 * P + 1][k]};
+            wpp[k][P] = f2{wp[2 * P][k], wp[2 * P + 1][k]};
+        }
+        b0p[P] = f2{b0[2 * P], b0[2 * P + 1]};
+        g0p[P] = f2{g0[2 * P], g0[2 * P + 1]};
+        e0p[P] = f2{e0[2 * P], e0[2 * P + 1]};
+        bpp[P] = f2{bp[2 * P], bp[2 * P + 1]};
+        b1p[P] = f2{b1[2 * P], b1[2 * P + 1]};
+        g1p[P] = f2{g1[2 * P], g1[2 * P + 1]};
+        e1p[P] = f2{e1[2 * P], e1[2 * P + 1]};
+    }
     for (int i0 = 0; i0 < n; i0 += NB) {
-        float v[NB][4];
+        f2 v[NB][2];
         float s[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
             const int i = i0 + b;
-            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
             if (i < n)
                 for (int p = rp[i]; p < rp[i + 1]; ++p) {
                     const float w = al[p * H + wave];
                     const uint2 u = *reinterpret_cast<const uint2*>(xs + (size_t)cl[p] * HC + f0);
-                    acc[0] += w * __uint_as_float(u.x << 16);
-                    acc[1] += w * __uint_as_float(u.x & 0xffff0000u);
-                    acc[2] += w * __uint_as_float(u.y << 16);
-                    acc[3] += w * __uint_as_float(u.y & 0xffff0000u);
+                    const f2 x01 = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u)};
+                    const f2 x23 = {__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+                    acc0 += w * x01;
+                    acc1 += w * x23;
                 }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[b][r] = acc[r] + b1[r];
-            s[b] = wave_sum_l0((v[b][0] + v[b][1]) + (v[b][2] + v[b][3]));
+            v[b][0] = acc0 + b1p[0];
+            v[b][1] = acc1 + b1p[1];
+            const f2 t = v[b][0] + v[b][1];
+            s[b] = wave_sum_l0(t.x + t.y);
         }
         if (lane == 0)
 #pragma unroll
@@ -393,13 +413,9 @@ __global__ void __launch_bounds__(HC / 4) gat_mid_gen_kernel(trx_gat_mid_args a)
             float t = 0.0f;
             for (int w = 0; w < NW; ++w) t += red[w * NB + b];
             mean[b] = t / (float)HC;
-            float q = 0.0f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float d = v[b][r] - mean[b];
-                q += d * d;
-            }
-            s[b] = wave_sum_l0(q);
+            const f2 d0 = v[b][0] - mean[b], d1 = v[b][1] - mean[b];
+            const f2 q = d0 * d0 + d1 * d1;
+            s[b] = wave_sum_l0(q.x + q.y);
         }
         if (lane == 0)
 #pragma unroll
@@ -414,24 +430,27 @@ __global__ void __launch_bounds__(HC / 4) gat_mid_gen_kernel(trx_gat_mid_args a)
             const float rstd = rsqrtf(t / (float)HC + a.ln_eps);
             // layer 0's row i, channels f0..f0+3 (trx_gat_layer0_infer's expression)
             const float* d = dsc + i * DS;
-            const float xbr[4] = {d[4 * h0], d[4 * h0 + 1], d[4 * h0 + 2], d[4 * h0 + 3]};
-            const float xr[4] = {d[4 * H0], d[4 * H0 + 1], d[4 * H0 + 2], d[4 * H0 + 3]};
+            const float4 xb4 = *reinterpret_cast<const float4*>(d + 4 * h0);
+            const float4 x4 = *reinterpret_cast<const float4*>(d + 4 * H0);
             const float mean0 = d[4 * H0 + 4], rstd0 = d[4 * H0 + 5];
-            float y[4];
+            f2 y[2];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float v0 = dot4(xbr, w0[r][0], w0[r][1], w0[r][2], w0[r][3]) + b0[r];
-                const float res = dot4(xr, wp[r][0], wp[r][1], wp[r][2], wp[r][3]) + bp[r];
-                const float yy0 = (g0[r] * (rstd0 * (v0 - mean0)) + e0[r]) + res;
-                const float y0 = yy0 > 0.0f ? yy0 : 0.0f;
-                const float yy = (g1[r] * (rstd * (v[b][r] - mean[b])) + e1[r]) + y0;
-                y[r] = yy > 0.0f ? yy : 0.0f;
+            for (int P = 0; P < 2; ++P) {
+                const f2 v0 = ((xb4.x * w0p[0][P] + xb4.y * w0p[1][P]) + (xb4.z * w0p[2][P] + xb4.w * w0p[3][P])) + b0p[P];
+                const f2 res = ((x4.x * wpp[0][P] + x4.y * wpp[1][P]) + (x4.z * wpp[2][P] + x4.w * wpp[3][P])) + bpp[P];
+                f2 y0 = (g0p[P] * (rstd0 * (v0 - mean0)) + e0p[P]) + res;
+                y0.x = y0.x > 0.0f ? y0.x : 0.0f;
+                y0.y = y0.y > 0.0f ? y0.y : 0.0f;
+                f2 yy = (g1p[P] * (rstd * (v[b][P] - mean[b])) + e1p[P]) + y0;
+                yy.x = yy.x > 0.0f ? yy.x : 0.0f;
+                yy.y = yy.y > 0.0f ? yy.y : 0.0f;
+                y[P] = yy;
             }
             const size_t o = (size_t)(node0 + i) * HC + f0;
-            if (a.out_f32) *reinterpret_cast<float4*>(a.out_f32 + o) = make_float4(y[0], y[1], y[2], y[3]);
+            if (a.out_f32) *reinterpret_cast<float4*>(a.out_f32 + o) = make_float4(y[0].x, y[0].y, y[1].x, y[1].y);
             if (a.out_bf16)
                 *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.out_bf16) + o) =
-                    make_uint2(pk_bf16_l0(y[0], y[1]), pk_bf16_l0(y[2], y[3]));
+                    make_uint2(pk_bf16_l0(y[0].x, y[0].y), pk_bf16_l0(y[1].x, y[1].y));
         }
     }
 }
