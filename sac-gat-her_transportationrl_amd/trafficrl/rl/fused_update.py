@@ -64,6 +64,27 @@ class NetCtx:
     head_w: tuple
 
 
+_MM32 = [None]   # torch.mm(..., out_dtype=torch.float32) available on this build (probed once, eagerly)
+
+
+def _mm32(a: torch.Tensor, b: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a @ b (+ add) from bf16 operands with the float32 accumulator as the
+    result (no bf16 rounding of the product: the update's gradients flow in
+    fp32 between the layer kernels, and no cast kernel runs)."""
+    if _MM32[0] is None and not torch.cuda.is_current_stream_capturing():
+        try:
+            t = torch.mm(a[:2], b, out_dtype=torch.float32)
+            _MM32[0] = t.dtype == torch.float32
+        except (RuntimeError, TypeError):
+            _MM32[0] = False
+    if _MM32[0]:
+        if add is None:
+            return torch.mm(a, b, out_dtype=torch.float32)
+        return torch.addmm(add, a, b, out_dtype=torch.float32)
+    r = (a @ b).float()
+    return r if add is None else r + add
+
+
 def _layer_args(l, norm, topo, a_all, off, stride, i, last):
     args = _lib.TrxGatLayerArgs()
     args.num_graphs, args.nodes_per_graph, args.heads, args.channels = topo.B, topo.n, l.heads, l.out_channels
@@ -169,7 +190,7 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     wn, wc, we, w2, b2 = head_w
     b1 = net.edge_mlp[0].bias.detach()
     p = F.linear(emb, wn)                                       # bf16 [N, 2H] per-node projections
-    c = torch.mm(ctx.to(torch.bfloat16), wc) + b1               # autocast's bf16 product + fp32 bias
+    c = _mm32(ctx.to(torch.bfloat16), wc, b1)                   # bf16 operands, fp32 product + fp32 bias
     logits = torch.empty(topo.B * topo.e, device=dev, dtype=torch.float32)
     a = fused._edge_args(p, c, ea, we, w2, b2, topo.src32, topo.dst32, topo.B, topo.n, topo.e)
     a.out = logits.data_ptr()
@@ -242,11 +263,11 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     g_we = torch.empty(Hd, k, device=dev, dtype=torch.float32)
     _lib.check(L.trx_partial_sum(_lib.ptr(gwep), B, Hd * k, Hd * k, _lib.ptr(g_we), stream), "trx_partial_sum")
     g_wn = _splitk_wgrad(g_p, cx.emb)                                   # [2H, embed] fp32
-    g_emb = g_p @ wn                                                    # bf16 [N, embed]
+    g_emb = _mm32(g_p, wn)                                              # fp32 [N, embed]
     g_cb = g_c.to(torch.bfloat16)
     ctx_b = cx.ctx.to(torch.bfloat16)
-    g_wc = (g_cb.t() @ ctx_b).float()                                   # [H, 2*embed]
-    g_ctx = (g_cb @ wc.t()).float()                                     # [B, 2*embed]
+    g_wc = _mm32(g_cb.t(), ctx_b)                                       # [H, 2*embed]
+    g_ctx = _mm32(g_cb, wc.t())                                         # [B, 2*embed]
     W1 = net.edge_mlp[0].weight
     gW1 = sink.take(W1.numel()).view_as(W1)
     torch.cat([g_wn[:Hd], g_wn[Hd:], g_we, g_wc], 1, out=gW1)
@@ -262,7 +283,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     a_all = cx.a_all
     g_a_all = torch.empty_like(a_all)
     g_x0 = torch.empty_like(cx.x0)
-    gy_f32, gy_b16, g_pool = None, g_emb, g_ctx
+    gy_f32, gy_b16, g_pool = g_emb, None, g_ctx
     for i in range(len(layers) - 1, -1, -1):
         l, rec = layers[i], cx.layers[i]
         last = i == len(layers) - 1
@@ -316,8 +337,8 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             _grad(l.lin.weight, gw)
             # the previous layer's output reaches this layer twice: bf16 through lin,
             # fp32 as the residual of a middle layer (gat_encoder.py:44-46)
-            gy_b16 = g_xh @ rec["w"]
-            gy_f32 = g_res if ba.residual == 1 else None
+            gy_f32 = _mm32(g_xh, rec["w"], g_res if ba.residual == 1 else None)
+            gy_b16 = None
             g_pool = None
     # ---- prologue: input LayerNorms, loop attrs, edge-logit projections
     A = a_all.shape[1]
