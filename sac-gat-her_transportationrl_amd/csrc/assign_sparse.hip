@@ -287,6 +287,64 @@ __device__ __forceinline__ void replay_tree_wave(int N, const uint8_t* ov, const
     }
 }
 
+// Fibonacci-heap storage of one replay sized for NP nodes, carved from the
+// wave's key rows in LDS (dead between the Dijkstra and the subtree pass).
+template <int NPX>
+struct FibSmall {
+    using idx_t = int8_t;
+    double val[NPX];
+    int8_t parent[NPX], left[NPX], right[NPX], child[NPX];
+    uint8_t rank[NPX], state[NPX];
+    int8_t roots[32];
+};
+
+// The exact scipy-heap replay of one ambiguous tree (rare: out of line so the
+// Dijkstra loop's registers are not sized for it); writes scan order and preds.
+// device_common.h exact_sssp's loop, with the adjacency and the costs read from
+// the workgroup's LDS tables instead of the graph in global memory: u's k-th
+// out-link (scipy CSR order) sits in slot (k % 4) * R + k / 4 of row u of the
+// sparse tables (head node in `ov`, cost in `oc`; empty slots name u itself and
+// come after the real ones).
+template <int NP, int R>
+__device__ __noinline__ void replay_tree_s(int N, const uint8_t* ov, const float* oc, int origin, FibSmall<NP>* h,
+                                           uint8_t* ol, uint8_t* pl) {
+    constexpr int DS = 4 * R;
+    for (int k = 0; k < N; ++k) {
+        h->val[k] = 0.0;
+        h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
+        h->rank[k] = 0;
+        h->state[k] = 0;
+        pl[k] = kNoPred;
+    }
+    Heap<FibSmall<NP>> H{h, -1};
+    fh_insert(H, origin);
+    int k = 0;
+    while (H.min >= 0) {
+        const int v = fh_remove_min(H);
+        h->state[v] = 2;
+        ol[k++] = (uint8_t)v;
+        const double vv = h->val[v];
+        for (int q = 0; q < DS; ++q) {
+            const int slot = v * DS + (q & 3) * R + (q >> 2);
+            const int jc = ov[slot];
+            if (jc == v) break;  // no more out-links
+            const int st = h->state[jc];
+            if (st != 2) {
+                const double nv = vv + (double)oc[slot];
+                if (st == 0) {
+                    h->state[jc] = 1;
+                    h->val[jc] = nv;
+                    fh_insert(H, jc);
+                    pl[jc] = (uint8_t)v;
+                } else if (h->val[jc] > nv) {
+                    fh_decrease(H, jc, nv);
+                    pl[jc] = (uint8_t)v;
+                }
+            }
+        }
+    }
+}
+
 // out-slot rounds of 4 (the kernel is instantiated for 1, 2 and 4)
 int sparse_rounds(const DevGraph& g) {
     const int r = (g.max_out_deg + kQs - 1) / kQs;
@@ -570,17 +628,48 @@ env_kernel_s(const DevGraph g, const trx_params p, const trx_state s, int B, int
 #ifdef TRX_PHASE_STAMPS
             if (tid == 0) atomicAdd(&trx_phase_cycles_s[7], (unsigned long long)__popcll(need));  // replayed trees (wave 0)
 #endif
-            if (need) {  // wave-uniform: exact scipy-heap replays of the ambiguous trees, one at a time
-                         // by the whole wave (replay_tree_wave: the heap in registers)
-                uint64_t pend = need;
-                while (pend) {
-                    const int bit = __builtin_ctzll(pend);
-                    pend &= pend - 1;
-                    const int t = (int)(tid >> 6) * 16 + (bit >> 2);  // the tree of quad leader `bit`
-                    const int le = t / Z, zt = t - le * Z;
-                    replay_tree_wave<NP, R>(N, sov, socost + le * NDS, g.origins[zt], sord + t * NP, spred + t * NP);
+            if (need) {  // wave-uniform: exact scipy-heap replays of the ambiguous trees
+                if (__ballot(1) == ~0ull) {
+                    // every lane of the wave is active: one tree at a time by the whole wave,
+                    // the heap in registers (replay_tree_wave)
+                    uint64_t pend = need;
+                    while (pend) {
+                        const int bit = __builtin_ctzll(pend);
+                        pend &= pend - 1;
+                        const int t = (int)(tid >> 6) * 16 + (bit >> 2);  // the tree of quad leader `bit`
+                        const int le = t / Z, zt = t - le * Z;
+                        replay_tree_wave<NP, R>(N, sov, socost + le * NDS, g.origins[zt], sord + t * NP,
+                                                spred + t * NP);
+                    }
+                    wave_sync_s();
+                } else {  // an inactive env leaves lanes of the wave off: per-lane heaps in LDS
+                    // the ambiguous trees' quad leaders replay their trees concurrently, each with
+                    // its own heap in LDS: the wave's 16 key rows (16 * NP * 8 bytes, dead until the
+                    // subtree pass re-initialises them) hold kSlots heaps, so up to kSlots trees per
+                    // round.  (A heap in global memory cost ~1 ms of dependent misses per replay,
+                    // and a single replay held the whole launch.)
+                    constexpr int kHeapBytes = (int)((sizeof(FibSmall<NP>) + 7) & ~(size_t)7);
+                    constexpr int kSlots = (16 * NP * 8) / kHeapBytes;
+                    static_assert(kSlots >= 1, "replay heap does not fit the wave's key rows");
+                    unsigned char* const area = reinterpret_cast<unsigned char*>(skeys + (size_t)(tid >> 6) * 16 * NP);
+                    const int lane = tid & 63;
+                    uint64_t pend = need;
+                    while (pend) {  // wave-uniform
+                        uint64_t batch = 0, m = pend;
+                        for (int c = 0; c < kSlots && m; ++c) {
+                            const uint64_t b = m & (~m + 1);
+                            batch |= b;
+                            m ^= b;
+                        }
+                        pend &= ~batch;
+                        if ((batch >> lane) & 1ull) {
+                            const int slot = __popcll(batch & ((1ull << lane) - 1ull));
+                            FibSmall<NP>* const h = reinterpret_cast<FibSmall<NP>*>(area + slot * kHeapBytes);
+                            replay_tree_s<NP, R>(N, sov, oc, origin, h, ol, pl);
+                        }
+                        wave_sync_s();
+                    }
                 }
-                wave_sync_s();
             }
             // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree
             // demand sums S(v) per tree in reverse scan order, once final added to

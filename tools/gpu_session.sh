@@ -47,7 +47,7 @@ for s in "$@"; do
         opprobe) step op_probe 300 python tools/op_probe.py ;;
         castprobe) step cast_probe 300 python tools/cast_probe.py ;;
         perbench) step per_bench 200 rocprofv3 --kernel-trace --stats -d gpurun_out/perb -o run --output-format csv -- python3 tools/per_bench.py 50 ;;
-        envtests) step env_tests 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sparse.py tests/test_gpu_fallback.py tests/test_torch_sp.py tests/test_rewards.py tests/test_replay_train.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        envtests) step env_tests 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sparse.py tests/test_gpu_fallback.py tests/test_torch_sp.py tests/test_rewards.py tests/test_replay_train.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         obstests) step obs_tests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_oracle_observe.py tests/test_gpu_gp.py tests/test_rewards.py tests/test_torch_sp.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
         largetests) step large_tests 400 python -u -m pytest tests/test_gpu_large.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         profana) step profana 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profana -o run --output-format csv -- python3 bench.py --network anaheim --steps 6 --warmup 2 --no-cpu ;;
