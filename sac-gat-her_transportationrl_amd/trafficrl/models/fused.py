@@ -122,6 +122,9 @@ def _bf16r(t: torch.Tensor) -> torch.Tensor:
 # graph).  Any other capture (the SAC update) recomputes the copies inside the
 # graph on every replay.
 LAYER0_LINEAR = True   # inference layer 0 through trx_gat_layer0_infer (tests compare both kernels)
+# layer 1 with its residual regenerated from layer 0's descriptor (trx_gat_mid_infer) instead of
+# layer 0 writing a float32 residual that the round-3 layer kernel reads (A/B: TRX_MID=0|1)
+MID_REGEN = os.environ.get("TRX_MID", "1") != "0"
 _PREP_EPOCH = [0]
 _prep_cache: Dict[Tuple, Tuple] = {}
 _STATIC = [False]
@@ -433,7 +436,7 @@ def encoder_infer(enc: GATEncoder, x: torch.Tensor, edge_attr: torch.Tensor, top
     stream = _lib.stream_ptr(dev)
     wts = prepared_encoder(enc, layers)
     lin0 = LAYER0_LINEAR and layer0_supported(enc)
-    mid = lin0 and mid_supported(enc)
+    mid = lin0 and MID_REGEN and mid_supported(enc)
     prev_f32, prev_bf16 = None, None
     emb = ctx = None
     for i, l in enumerate(layers):

@@ -115,7 +115,7 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     stride = a_all.shape[1]
     wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
     lin0 = not save and fused.LAYER0_LINEAR and fused.layer0_supported(enc)
-    mid = lin0 and fused.mid_supported(enc)
+    mid = lin0 and fused.MID_REGEN and fused.mid_supported(enc)
     keep = []
     recs = []
     prev_f32 = prev_bf16 = None

@@ -30,8 +30,8 @@ def main():
 
         def poisoned(*a, **k):
             t = _empty(*a, **k)
-            if t.is_cuda and t.is_floating_point() and not torch.cuda.is_current_stream_capturing():
-                t.fill_(float("nan"))
+            if t.is_cuda and t.is_floating_point():
+                t.fill_(float("nan"))   # captured into a graph too: poisoned on every replay
             return t
         torch.empty = poisoned
     from trafficrl.train import Trainer, sf_config
@@ -58,6 +58,11 @@ def main():
         rec = {"act": acts[-1], "flow": _digest(tr.env.flow), "tstt": _digest(tr.env.tstt)}
         if tr.last_losses:
             rec["td"] = _digest(tr.last_losses["td_errors"])
+        bad = [f"{m}.{k}" for m in ("actor", "critic1", "critic2") for k, p in getattr(tr.agent, m).named_parameters()
+               if p.grad is not None and not bool(torch.isfinite(p.grad).all())]
+        if bad:
+            rec["nonfinite_grads"] = ",".join(bad)
+            print(f"iteration {it}: non-finite gradients in {bad}", flush=True)
         rec["actor"] = _digest(torch.cat([p.detach().reshape(-1) for p in tr.agent.actor.parameters()]))
         rec["critic1"] = _digest(torch.cat([p.detach().reshape(-1) for p in tr.agent.critic1.parameters()]))
         trace.append(rec)

@@ -34,6 +34,8 @@ def test_training_is_bitwise_reproducible_across_processes(tmp_path):
 
 
 def test_no_kernel_reads_unwritten_memory(tmp_path):
+    """Fresh float allocations (eager and inside the captured update) filled
+    with NaN: every iteration's outputs equal the unpoisoned run's."""
     a = _run(tmp_path / "a.pt", 6)
     c = _run(tmp_path / "c.pt", 6, fill=True)
     for it, (ra, rc) in enumerate(zip(a["trace"], c["trace"])):
