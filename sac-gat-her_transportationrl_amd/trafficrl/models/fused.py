@@ -124,7 +124,7 @@ def _bf16r(t: torch.Tensor) -> torch.Tensor:
 LAYER0_LINEAR = True   # inference layer 0 through trx_gat_layer0_infer (tests compare both kernels)
 # layer 1 with its residual regenerated from layer 0's descriptor (trx_gat_mid_infer) instead of
 # layer 0 writing a float32 residual that the round-3 layer kernel reads (A/B: TRX_MID=0|1)
-MID_REGEN = os.environ.get("TRX_MID", "1") != "0"
+MID_REGEN = os.environ.get("TRX_MID", "0") == "1"
 _PREP_EPOCH = [0]
 _prep_cache: Dict[Tuple, Tuple] = {}
 _STATIC = [False]

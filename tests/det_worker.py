@@ -41,6 +41,8 @@ def main():
                her_ratio=0.0, assignment_method="msa", assignment_iters=30, fixed_damage=True, fixed_damage_seed=42,
                sp_backend="scipy", early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0, amp="bf16")
     tr = Trainer(cfg, device="cuda:0", log=False)
+    if os.environ.get("TRX_DET_SERIAL") == "1":   # diagnostics: no side streams in the update
+        tr.agent.concurrent = False
     tr._reset_envs(None)
     obs = tr.env.observe()
     trace = []

@@ -75,6 +75,7 @@ for s in "$@"; do
                     step stamps_rand 300 env TRX_DAMAGE=random python tools/phase_stamps.py 4096 &&
                     step stamps_rand_reset 300 env TRX_DAMAGE=random TRX_STAMP_RESET=1 python tools/phase_stamps.py 4096 ;;
         epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --workload env --steps 44 --warmup 22 --no-cpu; done ;;
+        detprobe) step det_probe 500 bash tools/det_probe.sh ;;
         dettests) step det_tests 600 python -u -m pytest tests/test_determinism.py -m gpu -v -s --timeout 500 --timeout-method thread ;;
         gattests) step gat_tests 400 python -u -m pytest tests/test_gat_infer.py tests/test_gat.py tests/test_sac.py tests/test_gat_tail.py -m gpu -v --timeout 120 --timeout-method thread ;;
         actmid) TRX_MID=0 step act_mid0 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_mid0 -o run --output-format csv -- python3 tools/agent_profile.py 4096 act &&
