@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 9   /* 9: fp32 edge scorer after its p GEMM; trx_gat_layer0_* */
+#define TRX_ABI_VERSION 10  /* 10: `exact` (float32) mode of the fused forward/backward kernels;
+                                  9: fp32 edge scorer after its p GEMM; trx_gat_layer0_* */
 
 /* error codes */
 #define TRX_OK 0
@@ -244,6 +245,9 @@ typedef struct trx_gat_layer_args {
     float* save_asd;            /* [N, 2*heads] a_src | a_dst                              */
     float* save_v;              /* [N, out] aggregate + bias (LayerNorm input)             */
     float* save_stats;          /* [N, 2] LayerNorm mean, rstd                             */
+    int32_t exact;              /* ABI 10: 1 = float32 throughout (xh float [N, out], layer 0 computes
+                                   xh and the input projection unrounded, x0 unrounded; heads*channels
+                                   <= 512); 0 = the bf16-autocast rounding points above */
 } trx_gat_layer_args;
 int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
 
@@ -345,6 +349,7 @@ typedef struct trx_edge_head_args {
                                    per graph from the probs (inverse CDF: the first link whose running
                                    sum of exp(logit - max) exceeds u * total) into `action` */
     int64_t* action;            /* [B] drawn graph-local link (u != NULL) */
+    int32_t exact;              /* ABI 10: 1 = p is float [N, 2*hidden] (and the backward's grad_p float) */
 } trx_edge_head_args;
 int trx_edge_head_infer(const trx_edge_head_args* a, void* stream);
 
@@ -444,6 +449,7 @@ typedef struct trx_gat_prologue_args {
     float* ea;                  /* out [B*e, edge_dim] */
     float* a_edge;              /* out [Et, sum heads], CSR order; a graph whose CSR range references
                                    links or nodes of another graph gets NaN rows */
+    int32_t exact;              /* ABI 10: 1 = M rows, link / loop features and a_edge unrounded (fp32) */
 } trx_gat_prologue_args;
 int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream);
 
@@ -498,6 +504,8 @@ typedef struct trx_gat_layer_bwd_args {
     float* g_x0;                /* [N, in_dim] (in_dim 4) */
     float* g_a_edge;            /* [Et, a_edge_stride] */
     float* part;                /* [num_graphs, part_floats] */
+    int32_t exact;              /* ABI 10: 1 = backward of the exact forward: xh and g_xh float [N, F],
+                                   w0 / wp unrounded, no bf16 rounding anywhere (heads*channels <= 512) */
 } trx_gat_layer_bwd_args;
 int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream);
 int64_t trx_gat_layer_backward_part_floats(int32_t heads, int32_t channels, int32_t in_dim);
@@ -530,6 +538,7 @@ typedef struct trx_gat_prologue_bwd_args {
     const float* g_x0;          /* [N, node_dim] */
     const float* g_ea_head;     /* [B*e, edge_dim] or NULL */
     float* part;                /* [num_graphs, 8A + 32] */
+    int32_t exact;              /* ABI 10: backward of the exact prologue (no bf16 rounding) */
 } trx_gat_prologue_bwd_args;
 int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream);
 /* Backward of every layer's edge-attention rows M (trx_gat_prologue_infer's

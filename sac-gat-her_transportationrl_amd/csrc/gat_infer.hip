@@ -86,6 +86,33 @@ __device__ __forceinline__ float bf16r(float x) { return bf2f(f2bf(x)); }
 // out of scratch when written conditionally, this one is
 typedef unsigned int trx_u4 __attribute__((ext_vector_type(4)));
 
+// Row elements of the staged xh / p tiles: bf16 bits (the autocast rounding
+// points) or, in the exact mode (trx_*_args.exact), float32.
+template <bool XF> struct XElem { typedef uint16_t T; };
+template <> struct XElem<true> { typedef float T; };
+// four consecutive row values as floats
+template <bool XF>
+__device__ __forceinline__ float4 xld4(const typename XElem<XF>::T* p) {
+    if constexpr (XF) {
+        return *reinterpret_cast<const float4*>(p);
+    } else {
+        const uint2 u = *reinterpret_cast<const uint2*>(p);
+        return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                           __uint_as_float(u.y & 0xffff0000u));
+    }
+}
+template <bool XF>
+__device__ __forceinline__ void xst4(typename XElem<XF>::T* p, float a, float b, float c, float d) {
+    if constexpr (XF) {
+        *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+    } else {
+        uint2 u;
+        u.x = pk_bf16(a, b);
+        u.y = pk_bf16(c, d);
+        *reinterpret_cast<uint2*>(p) = u;
+    }
+}
+
 }  // namespace
 
 #ifdef TRX_PHASE_STAMPS
@@ -130,9 +157,12 @@ extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
 
 // ------------------------------------------------------------- layer kernel
 // IN: 0 = xh given (layers >= 1), else the layer-0 input width (4).
-template <int HC, int IN, int NT>
+// XF: the exact mode -- xh float32 (staged as float rows), no bf16 rounding.
+template <int HC, int IN, int NT, bool XF>
 __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename XElem<XF>::T XE;
+    constexpr int EV = 16 / sizeof(XE);  // row elements per 16-byte piece
     constexpr int kInferThreads = NT, kInferWaves = NT / kWave;  // this instance's workgroup
     constexpr int KC = HC / 256;  // float4 chunks per lane in a row
     const int g = blockIdx.x;
@@ -150,8 +180,8 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
 #endif
     constexpr int kStageBatch = TRX_STAGE_BATCH;
     trx_u4 stg[kStageBatch];
-    const int nq = IN == 0 ? n * HC / 8 : 0;
-    const trx_u4* xsrc = IN == 0 ? reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.xh) + (size_t)node0 * HC)
+    const int nq = IN == 0 ? n * HC / EV : 0;
+    const trx_u4* xsrc = IN == 0 ? reinterpret_cast<const trx_u4*>(static_cast<const XE*>(a.xh) + (size_t)node0 * HC)
                                  : nullptr;
     if (IN == 0) {
 #pragma unroll
@@ -170,10 +200,10 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
         return;
     }
 
-    // xh rows padded by 8 bf16 (16 B): the attention dots read four nodes' rows
+    // xh rows padded by 16 B: the attention dots read four nodes' rows
     // per wave instruction, which an unpadded 2 KB stride puts on the same banks
-    constexpr int XS = HC + 8;
-    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);   // [n][XS] bf16
+    constexpr int XS = HC + EV;
+    XE* xs = reinterpret_cast<XE*>(smem);                // [n][XS] bf16 (exact: float)
     float* as_ = reinterpret_cast<float*>(xs + n * XS);  // [n*H]
     float* ad_ = as_ + n * H;                            // [n*H]
     float* al = ad_ + n * H;        // [me*H] edge logits, then attention weights (in place)
@@ -206,11 +236,11 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
         const int e = v / H, h = v - e * H;
         al[v] = a.a_edge[(size_t)(ebeg + e) * a.a_edge_stride + a.a_edge_offset + h];
     }
-    if (IN > 0 && tid < n * IN) x0l[tid] = bf16r(x0v);
+    if (IN > 0 && tid < n * IN) x0l[tid] = XF ? x0v : bf16r(x0v);
     if (IN == 0) {
-        constexpr int Q8 = HC / 8;  // 16-byte pieces per row
+        constexpr int Q8 = HC / EV;  // 16-byte pieces per row
         auto dst4 = [&](int v) -> trx_u4& {
-            return *reinterpret_cast<trx_u4*>(xs + (v / Q8) * XS + (v - (v / Q8) * Q8) * 8);
+            return *reinterpret_cast<trx_u4*>(xs + (v / Q8) * XS + (v - (v / Q8) * Q8) * EV);
         };
 #pragma unroll
         for (int j = 0; j < kStageBatch; ++j) {
@@ -245,10 +275,7 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
 #pragma unroll
                     for (int j = 0; j < IN; ++j) acc[r] += xv[j] * w[r][j];
                 }
-                uint2 u;
-                u.x = pk_bf16(acc[0], acc[1]);
-                u.y = pk_bf16(acc[2], acc[3]);
-                *reinterpret_cast<uint2*>(xs + i * XS + 4 * q) = u;
+                xst4<XF>(xs + i * XS + 4 * q, acc[0], acc[1], acc[2], acc[3]);
             }
         }
         __syncthreads();
@@ -287,9 +314,8 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
 #pragma unroll
                     for (int m = 0; m < 4; ++m)
                         if (m < CM) {
-                            const uint2 u = *reinterpret_cast<const uint2*>(xs + i * XS + h * C + 4 * sl + 64 * m);
-                            const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
-                            const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
+                            const float4 x4 = xld4<XF>(xs + i * XS + h * C + 4 * sl + 64 * m);
+                            const float v0 = x4.x, v1 = x4.y, v2 = x4.z, v3 = x4.w;
                             s1 += (v0 * sa[m].x + v1 * sa[m].y) + (v2 * sa[m].z + v3 * sa[m].w);
                             s2 += (v0 * da[m].x + v1 * da[m].y) + (v2 * da[m].z + v3 * da[m].w);
                         }
@@ -314,9 +340,8 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
                 for (int c = 4 * sl; c < C; c += 64) {
                     const float4 sa = *reinterpret_cast<const float4*>(a.att_src + h * C + c);
                     const float4 da = *reinterpret_cast<const float4*>(a.att_dst + h * C + c);
-                    const uint2 u = *reinterpret_cast<const uint2*>(xs + i * XS + h * C + c);
-                    const float v0 = __uint_as_float(u.x << 16), v1 = __uint_as_float(u.x & 0xffff0000u);
-                    const float v2 = __uint_as_float(u.y << 16), v3 = __uint_as_float(u.y & 0xffff0000u);
+                    const float4 x4 = xld4<XF>(xs + i * XS + h * C + c);
+                    const float v0 = x4.x, v1 = x4.y, v2 = x4.z, v3 = x4.w;
                     s1 += (v0 * sa.x + v1 * sa.y) + (v2 * sa.z + v3 * sa.w);
                     s2 += (v0 * da.x + v1 * da.y) + (v2 * da.z + v3 * da.w);
                 }
@@ -416,17 +441,17 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
 #pragma unroll
         for (int k = 0; k < KC; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         for (int p = rp[i]; p < rp[i + 1]; ++p) {
-            const uint16_t* row = xs + cl[p] * XS;
+            const XE* row = xs + cl[p] * XS;
             const float* alr = al + p * H;
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
                 const int q = lane + kWave * k;
                 const float w = alr[(4 * q) / C];
-                const uint2 u = *reinterpret_cast<const uint2*>(row + 4 * q);
-                acc[k].x += w * __uint_as_float(u.x << 16);
-                acc[k].y += w * __uint_as_float(u.x & 0xffff0000u);
-                acc[k].z += w * __uint_as_float(u.y << 16);
-                acc[k].w += w * __uint_as_float(u.y & 0xffff0000u);
+                const float4 x4 = xld4<XF>(row + 4 * q);
+                acc[k].x += w * x4.x;
+                acc[k].y += w * x4.y;
+                acc[k].z += w * x4.z;
+                acc[k].w += w * x4.w;
             }
         }
         float v[KC][4];
@@ -474,7 +499,7 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
                     float t = 0.0f;
 #pragma unroll
                     for (int j = 0; j < (IN > 0 ? IN : 1); ++j) t += xr[j] * wp_r[k][r][j];
-                    y = y + bf16r(t + bp_r[k][r]);
+                    y = y + (XF ? t + bp_r[k][r] : bf16r(t + bp_r[k][r]));
                 } else if (IN == 0 && a.residual == 1) {
                     y = y + resv[r];
                 }
@@ -524,9 +549,11 @@ constexpr int kEdgeED = 8;  // edge_dim <= 8
 // DK: the link-feature count when fixed at compile time (the regular case, 6: no
 // per-term edge_dim test and no padding terms in the link-feature product), 0 = any
 // edge_dim <= kEdgeED.  The same terms in the same order either way.
-template <int MQ, int DK>  // hidden <= 256 * MQ, hidden % 4 == 0
+template <int MQ, int DK, bool XF>  // hidden <= 256 * MQ, hidden % 4 == 0; XF: p float (exact mode)
 __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge_head_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename XElem<XF>::T XE;
+    constexpr int EV = 16 / sizeof(XE);
     constexpr int ED = kEdgeED;
     const int g = blockIdx.x;
     const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
@@ -534,7 +561,7 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
 #ifdef TRX_PHASE_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
 #endif
-    uint16_t* pr = reinterpret_cast<uint16_t*>(smem);               // [n][2*Hd] bf16
+    XE* pr = reinterpret_cast<XE*>(smem);                            // [n][2*Hd] bf16 (exact: float)
     float* eal = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);  // [E][ED] link features (fp32)
     float* lg = eal + (size_t)E * ED;                                // [E] logits
     float* mk = lg + E;                                              // [E] mask
@@ -546,9 +573,9 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
 
     // stage: the loads of a batch are all issued before its LDS stores
     const int64_t node0 = (int64_t)g * n;
-    const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.p) + node0 * 2 * Hd);
+    const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const XE*>(a.p) + node0 * 2 * Hd);
     trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
-    const int nq = n * 2 * Hd / 8;
+    const int nq = n * 2 * Hd / EV;
 #ifndef TRX_EH_ROWS
 #define TRX_EH_ROWS 6
 #endif
@@ -628,19 +655,16 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
             const float4 ea0 = *reinterpret_cast<const float4*>(eal + e * ED);
             const float4 ea1 = *reinterpret_cast<const float4*>(eal + e * ED + 4);
             const float ear[ED] = {ea0.x, ea0.y, ea0.z, ea0.w, ea1.x, ea1.y, ea1.z, ea1.w};
-            const uint16_t* ps = pr + sl[e] * 2 * Hd;
-            const uint16_t* pd = pr + dl[e] * 2 * Hd + Hd;
+            const XE* ps = pr + sl[e] * 2 * Hd;
+            const XE* pd = pr + dl[e] * 2 * Hd + Hd;
             part[u] = 0.0f;
 #pragma unroll
             for (int m = 0; m < MQ; ++m) {
                 const int k0 = 256 * m + 4 * lane;
                 if (k0 < Hd) {
-                    const uint2 us = *reinterpret_cast<const uint2*>(ps + k0);
-                    const uint2 ud = *reinterpret_cast<const uint2*>(pd + k0);
-                    const float psv[4] = {__uint_as_float(us.x << 16), __uint_as_float(us.x & 0xffff0000u),
-                                          __uint_as_float(us.y << 16), __uint_as_float(us.y & 0xffff0000u)};
-                    const float pdv[4] = {__uint_as_float(ud.x << 16), __uint_as_float(ud.x & 0xffff0000u),
-                                          __uint_as_float(ud.y << 16), __uint_as_float(ud.y & 0xffff0000u)};
+                    const float4 s4 = xld4<XF>(ps + k0), d4 = xld4<XF>(pd + k0);
+                    const float psv[4] = {s4.x, s4.y, s4.z, s4.w};
+                    const float pdv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         float ew = 0.0f;
@@ -766,7 +790,7 @@ __global__ void __launch_bounds__(NT) gat_prologue_kernel(trx_gat_prologue_args 
     const int p0 = a.rowptr[node0], p1 = a.rowptr[node0 + n];
     for (int v = tid; v < A * D; v += NT) {
         const int k = v / D, j = v - (v / D) * D;
-        Ml[k * MD + j] = bf16r(a.m_work[v]);
+        Ml[k * MD + j] = a.exact ? a.m_work[v] : bf16r(a.m_work[v]);
     }
     for (int l = tid; l < E; l += NT) {
         float x[MD];
@@ -817,13 +841,13 @@ __global__ void __launch_bounds__(NT) gat_prologue_kernel(trx_gat_prologue_args 
         const float* fr = code >= 0 ? ean + (ok ? li : 0) * MD : lp + (ok ? ni : 0) * MD;
         float f[MD];
 #pragma unroll
-        for (int j = 0; j < MD; ++j) f[j] = j < D ? bf16r(fr[j]) : 0.0f;
+        for (int j = 0; j < MD; ++j) f[j] = j < D ? (a.exact ? fr[j] : bf16r(fr[j])) : 0.0f;
         for (int k = 0; k < A; ++k) {
             float acc = 0.0f;
 #pragma unroll
             for (int j = 0; j < MD; ++j)
                 if (j < D) acc += f[j] * Ml[k * MD + j];
-            a.a_edge[(size_t)p * A + k] = ok ? bf16r(acc) : __builtin_nanf("");
+            a.a_edge[(size_t)p * A + k] = ok ? (a.exact ? acc : bf16r(acc)) : __builtin_nanf("");
         }
     }
 }
@@ -847,21 +871,21 @@ hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t strea
 }
 
 size_t edge_head_infer_smem(const trx_edge_head_args& a) {
-    return (size_t)a.nodes_per_graph * 2 * a.hidden * 2 + (size_t)a.edges_per_graph * (kEdgeED * 4 + 4 * 4) + 4;
+    return (size_t)a.nodes_per_graph * 2 * a.hidden * (a.exact ? 4 : 2) + (size_t)a.edges_per_graph * (kEdgeED * 4 + 4 * 4) + 4;
 }
 
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a) {
     const int HC = a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
     const size_t alsz = (size_t)me * H;
-    size_t b = (size_t)n * (HC + 8) * 2 + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 * 2 + (size_t)(n + 1) * 4 +
+    size_t b = (a.exact ? (size_t)n * (HC + 4) * 4 : (size_t)n * (HC + 8) * 2) + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 * 2 + (size_t)(n + 1) * 4 +
                (size_t)n * a.in_dim * 4;
     if (a.pool) b += (size_t)n * HC * 4;
     return b;
 }
 
-template <int HC, int IN, int NT>
+template <int HC, int IN, int NT, bool XF = false>
 static void set_lds_attr() {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_infer_kernel<HC, IN, NT>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_infer_kernel<HC, IN, NT, XF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
@@ -885,24 +909,37 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
         set_lds_attr<512, 4, 512>();
         set_lds_attr<256, 0, 512>();
         set_lds_attr<256, 4, 512>();
+        set_lds_attr<512, 0, 512, true>();
+        set_lds_attr<512, 4, 512, true>();
+        set_lds_attr<256, 0, 512, true>();
+        set_lds_attr<256, 4, 512, true>();
+        set_lds_attr<512, 0, 256, true>();
+        set_lds_attr<512, 4, 256, true>();
+        set_lds_attr<256, 0, 256, true>();
+        set_lds_attr<256, 4, 256, true>();
         attr_set = true;
     }
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
     const dim3 grid(a.num_graphs);
     const bool wide = a.num_graphs < 2048;
-#define TRX_LAYER_CASE(HCV, INV)                                                                          \
-    if (HC == HCV && a.in_dim == INV) {                                                                   \
-        if (wide)                                                                                         \
-            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 512>), grid, dim3(512), smem, stream, a); \
-        else                                                                                              \
-            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 256>), grid, dim3(256), smem, stream, a); \
-        return hipGetLastError();                                                                         \
+#define TRX_LAYER_CASE(HCV, INV, XFV)                                                                          \
+    if (HC == HCV && a.in_dim == INV && (a.exact != 0) == XFV) {                                               \
+        if (wide)                                                                                              \
+            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 512, XFV>), grid, dim3(512), smem, stream, a); \
+        else                                                                                                   \
+            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 256, XFV>), grid, dim3(256), smem, stream, a); \
+        return hipGetLastError();                                                                              \
     }
-    TRX_LAYER_CASE(1024, 0)
-    TRX_LAYER_CASE(1024, 4)
-    TRX_LAYER_CASE(512, 0)
-    TRX_LAYER_CASE(512, 4)
-    TRX_LAYER_CASE(256, 0)
-    TRX_LAYER_CASE(256, 4)
+    TRX_LAYER_CASE(1024, 0, false)
+    TRX_LAYER_CASE(1024, 4, false)
+    TRX_LAYER_CASE(512, 0, false)
+    TRX_LAYER_CASE(512, 4, false)
+    TRX_LAYER_CASE(256, 0, false)
+    TRX_LAYER_CASE(256, 4, false)
+    TRX_LAYER_CASE(512, 0, true)
+    TRX_LAYER_CASE(512, 4, true)
+    TRX_LAYER_CASE(256, 0, true)
+    TRX_LAYER_CASE(256, 4, true)
 #undef TRX_LAYER_CASE
     return hipErrorInvalidValue;
 }
@@ -929,15 +966,23 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 // grad_z [E_total, H] bf16 (dz) only when asked for.
 constexpr int kEhbThreads = 1024, kEhbParts = kEhbThreads / 256;
 
+template <bool XF>  // exact mode: p and grad_p float
 __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
-                                                                    uint16_t* grad_p, float* grad_c,
+                                                                    void* grad_p_, float* grad_c,
                                                                     uint16_t* grad_z, float* grad_w2_part,
                                                                     float* grad_we_part, float* grad_ea) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename XElem<XF>::T XE;
+    constexpr int EV = 16 / sizeof(XE);
+    XE* const grad_p = static_cast<XE*>(grad_p_);
+    auto xv = [](XE t) -> float {
+        if constexpr (XF) return t;
+        else return bf2f(t);
+    };
     constexpr int ED = kEdgeED, NT = kEhbThreads, P = kEhbParts;
     const int g = blockIdx.x, tid = threadIdx.x, k = tid & 255, part = tid >> 8;
     const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
-    uint16_t* pr = reinterpret_cast<uint16_t*>(smem);                   // [n][2*Hd] bf16
+    XE* pr = reinterpret_cast<XE*>(smem);                               // [n][2*Hd] bf16 (exact: float)
     float* dzs = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);     // [E][Hd] dL/dz (n*2*Hd even)
     float* eal = dzs + (size_t)E * Hd;                                  // [E][ED] link features
     float* gl = eal + (size_t)E * ED;                                   // [E] grad logit
@@ -951,9 +996,9 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
     int* ip = op + n + 1;                                               // [n+1] in-list offsets
     const int64_t node0 = (int64_t)g * n;
     {
-        const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const uint16_t*>(a.p) + node0 * 2 * Hd);
+        const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const XE*>(a.p) + node0 * 2 * Hd);
         trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
-        for (int v = tid; v < n * 2 * Hd / 8; v += NT) dst4[v] = src4[v];
+        for (int v = tid; v < n * 2 * Hd / EV; v += NT) dst4[v] = src4[v];
     }
     for (int e = tid; e < E; e += NT) {
         const int64_t eg = (int64_t)g * E + e;
@@ -1011,7 +1056,7 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
 #pragma unroll
             for (int j = 0; j < ED; ++j)
                 if (j < D) ew += eal[e * ED + j] * we[j];
-            const float z = ((bf2f(pr[s * 2 * Hd + k]) + bf2f(pr[d * 2 * Hd + Hd + k])) + ew) + ck;
+            const float z = ((xv(pr[s * 2 * Hd + k]) + xv(pr[d * 2 * Hd + Hd + k])) + ew) + ck;
             const float gb = gl[e];
             gw2 += gb * fmaxf(z, 0.0f);
             const float dz = z > 0.0f ? gb * w2 : 0.0f;
@@ -1064,14 +1109,19 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
             float so = 0.0f, si = 0.0f;
             for (int q = op[i]; q < op[i + 1]; ++q) so += dzs[lo[q] * Hd + k];
             for (int q = ip[i]; q < ip[i + 1]; ++q) si += dzs[li[q] * Hd + k];
-            grad_p[(node0 + i) * 2 * Hd + k] = f2bf(so);
-            grad_p[(node0 + i) * 2 * Hd + Hd + k] = f2bf(si);
+            if constexpr (XF) {
+                grad_p[(node0 + i) * 2 * Hd + k] = so;
+                grad_p[(node0 + i) * 2 * Hd + Hd + k] = si;
+            } else {
+                grad_p[(node0 + i) * 2 * Hd + k] = f2bf(so);
+                grad_p[(node0 + i) * 2 * Hd + Hd + k] = f2bf(si);
+            }
         }
 }
 
 size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
     const size_t n = a.nodes_per_graph, E = a.edges_per_graph, H = a.hidden;
-    return n * 2 * H * 2 + E * H * 4 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * (2 + kEdgeED) * 256 * 4 +
+    return n * 2 * H * (a.exact ? 4 : 2) + E * H * 4 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * (2 + kEdgeED) * 256 * 4 +
            256 * kEdgeED * 4 + 2 * (n + 1) * 4;
 }
 
@@ -1079,37 +1129,49 @@ hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_l
                                 void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea,
                                 hipStream_t stream) {
     const size_t smem = edge_head_bwd_smem(a);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
+    const void* fn = a.exact ? reinterpret_cast<const void*>(edge_head_bwd_kernel<true>)
+                             : reinterpret_cast<const void*>(edge_head_bwd_kernel<false>);
     if (smem > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(edge_head_bwd_kernel),
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+        if (e != hipSuccess) return e;
+    }
+    if (a.exact)
+        hipLaunchKernelGGL(edge_head_bwd_kernel<true>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a,
+                           grad_logits, grad_p, grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part, grad_we_part,
+                           grad_ea);
+    else
+        hipLaunchKernelGGL(edge_head_bwd_kernel<false>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a,
+                           grad_logits, grad_p, grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part, grad_we_part,
+                           grad_ea);
+    return hipGetLastError();
+}
+
+template <int MQ, int DK, bool XF>
+static hipError_t launch_edge_head_infer_t(const trx_edge_head_args& a, size_t smem, hipStream_t stream) {
+    if (smem > 64 * 1024) {  // opt in to more than 64 KB of dynamic LDS
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(edge_head_infer_kernel<MQ, DK, XF>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(edge_head_bwd_kernel, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a, grad_logits,
-                       static_cast<uint16_t*>(grad_p), grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part,
-                       grad_we_part, grad_ea);
+    hipLaunchKernelGGL((edge_head_infer_kernel<MQ, DK, XF>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream) {
     const size_t smem = edge_head_infer_smem(a);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
     const bool d6 = a.edge_dim == 6;  // the networks' link features (repair_env.py:800-808)
-    const void* fn = a.hidden <= 256 ? (d6 ? reinterpret_cast<const void*>(edge_head_infer_kernel<1, 6>)
-                                           : reinterpret_cast<const void*>(edge_head_infer_kernel<1, 0>))
-                                     : (d6 ? reinterpret_cast<const void*>(edge_head_infer_kernel<2, 6>)
-                                           : reinterpret_cast<const void*>(edge_head_infer_kernel<2, 0>));
-    if (smem > 64 * 1024) {  // opt in to more than 64 KB of dynamic LDS
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-        if (e != hipSuccess) return e;
+    if (a.exact) {
+        if (a.hidden > 256) return hipErrorInvalidValue;
+        return d6 ? launch_edge_head_infer_t<1, 6, true>(a, smem, stream)
+                  : launch_edge_head_infer_t<1, 0, true>(a, smem, stream);
     }
-    if (a.hidden <= 256 && d6)
-        hipLaunchKernelGGL((edge_head_infer_kernel<1, 6>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
-    else if (a.hidden <= 256)
-        hipLaunchKernelGGL((edge_head_infer_kernel<1, 0>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
-    else if (d6)
-        hipLaunchKernelGGL((edge_head_infer_kernel<2, 6>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
-    else
-        hipLaunchKernelGGL((edge_head_infer_kernel<2, 0>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
-    return hipGetLastError();
+    if (a.hidden <= 256)
+        return d6 ? launch_edge_head_infer_t<1, 6, false>(a, smem, stream)
+                  : launch_edge_head_infer_t<1, 0, false>(a, smem, stream);
+    return d6 ? launch_edge_head_infer_t<2, 6, false>(a, smem, stream)
+              : launch_edge_head_infer_t<2, 0, false>(a, smem, stream);
 }
 
 }  // namespace trx

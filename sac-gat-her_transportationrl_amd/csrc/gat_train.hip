@@ -64,15 +64,44 @@ __device__ __forceinline__ float rbf(float x) { return frbf(tobf(x)); }
 __device__ __forceinline__ float lo_bf(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
+// xh / g_xh row elements: bf16 bits, or float32 in the exact mode
+template <bool XF> struct XE_ { typedef uint16_t T; };
+template <> struct XE_<true> { typedef float T; };
+template <bool XF>
+__device__ __forceinline__ float4 ld4x(const typename XE_<XF>::T* p) {
+    if constexpr (XF) {
+        return *reinterpret_cast<const float4*>(p);
+    } else {
+        const uint2 u = *reinterpret_cast<const uint2*>(p);
+        return make_float4(lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y));
+    }
+}
+// store four values (bf16: rounded); returns the values as stored
+template <bool XF>
+__device__ __forceinline__ float4 st4x(typename XE_<XF>::T* p, float a, float b, float c, float d) {
+    if constexpr (XF) {
+        *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+        return make_float4(a, b, c, d);
+    } else {
+        uint2 u;
+        u.x = pkbf(a, b);
+        u.y = pkbf(c, d);
+        *reinterpret_cast<uint2*>(p) = u;
+        return make_float4(lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y));
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------ layer backward
 // Partial-sum layout per graph (floats): [0,F) bias, [F,2F) ln weight, [2F,3F) ln
 // bias, [3F,4F) att_src, [4F,5F) att_dst; layer 0 adds [5F,9F) lin.weight (F x 4,
 // row-major), [9F,13F) input_proj.weight, [13F,14F) input_proj.bias.  F = heads*channels.
-template <int HC, int IN, int NT>
+template <int HC, int IN, int NT, bool XF>
 __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename XE_<XF>::T XE;
+    constexpr int EV = 16 / sizeof(XE);
     constexpr int KC = HC / 256;  // float4 chunks per lane in a row
     constexpr int kT = NT, kNW = NT / kW;  // threads / waves per workgroup
     constexpr int INR = IN > 0 ? IN : 1;
@@ -87,8 +116,8 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 
     // rows padded by 16 B: phase C1 reads four pairs' rows per wave instruction,
     // which unpadded 2 KB / 4 KB strides put on the same LDS banks
-    constexpr int XS = HC + 8, GS = HC + 4;
-    uint16_t* xs = reinterpret_cast<uint16_t*>(smem);         // [n][XS] bf16 lin output
+    constexpr int XS = HC + EV, GS = HC + 4;
+    XE* xs = reinterpret_cast<XE*>(smem);                      // [n][XS] bf16 lin output (exact: float)
     float* gv = reinterpret_cast<float*>(xs + n * XS);         // [n][GS] dL/d(aggregate + bias)
     float* al = gv + n * GS;                                   // [me*H] attention weights
     float* ge = al + a.max_graph_edges * H;                    // [me*H] dL/dalpha, then dL/de
@@ -120,14 +149,14 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
     for (int v = tid; v < 2 * n; v += kT) st[v] = a.stats[(size_t)node0 * 2 + v];
     if (IN > 0)
         for (int v = tid; v < n * IN; v += kT) {
-            x0l[v] = rbf(a.x0[(size_t)node0 * IN + v]);
+            x0l[v] = XF ? a.x0[(size_t)node0 * IN + v] : rbf(a.x0[(size_t)node0 * IN + v]);
             gx0[v] = 0.0f;
         }
     if (IN == 0) {
-        const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.xh) + (size_t)node0 * HC);
-        constexpr int Q8 = HC / 8;
+        const uint4* src = reinterpret_cast<const uint4*>(static_cast<const XE*>(a.xh) + (size_t)node0 * HC);
+        constexpr int Q8 = HC / EV;
         for (int v = tid; v < n * Q8; v += kT)
-            *reinterpret_cast<uint4*>(xs + (v / Q8) * XS + (v - (v / Q8) * Q8) * 8) = src[v];
+            *reinterpret_cast<uint4*>(xs + (v / Q8) * XS + (v - (v / Q8) * Q8) * EV) = src[v];
     }
     __syncthreads();
     for (int i = tid; i < n; i += kT)
@@ -147,10 +176,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 #pragma unroll
                     for (int j = 0; j < INR; ++j) acc[r] += x0l[i * IN + j] * w[r][j];
                 }
-                uint2 u;
-                u.x = pkbf(acc[0], acc[1]);
-                u.y = pkbf(acc[2], acc[3]);
-                *reinterpret_cast<uint2*>(xs + i * XS + 4 * q) = u;
+                st4x<XF>(xs + i * XS + 4 * q, acc[0], acc[1], acc[2], acc[3]);
             }
         }
     }
@@ -319,11 +345,11 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             float s = 0.0f;
             if (ok) {
                 const float* gr = gv + dl[p] * GS + h * C;
-                const uint16_t* xr = xs + cl[p] * XS + h * C;
+                const XE* xr = xs + cl[p] * XS + h * C;
                 for (int c = 4 * sl; c < C; c += 64) {
                     const float4 g4 = *reinterpret_cast<const float4*>(gr + c);
-                    const uint2 u = *reinterpret_cast<const uint2*>(xr + c);
-                    s += (g4.x * lo_bf(u.x) + g4.y * hi_bf(u.x)) + (g4.z * lo_bf(u.y) + g4.w * hi_bf(u.y));
+                    const float4 x4 = ld4x<XF>(xr + c);
+                    s += (g4.x * x4.x + g4.y * x4.y) + (g4.z * x4.z + g4.w * x4.w);
                 }
             }
             s = rsum16(s);
@@ -396,12 +422,9 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             o[1] = acc[k][1] + (gs * s4.y + gd * d4.y);
             o[2] = acc[k][2] + (gs * s4.z + gd * d4.z);
             o[3] = acc[k][3] + (gs * s4.w + gd * d4.w);
-            uint2 u;
-            u.x = pkbf(o[0], o[1]);
-            u.y = pkbf(o[2], o[3]);
-            *reinterpret_cast<uint2*>(static_cast<uint16_t*>(a.g_xh) + (size_t)(node0 + j) * HC + f0) = u;
-            if (IN > 0) {  // dL/dx0 through xh = bf16(x0l @ w0^T): the bf16 gradient times w0
-                const float ob[4] = {lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y)};
+            const float4 ov = st4x<XF>(static_cast<XE*>(a.g_xh) + (size_t)(node0 + j) * HC + f0, o[0], o[1], o[2], o[3]);
+            if (IN > 0) {  // dL/dx0 through xh = bf16(x0l @ w0^T): the (bf16) gradient times w0
+                const float ob[4] = {ov.x, ov.y, ov.z, ov.w};
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -428,9 +451,9 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int j = 0; j < INR; ++j) pw0[r][j] = 0.0f;
-        auto node_terms = [&](int j, const uint2 w) {
-            const uint2 u = *reinterpret_cast<const uint2*>(xs + j * XS + 4 * q);
-            const float xv[4] = {lo_bf(u.x), hi_bf(u.x), lo_bf(u.y), hi_bf(u.y)};
+        auto node_terms = [&](int j, const float4 w) {
+            const float4 x4 = ld4x<XF>(xs + j * XS + 4 * q);
+            const float xv[4] = {x4.x, x4.y, x4.z, x4.w};
             const float gs = gas[j * H + h], gd = gad[j * H + h];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -438,7 +461,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
                 pd[r] += gd * xv[r];
             }
             if (IN > 0) {
-                const float gb[4] = {lo_bf(w.x), hi_bf(w.x), lo_bf(w.y), hi_bf(w.y)};
+                const float gb[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -446,13 +469,12 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             }
         };
         auto gxh = [&](int j) {
-            return IN > 0 ? *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(a.g_xh) +
-                                                           (size_t)(node0 + j) * HC + 4 * q)
-                          : make_uint2(0u, 0u);
+            return IN > 0 ? ld4x<XF>(static_cast<const XE*>(a.g_xh) + (size_t)(node0 + j) * HC + 4 * q)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
         };
         int j = 0;
         for (; j + 4 <= n; j += 4) {
-            uint2 w[4];
+            float4 w[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) w[u] = gxh(j + u);
 #pragma unroll
@@ -474,13 +496,13 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 
 size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a) {
     const size_t HC = (size_t)a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
-    return n * (HC + 8) * 2 + n * (HC + 4) * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
+    return (a.exact ? n * (HC + 4) * 4 : n * (HC + 8) * 2) + n * (HC + 4) * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
            (a.g_pool ? 2 * HC * 4 : 0) + (2 * me + 2 * (n + 1) + me) * 4;
 }
 
-template <int HC, int IN, int NT>
+template <int HC, int IN, int NT, bool XF = false>
 static void set_bwd_lds_attr() {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_bwd_kernel<HC, IN, NT>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gat_layer_bwd_kernel<HC, IN, NT, XF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
@@ -496,22 +518,31 @@ hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t str
         set_bwd_lds_attr<512, 4, 1024>();
         set_bwd_lds_attr<256, 0, 1024>();
         set_bwd_lds_attr<256, 4, 1024>();
+        set_bwd_lds_attr<512, 0, 1024, true>();
+        set_bwd_lds_attr<512, 4, 1024, true>();
+        set_bwd_lds_attr<256, 0, 1024, true>();
+        set_bwd_lds_attr<256, 4, 1024, true>();
         attr_set = true;
     }
     const int HC = a.heads * a.channels;
     const size_t smem = gat_layer_bwd_smem(a);
+    if (smem > 160 * 1024) return hipErrorInvalidValue;
     const dim3 grid(a.num_graphs);
-#define TRX_BWD_CASE(HCV, INV, NTV)                                                                    \
-    if (HC == HCV && a.in_dim == INV) {                                                                \
-        hipLaunchKernelGGL((gat_layer_bwd_kernel<HCV, INV, NTV>), grid, dim3(NTV), smem, stream, a);   \
-        return hipGetLastError();                                                                      \
+#define TRX_BWD_CASE(HCV, INV, NTV, XFV)                                                                 \
+    if (HC == HCV && a.in_dim == INV && (a.exact != 0) == XFV) {                                         \
+        hipLaunchKernelGGL((gat_layer_bwd_kernel<HCV, INV, NTV, XFV>), grid, dim3(NTV), smem, stream, a); \
+        return hipGetLastError();                                                                        \
     }
-    TRX_BWD_CASE(1024, 0, 512)
-    TRX_BWD_CASE(1024, 4, 512)
-    TRX_BWD_CASE(512, 0, 1024)
-    TRX_BWD_CASE(512, 4, 1024)
-    TRX_BWD_CASE(256, 0, 1024)
-    TRX_BWD_CASE(256, 4, 1024)
+    TRX_BWD_CASE(1024, 0, 512, false)
+    TRX_BWD_CASE(1024, 4, 512, false)
+    TRX_BWD_CASE(512, 0, 1024, false)
+    TRX_BWD_CASE(512, 4, 1024, false)
+    TRX_BWD_CASE(256, 0, 1024, false)
+    TRX_BWD_CASE(256, 4, 1024, false)
+    TRX_BWD_CASE(512, 0, 1024, true)
+    TRX_BWD_CASE(512, 4, 1024, true)
+    TRX_BWD_CASE(256, 0, 1024, true)
+    TRX_BWD_CASE(256, 4, 1024, true)
 #undef TRX_BWD_CASE
     return hipErrorInvalidValue;
 }
@@ -651,7 +682,7 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(trx_gat_prologue
     float* part = a.part + (size_t)g * (8 * A + 32);
     for (int v = tid; v < A * MD; v += kPBT) {
         const int k = v / MD, j = v - (v / MD) * MD;
-        Ml[v] = j < D ? rbf(a.m_work[k * D + j]) : 0.0f;
+        Ml[v] = j < D ? (a.exact ? a.m_work[k * D + j] : rbf(a.m_work[k * D + j])) : 0.0f;
     }
     for (int l = tid; l < E; l += kPBT) {
         float x[MD], xh[MD];
@@ -718,7 +749,7 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(trx_gat_prologue
             const float* fr = code >= 0 ? ean + ((int64_t)code - link0) * MD : lp + (-(int64_t)code - 1 - node0) * MD;
             const float gk = a.g_a_edge[(size_t)p * A + k];
 #pragma unroll
-            for (int j = 0; j < MD; ++j) gm[j] += gk * (j < D ? rbf(fr[j]) : 0.0f);
+            for (int j = 0; j < MD; ++j) gm[j] += gk * (j < D ? (a.exact ? fr[j] : rbf(fr[j])) : 0.0f);
         }
 #pragma unroll
         for (int j = 0; j < MD; ++j) {

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("TRX_LIB") or os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 9
+ABI_VERSION = 10
 SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
@@ -89,7 +89,7 @@ class TrxGatLayerArgs(ctypes.Structure):
         ("residual", _i32), ("res", _vp), ("wp", _vp), ("bp", _vp),
         ("activation", _i32),
         ("out_f32", _vp), ("out_bf16", _vp), ("pool", _vp),
-        ("save_alpha", _vp), ("save_asd", _vp), ("save_v", _vp), ("save_stats", _vp),
+        ("save_alpha", _vp), ("save_asd", _vp), ("save_v", _vp), ("save_stats", _vp), ("exact", _i32),
     ]
 
 
@@ -122,7 +122,7 @@ class TrxEdgeHeadArgs(ctypes.Structure):
         ("num_graphs", _i32), ("edges_per_graph", _i32), ("hidden", _i32), ("edge_dim", _i32),
         ("src", _vp), ("dst", _vp), ("p", _vp), ("c", _vp), ("ea", _vp), ("we", _vp), ("w2", _vp),
         ("b2", _vp), ("mask", _vp), ("softmax", _i32), ("out", _vp), ("logits", _vp),
-        ("nodes_per_graph", _i32), ("u", _vp), ("action", _vp),
+        ("nodes_per_graph", _i32), ("u", _vp), ("action", _vp), ("exact", _i32),
     ]
 
 
@@ -153,7 +153,7 @@ class TrxGatPrologueArgs(ctypes.Structure):
         ("src", _vp), ("dst", _vp), ("rowptr", _vp), ("pos_src", _vp),
         ("num_layers", _i32), ("heads", _i32 * MAX_GAT_LAYERS), ("channels", _i32 * MAX_GAT_LAYERS),
         ("lin_edge_w", _vp * MAX_GAT_LAYERS), ("att_edge", _vp * MAX_GAT_LAYERS),
-        ("m_work", _vp), ("x0", _vp), ("ea", _vp), ("a_edge", _vp),
+        ("m_work", _vp), ("x0", _vp), ("ea", _vp), ("a_edge", _vp), ("exact", _i32),
     ]
 
 
@@ -168,7 +168,7 @@ class TrxGatLayerBwdArgs(ctypes.Structure):
         ("activation", _i32), ("residual", _i32), ("wp", _vp),
         ("alpha", _vp), ("asd", _vp), ("v", _vp), ("stats", _vp), ("y", _vp),
         ("gy", _vp), ("gy_bf16", _vp), ("g_pool", _vp),
-        ("g_xh", _vp), ("g_res", _vp), ("g_x0", _vp), ("g_a_edge", _vp), ("part", _vp),
+        ("g_xh", _vp), ("g_res", _vp), ("g_x0", _vp), ("g_a_edge", _vp), ("part", _vp), ("exact", _i32),
     ]
 
 
@@ -180,7 +180,7 @@ class TrxGatPrologueBwdArgs(ctypes.Structure):
         ("node_ln_w", _vp), ("node_ln_b", _vp), ("node_ln_eps", _f32),
         ("edge_ln_w", _vp), ("edge_ln_b", _vp), ("edge_ln_eps", _f32),
         ("src", _vp), ("dst", _vp), ("rowptr", _vp), ("pos_src", _vp),
-        ("m_work", _vp), ("g_a_edge", _vp), ("g_x0", _vp), ("g_ea_head", _vp), ("part", _vp),
+        ("m_work", _vp), ("g_a_edge", _vp), ("g_x0", _vp), ("g_ea_head", _vp), ("part", _vp), ("exact", _i32),
     ]
 
 

@@ -357,11 +357,38 @@ def _head_weights(head, into=None):
     return wn, wc.t(), we, w2, b2
 
 
-def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology, keep_m: bool = False):
+def _head_weights_exact(head):
+    """_head_weights for the exact (float32) update mode: every block an
+    unrounded float32 copy (one trx_bf16_round launch in copy mode)."""
+    W1 = head.edge_mlp[0].weight
+    d, k = head.embed, head.edge_in
+    hid = W1.shape[0]
+    dev = W1.device
+    wn = torch.empty(2 * hid, d, device=dev)
+    wc = torch.empty(hid, W1.shape[1] - 2 * d - k, device=dev)
+    we = torch.empty(hid, k, device=dev)
+    w2 = torch.empty(hid, device=dev)
+    b2 = torch.empty(1, device=dev)
+    _round_into([(W1[:, :d], wn[:hid], True), (W1[:, d:2 * d], wn[hid:], True), (W1[:, 2 * d + k:], wc, True),
+                 (W1[:, 2 * d:2 * d + k], we, True), (head.edge_mlp[2].weight.reshape(-1), w2, True),
+                 (head.edge_mlp[2].bias.reshape(-1), b2, True)])
+    return wn, wc.t(), we, w2, b2
+
+
+def exact_supported(model) -> bool:
+    """The exact (float32) kernels' limits: heads*channels <= 512 per layer,
+    edge-MLP hidden <= 256."""
+    return (all(l.heads * l.out_channels <= 512 for l in model.encoder.layers)
+            and model.edge_mlp[0].weight.shape[0] <= 256)
+
+
+def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology, keep_m: bool = False,
+             exact: bool = False):
     """Actor/Critic input LayerNorms + every encoder layer's edge logits in
     CSR order (trx_gat_prologue_infer: one small kernel for the M rows, one
     wave per graph for the rest).  Returns (x0, ea, a_all), or with keep_m
-    ((x0, ea, a_all, M rows), None, None) for the training backward."""
+    ((x0, ea, a_all, M rows), None, None) for the training backward.
+    exact: no bf16 rounding of the M rows / link features / edge logits."""
     L = _lib.load()
     layers = list(model.encoder.layers)
     dev = node_x.device
@@ -392,6 +419,7 @@ def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topolog
         a.heads[i], a.channels[i] = l.heads, l.out_channels
         a.lin_edge_w[i], a.att_edge[i] = w.data_ptr(), at.data_ptr()
     a.m_work, a.x0, a.ea, a.a_edge = m_work.data_ptr(), x0.data_ptr(), ea.data_ptr(), a_all.data_ptr()
+    a.exact = int(exact)
     _lib.check(L.trx_gat_prologue_infer(a, _lib.stream_ptr(dev)), "trx_gat_prologue_infer")
     del keep
     if keep_m:

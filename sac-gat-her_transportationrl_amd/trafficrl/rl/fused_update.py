@@ -32,14 +32,28 @@ from ..models.fused import Topology
 from ..models.skinny import _splitk_wgrad
 
 
+def exact_nets(agent) -> dict:
+    """Which networks' passes run in the exact (float32) mode: every one when
+    the agent trains in float32 (amp off: the reference's precision), the
+    actor's two (next-state probabilities and its training pass) under bf16
+    autocast with agent.fp32_actor (its gradient is the softmax-centred logit
+    difference, which bf16 operands blur: tests/test_fused_update.py)."""
+    full = agent.amp_dtype is None
+    actor = full or bool(getattr(agent, "fp32_actor", False))
+    return {"actor": actor, "critic": full}
+
+
 def supported(agent, topo: Optional[Topology]) -> bool:
-    """The fused update takes regular batches of <= 32-node graphs under bf16
-    autocast on the GPU, with the reference's network shapes."""
-    if topo is None or agent.amp_dtype != torch.bfloat16 or not agent.log_alpha.is_cuda:
+    """The fused update takes regular batches of <= 32-node graphs on the GPU,
+    under bf16 autocast or in float32, with the reference's network shapes."""
+    if topo is None or agent.amp_dtype not in (torch.bfloat16, None) or not agent.log_alpha.is_cuda:
         return False
+    ex = exact_nets(agent)
     for net in (agent.actor, agent.critic1, agent.critic2, agent.target1, agent.target2):
         enc = net.encoder
         if not (fused.encoder_supported(enc) and fused.head_supported(net) and fused.prologue_supported(net)):
+            return False
+        if ex["actor" if net is agent.actor else "critic"] and not fused.exact_supported(net):
             return False
         layers = list(enc.layers)
         if len(layers) != 3 or net.edge_mlp[0].weight.shape[0] > 256:
@@ -98,23 +112,30 @@ def _layer_args(l, norm, topo, a_all, off, stride, i, last):
 
 
 def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology, save: bool,
-                mask: Optional[torch.Tensor] = None):
+                mask: Optional[torch.Tensor] = None, exact: bool = False):
     """Actor/Critic raw edge logits [B*e] (fp32) through the fused kernels, or
     with `mask` the Actor's masked softmax probabilities (sac.py:45-46).
-    save=True also returns the NetCtx the backward needs."""
+    save=True also returns the NetCtx the backward needs.  exact=True: the
+    float32 mode -- float32 GEMMs, activations and weights, no bf16 rounding
+    (the reference's own precision)."""
     L = _lib.load()
     dev = node_x.device
     stream = _lib.stream_ptr(dev)
     enc = net.encoder
     layers = list(enc.layers)
-    x0, ea, a_all = fused.prologue(net, node_x, edge_x, topo, keep_m=save)
+    x0, ea, a_all = fused.prologue(net, node_x, edge_x, topo, keep_m=save, exact=exact)
     m_work = None
     if save:
         x0, ea, a_all, m_work = x0
     N = x0.shape[0]
     stride = a_all.shape[1]
-    wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
-    lin0 = not save and fused.LAYER0_LINEAR and fused.layer0_supported(enc)
+    if exact:
+        ip = enc.input_proj
+        wts = [(layers[0].lin.weight.detach(), ip.weight.detach(), ip.bias.detach())] + \
+              [l.lin.weight.detach() for l in layers[1:]]
+    else:
+        wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
+    lin0 = not save and not exact and fused.LAYER0_LINEAR and fused.layer0_supported(enc)
     mid = lin0 and fused.MID_REGEN and fused.mid_supported(enc)
     keep = []
     recs = []
@@ -127,6 +148,7 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         norm = enc.norms[i]
         args = _layer_args(l, norm, topo, a_all, off, stride, i, last)
         rec = {"off": off, "heads": l.heads, "channels": l.out_channels}
+        args.exact = int(exact)
         if i == 0 and lin0:
             # no-grad passes: the linear-form layer 0 (csrc/gat_layer0.hip)
             out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
@@ -152,9 +174,10 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
             args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
             rec.update(w0=w0, wp=wp)
         else:
-            xh = F.linear(prev_bf16, wts[i])
+            x_in = prev_f32 if exact else prev_bf16
+            xh = F.linear(x_in, wts[i])
             args.in_dim, args.xh = 0, xh.data_ptr()
-            rec.update(xh=xh, x_in=prev_bf16, w=wts[i])
+            rec.update(xh=xh, x_in=x_in, w=wts[i])
             if last:
                 args.residual = 0
             else:
@@ -166,10 +189,10 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         keep += [att_s, att_d, bias, lw, lb]
         args.att_src, args.att_dst, args.bias = att_s.data_ptr(), att_d.data_ptr(), bias.data_ptr()
         args.ln_weight, args.ln_bias = lw.data_ptr(), lb.data_ptr()
-        out_bf16 = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
-        args.out_bf16 = out_bf16.data_ptr()
+        out_bf16 = None if exact else torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+        args.out_bf16 = 0 if exact else out_bf16.data_ptr()
         out_f32 = None
-        if save or (i + 1 < len(layers) - 1):
+        if save or exact or (i + 1 < len(layers) - 1):
             out_f32 = torch.empty(N, HC, device=dev, dtype=torch.float32)
             args.out_f32 = out_f32.data_ptr()
         if last:
@@ -185,14 +208,22 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         recs.append(rec)
         prev_f32, prev_bf16 = out_f32, out_bf16
         off += l.heads
-    emb = prev_bf16
-    head_w = fused._head_weights(net) if save else fused.prepared_head(net)
-    wn, wc, we, w2, b2 = head_w
     b1 = net.edge_mlp[0].bias.detach()
-    p = F.linear(emb, wn)                                       # bf16 [N, 2H] per-node projections
-    c = _mm32(ctx.to(torch.bfloat16), wc, b1)                   # bf16 operands, fp32 product + fp32 bias
+    if exact:
+        emb = prev_f32
+        head_w = fused._head_weights_exact(net)
+        wn, wc, we, w2, b2 = head_w
+        p = F.linear(emb, wn)                                   # float32 [N, 2H]
+        c = torch.addmm(b1, ctx, wc)
+    else:
+        emb = prev_bf16
+        head_w = fused._head_weights(net) if save else fused.prepared_head(net)
+        wn, wc, we, w2, b2 = head_w
+        p = F.linear(emb, wn)                                   # bf16 [N, 2H] per-node projections
+        c = _mm32(ctx.to(torch.bfloat16), wc, b1)               # bf16 operands, fp32 product + fp32 bias
     logits = torch.empty(topo.B * topo.e, device=dev, dtype=torch.float32)
     a = fused._edge_args(p, c, ea, we, w2, b2, topo.src32, topo.dst32, topo.B, topo.n, topo.e)
+    a.exact = int(exact)
     a.out = logits.data_ptr()
     if mask is not None:
         m = mask.float().contiguous()
@@ -237,9 +268,10 @@ def _grad(param, g):
     param.grad = g.view_as(param) if g.shape != param.shape else g
 
 
-def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: GradFlat):
+def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: GradFlat, exact: bool = False):
     """Gradients of every parameter of `net` from dL/dlogits [B*e] fp32,
-    written into `sink` and handed to the parameters as views."""
+    written into `sink` and handed to the parameters as views (exact: the
+    backward of net_forward(..., exact=True), float32 throughout)."""
     L = _lib.load()
     dev = g_logits.device
     stream = _lib.stream_ptr(dev)
@@ -251,6 +283,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     Hd = wn.shape[0] // 2
     # ---- edge scorer (sac.py:42-44 factored): kernel + link-feature / weight products
     a = fused._edge_args(cx.p, cx.c, cx.ea, we, w2, b2, topo.src32, topo.dst32, B, n, e)
+    a.exact = int(exact)
     k = we.shape[1]
     g_p = torch.empty_like(cx.p)
     g_c = torch.empty(B, Hd, device=dev, dtype=torch.float32)
@@ -263,11 +296,16 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     g_we = torch.empty(Hd, k, device=dev, dtype=torch.float32)
     _lib.check(L.trx_partial_sum(_lib.ptr(gwep), B, Hd * k, Hd * k, _lib.ptr(g_we), stream), "trx_partial_sum")
     g_wn = _splitk_wgrad(g_p, cx.emb)                                   # [2H, embed] fp32
-    g_emb = _mm32(g_p, wn)                                              # fp32 [N, embed]
-    g_cb = g_c.to(torch.bfloat16)
-    ctx_b = cx.ctx.to(torch.bfloat16)
-    g_wc = _mm32(g_cb.t(), ctx_b)                                       # [H, 2*embed]
-    g_ctx = _mm32(g_cb, wc.t())                                         # [B, 2*embed]
+    if exact:
+        g_emb = g_p @ wn
+        g_wc = g_c.t() @ cx.ctx
+        g_ctx = g_c @ wc.t()
+    else:
+        g_emb = _mm32(g_p, wn)                                          # fp32 [N, embed]
+        g_cb = g_c.to(torch.bfloat16)
+        ctx_b = cx.ctx.to(torch.bfloat16)
+        g_wc = _mm32(g_cb.t(), ctx_b)                                   # [H, 2*embed]
+        g_ctx = _mm32(g_cb, wc.t())                                     # [B, 2*embed]
     W1 = net.edge_mlp[0].weight
     gW1 = sink.take(W1.numel()).view_as(W1)
     torch.cat([g_wn[:Hd], g_wn[Hd:], g_we, g_wc], 1, out=gW1)
@@ -299,6 +337,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         ba.att_src, ba.att_dst, ba.ln_weight = att_s.data_ptr(), att_d.data_ptr(), lw.data_ptr()
         ba.a_edge, ba.a_edge_stride, ba.a_edge_offset = a_all.data_ptr(), a_all.shape[1], rec["off"]
         ba.negative_slope = float(l.negative_slope)
+        ba.exact = int(exact)
         ba.activation = 1 if last else 0
         ba.residual = 0 if last else (2 if i == 0 else 1)
         if i == 0:
@@ -310,7 +349,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         ba.gy = 0 if gy_f32 is None else gy_f32.data_ptr()
         ba.gy_bf16 = 0 if gy_b16 is None else gy_b16.data_ptr()
         ba.g_pool = 0 if g_pool is None else g_pool.data_ptr()
-        g_xh = torch.empty(N, HC, device=dev, dtype=torch.bfloat16)
+        g_xh = torch.empty(N, HC, device=dev, dtype=torch.float32 if exact else torch.bfloat16)
         g_res = torch.empty(N, HC, device=dev, dtype=torch.float32)
         PW = int(L.trx_gat_layer_backward_part_floats(l.heads, l.out_channels, ba.in_dim))
         part = torch.empty(B, PW, device=dev, dtype=torch.float32)
@@ -331,13 +370,19 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             # lin: xh = x_in @ w^T (bf16): split-K fp32 weight gradient, bf16 input gradient
             x_in = rec["x_in"]
             S = 4 if N % 4 == 0 else 1
-            part_w = torch.bmm(g_xh.view(S, N // S, -1).transpose(1, 2), x_in.view(S, N // S, -1))
             gw = sink.take(l.lin.weight.numel()).view_as(l.lin.weight)
-            torch.sum(part_w, 0, dtype=torch.float32, out=gw)
+            if exact:
+                torch.mm(g_xh.t(), x_in, out=gw)
+            else:
+                part_w = torch.bmm(g_xh.view(S, N // S, -1).transpose(1, 2), x_in.view(S, N // S, -1))
+                torch.sum(part_w, 0, dtype=torch.float32, out=gw)
             _grad(l.lin.weight, gw)
             # the previous layer's output reaches this layer twice: bf16 through lin,
             # fp32 as the residual of a middle layer (gat_encoder.py:44-46)
-            gy_f32 = _mm32(g_xh, rec["w"], g_res if ba.residual == 1 else None)
+            if exact:
+                gy_f32 = torch.addmm(g_res, g_xh, rec["w"]) if ba.residual == 1 else g_xh @ rec["w"]
+            else:
+                gy_f32 = _mm32(g_xh, rec["w"], g_res if ba.residual == 1 else None)
             gy_b16 = None
             g_pool = None
     # ---- prologue: input LayerNorms, loop attrs, edge-logit projections
@@ -358,6 +403,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     PP = 8 * A + 32
     ppart = torch.empty(B, PP, device=dev, dtype=torch.float32)
     pa.part = ppart.data_ptr()
+    pa.exact = int(exact)
     _lib.check(L.trx_gat_prologue_backward(pa, stream), "trx_gat_prologue_backward")
     pp = sink.take(PP)
     _lib.check(L.trx_partial_sum(_lib.ptr(ppart), B, PP, PP, _lib.ptr(pp), stream), "trx_partial_sum")
@@ -403,13 +449,14 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     # critics) and the training forwards of the two critics and the actor (raw
     # logits, with saves) are independent: six streams at once (each network's
     # kernels fill a fraction of the GPU at batch 256)
+    xa, xc = (exact_nets(agent)[k] for k in ("actor", "critic"))
     with torch.no_grad():
         outs = agent._concurrent([
-            lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask)[0],
-            lambda: net_forward(agent.target1, nnx, nex, topo, save=False)[0],
-            lambda: net_forward(agent.target2, nnx, nex, topo, save=False)[0]] +
-            [lambda net=net: net_forward(net, nx, ex, topo, save=True)
-             for net in (agent.critic1, agent.critic2, agent.actor)])
+            lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask, exact=xa)[0],
+            lambda: net_forward(agent.target1, nnx, nex, topo, save=False, exact=xc)[0],
+            lambda: net_forward(agent.target2, nnx, nex, topo, save=False, exact=xc)[0]] +
+            [lambda net=net, x=x: net_forward(net, nx, ex, topo, save=True, exact=x)
+             for net, x in ((agent.critic1, xc), (agent.critic2, xc), (agent.actor, xa))])
     nprobs, qt1, qt2 = outs[:3]
     (q1, c1), (q2, c2), (lg, ca) = outs[3:]
     L = _lib.load()
@@ -457,9 +504,11 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     agent.critic_opt.zero_grad(set_to_none=True)
     agent.actor_opt.zero_grad(set_to_none=True)
     agent.alpha_opt.zero_grad(set_to_none=True)
-    agent._concurrent([lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0]),
-                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1]),
-                       lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2])])
+    # each network's backward on the stream its training forward ran on: the
+    # saved tensors are read on the stream that allocated them
+    agent._concurrent([lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc),
+                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc),
+                       lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa)], streams=(3, 4, 5))
     agent.log_alpha.grad = g_la.view_as(agent.log_alpha)
     agent.grad_flat = flat        # every gradient of this update is a view of it (GradAllReduce)
     agent._warm = True

@@ -324,7 +324,7 @@ class DiscreteSAC:
                  grad_clip: float | None = None, gamma: float = 0.99, target_tau: float = 0.005,
                  target_entropy: float = None, target_entropy_ratio: float = 0.1, alpha_init: float = 0.1,
                  share_critic_encoder: bool = True, device=None, amp_dtype: Optional[torch.dtype] = None,
-                 capturable: bool = False):
+                 capturable: bool = False, fp32_actor: bool = True):
         self.actor = Actor(node_in, edge_in, hidden, embed, num_layers=num_layers)
         self.share_critic_encoder = share_critic_encoder
         if share_critic_encoder:
@@ -369,6 +369,9 @@ class DiscreteSAC:
         self.target_entropy_ratio = target_entropy_ratio
         self.grad_clip = grad_clip
         self.amp_dtype = amp_dtype
+        # fused update under bf16 autocast: the actor's passes in float32
+        # (rl/fused_update.py exact_nets; the critics keep bf16 GEMMs)
+        self.fp32_actor = fp32_actor
         # data-parallel hook: called once per update with every gradient tensor
         self.grad_sync: Optional[Callable[[list], None]] = None
         # independent forwards (and their backwards) on side streams (_concurrent)
@@ -556,22 +559,25 @@ class DiscreteSAC:
             "td_errors": td_error,
         }
 
-    def _concurrent(self, fns):
+    def _concurrent(self, fns, streams=None):
         """Run the callables on side streams forked from (and joined back into)
-        the current stream; sequentially on the CPU, with concurrent=False, or
-        before the first compute_gradients has completed."""
+        the current stream -- fns[i] on side stream streams[i] (default i) --;
+        sequentially on the CPU, with concurrent=False, or before the first
+        compute_gradients has completed."""
         dev = self.log_alpha.device
         if dev.type != "cuda" or not self.concurrent or not self._warm:
             return [fn() for fn in fns]
         main = torch.cuda.current_stream(dev)
-        if self._side is None or len(self._side) < len(fns):
-            self._side = [torch.cuda.Stream(dev) for _ in range(max(3, len(fns)))]
+        streams = list(range(len(fns))) if streams is None else list(streams)
+        if self._side is None or len(self._side) <= max(streams):
+            self._side = [torch.cuda.Stream(dev) for _ in range(max(6, max(streams) + 1))]
+        used = [self._side[k] for k in streams]
         outs = []
-        for st, fn in zip(self._side, fns):
+        for st, fn in zip(used, fns):
             st.wait_stream(main)
             with torch.cuda.stream(st):
                 outs.append(fn())
-        for st in self._side[:len(fns)]:
+        for st in used:
             main.wait_stream(st)
         for o in outs:   # consumed (and freed) on the main stream from here on
             for t in (o if isinstance(o, (tuple, list)) else (o,)):

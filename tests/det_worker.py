@@ -41,8 +41,32 @@ def main():
                her_ratio=0.0, assignment_method="msa", assignment_iters=30, fixed_damage=True, fixed_damage_seed=42,
                sp_backend="scipy", early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0, amp="bf16")
     tr = Trainer(cfg, device="cuda:0", log=False)
-    if os.environ.get("TRX_DET_SERIAL") == "1":   # diagnostics: no side streams in the update
+    serial = os.environ.get("TRX_DET_SERIAL", "")
+    if serial == "1":   # diagnostics: no side streams in the update
         tr.agent.concurrent = False
+    elif serial in ("fwd", "bwd"):   # only the fused update's forward (6 calls) or backward (3) phase serial
+        conc = tr.agent._concurrent
+        n_serial = 6 if serial == "fwd" else 3
+
+        def phase(fns, streams=None):
+            return [fn() for fn in fns] if len(fns) == n_serial else conc(fns, streams)
+        tr.agent._concurrent = phase
+    if os.environ.get("TRX_DET_NOGRAPH") == "1":   # diagnostics: eager updates throughout
+        tr._graphed = None
+    groups = os.environ.get("TRX_DET_FWD_GROUPS", "")   # e.g. "012|345": forward passes concurrent per group
+    if groups:
+        conc = tr.agent._concurrent
+        order = [[int(c) for c in g] for g in groups.split("|")]
+
+        def grouped(fns, streams=None):
+            if len(fns) != 6:
+                return conc(fns, streams)
+            outs = [None] * 6
+            for grp in order:
+                for i, o in zip(grp, conc([fns[i] for i in grp]) if len(grp) > 1 else [fns[grp[0]]()]):
+                    outs[i] = o
+            return outs
+        tr.agent._concurrent = grouped
     tr._reset_envs(None)
     obs = tr.env.observe()
     trace = []
@@ -65,6 +89,7 @@ def main():
         if bad:
             rec["nonfinite_grads"] = ",".join(bad)
             print(f"iteration {it}: non-finite gradients in {bad}", flush=True)
+        print(f"iteration {it}: {rec.get('td', '-')}", flush=True)
         rec["actor"] = _digest(torch.cat([p.detach().reshape(-1) for p in tr.agent.actor.parameters()]))
         rec["critic1"] = _digest(torch.cat([p.detach().reshape(-1) for p in tr.agent.critic1.parameters()]))
         trace.append(rec)

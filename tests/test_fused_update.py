@@ -91,13 +91,15 @@ def test_fused_update_vs_fp32_restatement():
     """Absolute bounds against the fp32 restatement: actor gradients within
     3e-2 per tensor, critics within 6e-2, losses within 6e-2.  The actor's
     gradient is made of the centred logits (softmax backward) and a graph's
-    logits span only ~1e-2 at random init, so the edge scorer computes in
-    fp32 after its bf16 node-projection GEMM (round 3 rounded the hidden
-    units and the logits to bf16, ~1e-3 at their magnitude: 9 % actor error
-    on both bf16 paths)."""
+    logits span only ~1e-2 at random init: every bf16 operand on its path
+    costs 1-2.5 % of it (tools/precision_sites.py attributes the autograd
+    path's 6 % to the rounding sites; no single one dominates), so the actor's
+    passes run in the fused kernels' exact float32 mode (fp32_actor, the
+    default) while the critics keep their bf16 GEMMs."""
     B = 256
     batch = _update_batch(B)
     agent = make_agent(hidden=256, embed=256)
+    assert agent.fp32_actor
     w = torch.rand(B, device="cuda") * 0.5 + 0.5
     out = agent.compute_gradients(batch, weights=w)
     assert agent.last_update_path == "fused"
@@ -115,22 +117,47 @@ def test_fused_update_vs_fp32_restatement():
         assert abs(float(out[k]) - r) <= 6e-2 * max(1e-3, abs(r)), (k, float(out[k]), r)
 
 
+def test_fused_update_fp32_mode_vs_restatement():
+    """amp off (the reference's float32): every pass of the fused update in
+    the kernels' exact mode -- float32 GEMMs, activations, edge logits, no
+    bf16 anywhere -- against autograd over the fp32 restatement: summation
+    order only, every tensor within 2e-3, losses within 1e-4."""
+    B = 256
+    batch = _update_batch(B)
+    agent = make_agent(hidden=256, embed=256, amp=None)
+    w = torch.rand(B, device="cuda") * 0.5 + 0.5
+    out = agent.compute_gradients(batch, weights=w)
+    assert agent.last_update_path == "fused"
+    got, got_alpha = _grads(agent), float(agent.log_alpha.grad)
+    ref, ref_alpha, losses = _ref_grads(agent, batch, w, B)
+    worst = _worst(got, ref)
+    print(f"fused fp32 mode vs fp32 restatement: worst {worst}")
+    assert worst[0] < 2e-3, worst
+    assert abs(got_alpha - ref_alpha) <= 1e-3 * max(1e-6, abs(ref_alpha))
+    for k, r in zip(("critic_loss", "actor_loss", "alpha_loss"), losses):
+        assert abs(float(out[k]) - r) <= 1e-4 * max(1e-3, abs(r)), (k, float(out[k]), r)
+
+
 def test_fused_update_vs_autograd_path():
-    """Same bf16 rounding points, different summation orders: per tensor
-    within 3e-2 (measured 3.6e-3; 1.4e-2 on the actor's last bias, whose
-    gradient vanishes analytically), metrics within 3e-2."""
+    """The bf16 rounding points of autocast (fp32_actor off), different
+    summation orders and layer-0 arithmetic: critics per tensor within 3e-2,
+    the actor within 6e-2 (its centred-logit gradient magnifies the bf16
+    differences, as against fp32), metrics within 3e-2."""
     B = 256
     batch = _update_batch(B)
     agent = make_agent(hidden=256, embed=256)
+    agent.fp32_actor = False
     w = torch.rand(B, device="cuda") * 0.5 + 0.5
     out_f = agent.compute_gradients(batch, weights=w)
     assert agent.last_update_path == "fused"
     got, got_alpha = _grads(agent), float(agent.log_alpha.grad)
     td_f = out_f["td_errors"].clone()
     ref, ref_alpha, out_a = _autograd_grads(agent, batch, w)
-    worst = _worst(got, ref)
-    print(f"fused vs autograd path: worst relative gradient error {worst}")
-    assert worst[0] < 3e-2, worst
+    for m in MODS:
+        sub = {k: v for k, v in ref.items() if k.startswith(m + ".")}
+        worst = _worst({k: got[k] for k in sub}, sub)
+        print(f"{m}: fused vs autograd path: worst relative gradient error {worst}")
+        assert worst[0] < (3e-2 if m != "actor" else 6e-2), (m, worst)
     assert abs(got_alpha - ref_alpha) <= 3e-2 * max(1e-6, abs(ref_alpha))
     torch.testing.assert_close(td_f, out_a["td_errors"].float(), rtol=3e-2, atol=3e-2 * float(td_f.abs().mean()))
     for k in ("critic_loss", "actor_loss", "alpha_loss", "policy_entropy", "q_taken", "q_mean", "logp_mean"):
@@ -153,10 +180,10 @@ def test_fused_update_trajectory():
     autograd path's bf16 gradients, and fp32-restatement gradients.
     Parameter drift = ||theta_x - theta_y|| / distance travelled, per module.
     Against fp32 the fused run drifts no more than the autograd bf16 run
-    (x 1.2 + 2e-2), and the two bf16 runs are no further apart than the
+    (x 1.2 + 2e-2), and the two bf16 critics are no further apart than the
     autograd run is from fp32: Adam turns bf16 gradient noise into
     full-size sign-driven steps on small-gradient weights, so bf16 runs part
-    along the way.  Absolute: every module's fused run within 0.15 of the
+    along the way (the fused actor trains in float32: fp32_actor).  Absolute: every module's fused run within 0.15 of the
     distance travelled from the fp32 run.  Losses of every step within 6e-2
     of fp32."""
     from trafficrl.rl import sac
@@ -188,6 +215,7 @@ def test_fused_update_trajectory():
     for m in MODS:
         dfa, dfr, dar = _drift(a_f, a_a, start, m), _drift(a_f, a_r, start, m), _drift(a_a, a_r, start, m)
         print(f"{m}: drift fused-autograd {dfa:.4f}, fused-fp32 {dfr:.4f}, autograd-fp32 {dar:.4f}")
-        assert dfa <= dar, (m, dfa, dar)
+        if m != "actor":   # both bf16: no further apart than the autograd run is from fp32
+            assert dfa <= dar, (m, dfa, dar)
         assert dfr <= 1.2 * dar + 2e-2, (m, dfr, dar)
         assert dfr <= 0.15, (m, dfr)

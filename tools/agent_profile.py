@@ -23,6 +23,11 @@ def main():
     cfg = sf_config()
     cfg.update(num_envs=B, batch_start=256, update_unit="iterations", eval_every=0, output_dir="/tmp/trx_prof", buffer_size=65536)
     tr = Trainer(cfg, device="cuda:0", log=False)
+    serial = os.environ.get("TRX_UPD_SERIAL", "")   # fwd | bwd: that phase of the fused update on one stream
+    if serial in ("fwd", "bwd"):
+        conc, n_serial = tr.agent._concurrent, (6 if serial == "fwd" else 3)
+        tr.agent._concurrent = lambda fns, streams=None: ([fn() for fn in fns] if len(fns) == n_serial
+                                                         else conc(fns, streams))
     tr._reset_envs(None)
     obs = tr.env.observe()
     for it in range(8):

@@ -75,7 +75,7 @@ for s in "$@"; do
                     step stamps_rand 300 env TRX_DAMAGE=random python tools/phase_stamps.py 4096 &&
                     step stamps_rand_reset 300 env TRX_DAMAGE=random TRX_STAMP_RESET=1 python tools/phase_stamps.py 4096 ;;
         epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --workload env --steps 44 --warmup 22 --no-cpu; done ;;
-        detprobe) step det_probe 500 bash tools/det_probe.sh ;;
+        detprobe) step det_probe 1000 bash tools/det_probe.sh ;;
         dettests) step det_tests 600 python -u -m pytest tests/test_determinism.py -m gpu -v -s --timeout 500 --timeout-method thread ;;
         gattests) step gat_tests 400 python -u -m pytest tests/test_gat_infer.py tests/test_gat.py tests/test_sac.py tests/test_gat_tail.py -m gpu -v --timeout 120 --timeout-method thread ;;
         actmid) TRX_MID=0 step act_mid0 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_mid0 -o run --output-format csv -- python3 tools/agent_profile.py 4096 act &&
@@ -83,6 +83,9 @@ for s in "$@"; do
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         upd) step upd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/upd -o run --output-format csv -- python3 tools/agent_profile.py 4096 update ;;
         overlap) step overlap 300 python tools/overlap_probe.py 4096 ;;
+        gemmrace) step gemm_race 200 python tools/gemm_stream_race.py ;;
+        updserial) step upd_default 300 python tools/agent_profile.py 4096 update &&
+                   TRX_UPD_SERIAL=fwd step upd_fwdserial 300 python tools/agent_profile.py 4096 update ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         hostprobe) step hostprobe 300 python tools/cpu_bound_probe.py 4096 ;;
         mm) step mm 200 python tools/mm_probe.py ;;
