@@ -247,7 +247,7 @@ typedef struct trx_gat_layer_args {
     float* save_stats;          /* [N, 2] LayerNorm mean, rstd                             */
     int32_t exact;              /* ABI 10: 1 = float32 throughout (xh float [N, out], layer 0 computes
                                    xh and the input projection unrounded, x0 unrounded; heads*channels
-                                   <= 512); 0 = the bf16-autocast rounding points above */
+                                   <= 1024); 0 = the bf16-autocast rounding points above */
 } trx_gat_layer_args;
 int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
 
@@ -505,7 +505,8 @@ typedef struct trx_gat_layer_bwd_args {
     float* g_a_edge;            /* [Et, a_edge_stride] */
     float* part;                /* [num_graphs, part_floats] */
     int32_t exact;              /* ABI 10: 1 = backward of the exact forward: xh and g_xh float [N, F],
-                                   w0 / wp unrounded, no bf16 rounding anywhere (heads*channels <= 512) */
+                                   w0 / wp unrounded, no bf16 rounding anywhere (at heads*channels 1024 xh
+                                   is read from global memory, layer 0 recomputes it) */
 } trx_gat_layer_bwd_args;
 int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream);
 int64_t trx_gat_layer_backward_part_floats(int32_t heads, int32_t channels, int32_t in_dim);

@@ -909,6 +909,10 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
         set_lds_attr<512, 4, 512>();
         set_lds_attr<256, 0, 512>();
         set_lds_attr<256, 4, 512>();
+        set_lds_attr<1024, 0, 512, true>();
+        set_lds_attr<1024, 4, 512, true>();
+        set_lds_attr<1024, 0, 256, true>();
+        set_lds_attr<1024, 4, 256, true>();
         set_lds_attr<512, 0, 512, true>();
         set_lds_attr<512, 4, 512, true>();
         set_lds_attr<256, 0, 512, true>();
@@ -936,6 +940,8 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
     TRX_LAYER_CASE(512, 4, false)
     TRX_LAYER_CASE(256, 0, false)
     TRX_LAYER_CASE(256, 4, false)
+    TRX_LAYER_CASE(1024, 0, true)
+    TRX_LAYER_CASE(1024, 4, true)
     TRX_LAYER_CASE(512, 0, true)
     TRX_LAYER_CASE(512, 4, true)
     TRX_LAYER_CASE(256, 0, true)
@@ -982,8 +988,10 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
     constexpr int ED = kEdgeED, NT = kEhbThreads, P = kEhbParts;
     const int g = blockIdx.x, tid = threadIdx.x, k = tid & 255, part = tid >> 8;
     const int E = a.edges_per_graph, Hd = a.hidden, D = a.edge_dim, n = a.nodes_per_graph;
-    XE* pr = reinterpret_cast<XE*>(smem);                               // [n][2*Hd] bf16 (exact: float)
-    float* dzs = reinterpret_cast<float*>(pr + (size_t)n * 2 * Hd);     // [E][Hd] dL/dz (n*2*Hd even)
+    // exact mode: the float p rows are read from global memory (L2) instead of
+    // LDS, which then holds the [E][Hd] dz block and the sums within 160 KB
+    XE* pr = reinterpret_cast<XE*>(smem);                               // [n][2*Hd] bf16 (exact: none)
+    float* dzs = reinterpret_cast<float*>(pr + (XF ? 0 : (size_t)n * 2 * Hd));  // [E][Hd] dL/dz
     float* eal = dzs + (size_t)E * Hd;                                  // [E][ED] link features
     float* gl = eal + (size_t)E * ED;                                   // [E] grad logit
     float* red = gl + E;                                                // [P][2 + ED][256] per-part sums
@@ -995,7 +1003,8 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
     int* op = li + E;                                                   // [n+1] out-list offsets
     int* ip = op + n + 1;                                               // [n+1] in-list offsets
     const int64_t node0 = (int64_t)g * n;
-    {
+    const XE* prow = XF ? static_cast<const XE*>(a.p) + node0 * 2 * Hd : pr;
+    if (!XF) {
         const trx_u4* src4 = reinterpret_cast<const trx_u4*>(static_cast<const XE*>(a.p) + node0 * 2 * Hd);
         trx_u4* dst4 = reinterpret_cast<trx_u4*>(pr);
         for (int v = tid; v < n * 2 * Hd / EV; v += NT) dst4[v] = src4[v];
@@ -1056,7 +1065,7 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
 #pragma unroll
             for (int j = 0; j < ED; ++j)
                 if (j < D) ew += eal[e * ED + j] * we[j];
-            const float z = ((xv(pr[s * 2 * Hd + k]) + xv(pr[d * 2 * Hd + Hd + k])) + ew) + ck;
+            const float z = ((xv(prow[s * 2 * Hd + k]) + xv(prow[d * 2 * Hd + Hd + k])) + ew) + ck;
             const float gb = gl[e];
             gw2 += gb * fmaxf(z, 0.0f);
             const float dz = z > 0.0f ? gb * w2 : 0.0f;
@@ -1121,7 +1130,7 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_hea
 
 size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
     const size_t n = a.nodes_per_graph, E = a.edges_per_graph, H = a.hidden;
-    return n * 2 * H * (a.exact ? 4 : 2) + E * H * 4 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * (2 + kEdgeED) * 256 * 4 +
+    return (a.exact ? 0 : n * 2 * H * 2) + E * H * 4 + E * (kEdgeED * 4 + 4 + 16) + kEhbParts * (2 + kEdgeED) * 256 * 4 +
            256 * kEdgeED * 4 + 2 * (n + 1) * 4;
 }
 

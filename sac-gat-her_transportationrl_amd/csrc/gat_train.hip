@@ -102,6 +102,10 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename XE_<XF>::T XE;
     constexpr int EV = 16 / sizeof(XE);
+    // exact mode at HC 1024: float xh rows and float gv rows do not both fit in
+    // LDS; xh is then read from global memory (layers >= 1) or recomputed from
+    // the 4 inputs (layer 0, the same arithmetic as the staged rows)
+    constexpr bool XG = XF && HC > 512;
     constexpr int KC = HC / 256;  // float4 chunks per lane in a row
     constexpr int kT = NT, kNW = NT / kW;  // threads / waves per workgroup
     constexpr int INR = IN > 0 ? IN : 1;
@@ -117,8 +121,8 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
     // rows padded by 16 B: phase C1 reads four pairs' rows per wave instruction,
     // which unpadded 2 KB / 4 KB strides put on the same LDS banks
     constexpr int XS = HC + EV, GS = HC + 4;
-    XE* xs = reinterpret_cast<XE*>(smem);                      // [n][XS] bf16 lin output (exact: float)
-    float* gv = reinterpret_cast<float*>(xs + n * XS);         // [n][GS] dL/d(aggregate + bias)
+    XE* xs = reinterpret_cast<XE*>(smem);                      // [n][XS] bf16 lin output (exact: float; XG: none)
+    float* gv = reinterpret_cast<float*>(xs + (XG ? 0 : n * XS));  // [n][GS] dL/d(aggregate + bias)
     float* al = gv + n * GS;                                   // [me*H] attention weights
     float* ge = al + a.max_graph_edges * H;                    // [me*H] dL/dalpha, then dL/de
     float* asd = ge + a.max_graph_edges * H;                   // [n][2H] a_src | a_dst
@@ -152,7 +156,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             x0l[v] = XF ? a.x0[(size_t)node0 * IN + v] : rbf(a.x0[(size_t)node0 * IN + v]);
             gx0[v] = 0.0f;
         }
-    if (IN == 0) {
+    if (IN == 0 && !XG) {
         const uint4* src = reinterpret_cast<const uint4*>(static_cast<const XE*>(a.xh) + (size_t)node0 * HC);
         constexpr int Q8 = HC / EV;
         for (int v = tid; v < n * Q8; v += kT)
@@ -161,7 +165,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
     __syncthreads();
     for (int i = tid; i < n; i += kT)
         for (int p = rp[i]; p < rp[i + 1]; ++p) dl[p] = i;
-    if (IN > 0) {  // xh = bf16(x0l @ w0^T), the forward's arithmetic (gat_infer.hip phase 1)
+    if (IN > 0 && !XG) {  // xh = bf16(x0l @ w0^T), the forward's arithmetic (gat_infer.hip phase 1)
         for (int q = tid; q < HC / 4; q += kT) {
             float w[4][INR];
 #pragma unroll
@@ -180,6 +184,23 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             }
         }
     }
+    // xh[i, col..col+3] as floats (staged rows, or the XG sources above)
+    auto xget4 = [&](int i, int col) -> float4 {
+        if constexpr (!XG) {
+            return ld4x<XF>(xs + i * XS + col);
+        } else if constexpr (IN == 0) {
+            return *reinterpret_cast<const float4*>(static_cast<const float*>(a.xh) + (size_t)(node0 + i) * HC + col);
+        } else {
+            float acc[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                acc[r] = 0.0f;
+#pragma unroll
+                for (int j = 0; j < INR; ++j) acc[r] += x0l[i * IN + j] * a.w0[(size_t)(col + r) * IN + j];
+            }
+            return make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
+    };
     if (a.g_pool) {  // column max and its multiplicity over the graph's rows (torch amax backward)
         for (int c = tid; c < HC; c += kT) {
             float mx = -__builtin_huge_valf(), cnt = 0.0f;
@@ -345,10 +366,9 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
             float s = 0.0f;
             if (ok) {
                 const float* gr = gv + dl[p] * GS + h * C;
-                const XE* xr = xs + cl[p] * XS + h * C;
                 for (int c = 4 * sl; c < C; c += 64) {
                     const float4 g4 = *reinterpret_cast<const float4*>(gr + c);
-                    const float4 x4 = ld4x<XF>(xr + c);
+                    const float4 x4 = xget4(cl[p], h * C + c);
                     s += (g4.x * x4.x + g4.y * x4.y) + (g4.z * x4.z + g4.w * x4.w);
                 }
             }
@@ -452,7 +472,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 #pragma unroll
             for (int j = 0; j < INR; ++j) pw0[r][j] = 0.0f;
         auto node_terms = [&](int j, const float4 w) {
-            const float4 x4 = ld4x<XF>(xs + j * XS + 4 * q);
+            const float4 x4 = xget4(j, 4 * q);
             const float xv[4] = {x4.x, x4.y, x4.z, x4.w};
             const float gs = gas[j * H + h], gd = gad[j * H + h];
 #pragma unroll
@@ -496,7 +516,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_arg
 
 size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a) {
     const size_t HC = (size_t)a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
-    return (a.exact ? n * (HC + 4) * 4 : n * (HC + 8) * 2) + n * (HC + 4) * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
+    return (a.exact ? (HC > 512 ? 0 : n * (HC + 4) * 4) : n * (HC + 8) * 2) + n * (HC + 4) * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
            (a.g_pool ? 2 * HC * 4 : 0) + (2 * me + 2 * (n + 1) + me) * 4;
 }
 
@@ -518,6 +538,8 @@ hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t str
         set_bwd_lds_attr<512, 4, 1024>();
         set_bwd_lds_attr<256, 0, 1024>();
         set_bwd_lds_attr<256, 4, 1024>();
+        set_bwd_lds_attr<1024, 0, 512, true>();
+        set_bwd_lds_attr<1024, 4, 512, true>();
         set_bwd_lds_attr<512, 0, 1024, true>();
         set_bwd_lds_attr<512, 4, 1024, true>();
         set_bwd_lds_attr<256, 0, 1024, true>();
@@ -539,6 +561,8 @@ hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t str
     TRX_BWD_CASE(512, 4, 1024, false)
     TRX_BWD_CASE(256, 0, 1024, false)
     TRX_BWD_CASE(256, 4, 1024, false)
+    TRX_BWD_CASE(1024, 0, 512, true)
+    TRX_BWD_CASE(1024, 4, 512, true)
     TRX_BWD_CASE(512, 0, 1024, true)
     TRX_BWD_CASE(512, 4, 1024, true)
     TRX_BWD_CASE(256, 0, 1024, true)

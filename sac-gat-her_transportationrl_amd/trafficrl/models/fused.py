@@ -376,9 +376,9 @@ def _head_weights_exact(head):
 
 
 def exact_supported(model) -> bool:
-    """The exact (float32) kernels' limits: heads*channels <= 512 per layer,
-    edge-MLP hidden <= 256."""
-    return (all(l.heads * l.out_channels <= 512 for l in model.encoder.layers)
+    """The exact (float32) kernels' limits: edge-MLP hidden <= 256 (the
+    layer kernels take heads*channels 256 / 512 / 1024 in both modes)."""
+    return (all(l.heads * l.out_channels <= 1024 for l in model.encoder.layers)
             and model.edge_mlp[0].weight.shape[0] <= 256)
 
 

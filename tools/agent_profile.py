@@ -22,6 +22,8 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
     cfg = sf_config()
     cfg.update(num_envs=B, batch_start=256, update_unit="iterations", eval_every=0, output_dir="/tmp/trx_prof", buffer_size=65536)
+    if os.environ.get("TRX_FP32_ACTOR"):   # A/B the float32 actor of the fused update
+        cfg.update(fp32_actor=os.environ["TRX_FP32_ACTOR"] == "1")
     tr = Trainer(cfg, device="cuda:0", log=False)
     serial = os.environ.get("TRX_UPD_SERIAL", "")   # fwd | bwd: that phase of the fused update on one stream
     if serial in ("fwd", "bwd"):

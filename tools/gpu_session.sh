@@ -83,7 +83,10 @@ for s in "$@"; do
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         upd) step upd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/upd -o run --output-format csv -- python3 tools/agent_profile.py 4096 update ;;
         overlap) step overlap 300 python tools/overlap_probe.py 4096 ;;
+        graphrace) step graph_race 200 python tools/graph_branch_race.py ;;
         gemmrace) step gemm_race 200 python tools/gemm_stream_race.py ;;
+        updactor) TRX_FP32_ACTOR=0 step upd_bf16actor 300 python tools/agent_profile.py 4096 update &&
+                  TRX_FP32_ACTOR=1 step upd_fp32actor 300 python tools/agent_profile.py 4096 update ;;
         updserial) step upd_default 300 python tools/agent_profile.py 4096 update &&
                    TRX_UPD_SERIAL=fwd step upd_fwdserial 300 python tools/agent_profile.py 4096 update ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
