@@ -747,8 +747,10 @@ int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, con
  * dst[k] = bf16(src[k]) for up to TRX_MAX_ROUND row-major blocks in one launch
  * (src rows x cols float32 with row stride src_stride; dst contiguous;
  * out_bf16[k] = 1: bf16 bits, 0: the bf16-rounded value as float32, 2: the
- * float32 value unrounded -- a plain strided copy).  Used to prepare the
- * small weight blocks of the fused inference passes.                       */
+ * float32 value unrounded -- a plain strided copy, 3 (ABI 10): bf16 bits of
+ * the remainder x - bf16(x), the low half of a two-term split x ~ hi + lo).
+ * Used to prepare the small weight blocks of the fused inference passes and
+ * the split operands of the update's three-product float32 GEMMs.          */
 #define TRX_MAX_ROUND 16
 typedef struct trx_round_list {
     int32_t count;

@@ -78,14 +78,23 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     const uint32_t cols = (uint32_t)l.cols[k], n = (uint32_t)(l.rows[k] * l.cols[k]);
     const float* src = l.src[k];
     const int64_t ss = l.src_stride[k];
-    const int mode = l.out_bf16[k];  // 0 bf16-rounded float32, 1 bf16 bits, 2 exact float32 copy
-    const bool bf = mode == 1;
+    // 0 bf16-rounded float32, 1 bf16 bits, 2 exact float32 copy, 3 bf16 bits of the
+    // remainder x - bf16(x) (the low half of a two-term bf16 split)
+    const int mode = l.out_bf16[k];
+    const bool bf = mode == 1 || mode == 3;
+    auto lo = [](float x, __bf16 h) -> __bf16 { return (__bf16)(x - (float)h); };
     const uint32_t step = gridDim.x * 256u;
     if ((cols & 3u) == 0 && (ss & 3) == 0 && ((uintptr_t)src & 15) == 0) {
         for (uint32_t q = blockIdx.x * 256u + threadIdx.x; 4 * q < n; q += step) {
             const uint32_t i = 4 * q, r = i / cols, c = i - r * cols;
             const float4 v = *reinterpret_cast<const float4*>(src + r * ss + c);
-            const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+            __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+            if (mode == 3) {
+                h0 = lo(v.x, h0);
+                h1 = lo(v.y, h1);
+                h2 = lo(v.z, h2);
+                h3 = lo(v.w, h3);
+            }
             if (bf) {
                 uint2 u;
                 u.x = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
@@ -103,7 +112,7 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += step) {
         const uint32_t r = i / cols, c = i - r * cols;
         const float x = src[r * ss + c];
-        const __bf16 h = (__bf16)x;
+        const __bf16 h = mode == 3 ? lo(x, (__bf16)x) : (__bf16)x;
         if (bf)
             static_cast<uint16_t*>(l.dst[k])[i] = __builtin_bit_cast(uint16_t, h);
         else

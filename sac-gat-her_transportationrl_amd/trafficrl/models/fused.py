@@ -153,6 +153,36 @@ def _round_into(pairs):
     _lib.check(L.trx_bf16_round(lst, _lib.stream_ptr(dev)), "trx_bf16_round")
 
 
+def split_bf16(tensors):
+    """Two-term bf16 splits x ~ hi + lo (lo = bf16(x - bf16(x)): 16 mantissa
+    bits together) of float32 tensors with unit column stride, one
+    trx_bf16_round launch for up to 8 tensors: [(hi, lo)] contiguous bf16 of
+    the tensors' shapes.  The operands of the update's three-product float32
+    GEMMs (rl/fused_update.py _mm3)."""
+    assert len(tensors) <= 8
+    L = _lib.load()
+    lst = _lib.TrxRoundList()
+    lst.count = 2 * len(tensors)
+    out = []
+    dev = None
+    for k, t in enumerate(tensors):
+        t = t.detach()
+        t2 = t.reshape(1, -1) if t.dim() == 1 else t
+        assert t2.dtype == torch.float32 and t2.dim() == 2 and t2.stride(1) == 1
+        hi = torch.empty(t2.shape, device=t.device, dtype=torch.bfloat16)
+        lo = torch.empty(t2.shape, device=t.device, dtype=torch.bfloat16)
+        for j, (dst, mode) in enumerate(((hi, 1), (lo, 3))):
+            e = 2 * k + j
+            lst.out_bf16[e] = mode
+            lst.rows[e], lst.cols[e] = t2.shape
+            lst.src_stride[e] = t2.stride(0)
+            lst.src[e], lst.dst[e] = t2.data_ptr(), dst.data_ptr()
+        out.append((hi.view(t.shape), lo.view(t.shape)))
+        dev = t.device
+    _lib.check(L.trx_bf16_round(lst, _lib.stream_ptr(dev)), "trx_bf16_round")
+    return out
+
+
 def weights_changed():
     _PREP_EPOCH[0] += 1
 

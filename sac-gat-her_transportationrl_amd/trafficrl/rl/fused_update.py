@@ -36,8 +36,9 @@ def exact_nets(agent) -> dict:
     """Which networks' passes run in the exact (float32) mode: every one when
     the agent trains in float32 (amp off: the reference's precision), the
     actor's two (next-state probabilities and its training pass) under bf16
-    autocast with agent.fp32_actor (its gradient is the softmax-centred logit
-    difference, which bf16 operands blur: tests/test_fused_update.py)."""
+    autocast with agent.fp32_actor, the actor's training pass and its backward
+    (its gradient is the softmax-centred logit difference, which bf16 operands
+    blur: tests/test_fused_update.py, tools/precision_sites.py)."""
     full = agent.amp_dtype is None
     actor = full or bool(getattr(agent, "fp32_actor", False))
     return {"actor": actor, "critic": full}
@@ -99,6 +100,23 @@ def _mm32(a: torch.Tensor, b: torch.Tensor, add: Optional[torch.Tensor] = None) 
     return r if add is None else r + add
 
 
+def _mm3(a, b, add: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a @ b (+ add) to ~float32 accuracy from two-term bf16 splits a = (a_hi,
+    a_lo), b = (b_hi, b_lo) (models/fused.py split_bf16): a_hi b_lo + a_lo b_hi
+    + a_hi b_hi on the bf16 MFMA path with float32 accumulation (the dropped
+    a_lo b_lo and the splits' rounding are ~2^-16 relative).  Three bf16 GEMMs
+    cost less than one float32 GEMM on gfx950 (no xf32: float32 matrix
+    throughput is 1/16 of bf16's)."""
+    (ah, al), (bh, bl) = a, b
+    c = _mm32(ah, bl, add)
+    c = torch.addmm(c, al, bh, out_dtype=torch.float32) if _MM32[0] else c + (al @ bh).float()
+    if out is None:
+        return torch.addmm(c, ah, bh, out_dtype=torch.float32) if _MM32[0] else c + (ah @ bh).float()
+    if _MM32[0]:
+        return torch.addmm(c, ah, bh, out_dtype=torch.float32, out=out)
+    return out.copy_(c + (ah @ bh).float())
+
+
 def _layer_args(l, norm, topo, a_all, off, stride, i, last):
     args = _lib.TrxGatLayerArgs()
     args.num_graphs, args.nodes_per_graph, args.heads, args.channels = topo.B, topo.n, l.heads, l.out_channels
@@ -130,9 +148,13 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     N = x0.shape[0]
     stride = a_all.shape[1]
     if exact:
+        # float32 weights as they are; the lin / edge-head GEMM operands as
+        # two-term bf16 splits (one launch for the four weight blocks)
         ip = enc.input_proj
         wts = [(layers[0].lin.weight.detach(), ip.weight.detach(), ip.bias.detach())] + \
               [l.lin.weight.detach() for l in layers[1:]]
+        head_w = fused._head_weights_exact(net)
+        wsplit = fused.split_bf16([l.lin.weight for l in layers[1:]] + [head_w[0], head_w[1].t()])
     else:
         wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
     lin0 = not save and not exact and fused.LAYER0_LINEAR and fused.layer0_supported(enc)
@@ -173,8 +195,14 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
             args.in_dim, args.x0, args.w0 = x0.shape[1], x0.data_ptr(), w0.data_ptr()
             args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
             rec.update(w0=w0, wp=wp)
+        elif exact:
+            x_s = fused.split_bf16([prev_f32])[0]
+            w_s = wsplit[i - 1]
+            xh = _mm3(x_s, (w_s[0].t(), w_s[1].t()))              # x_in @ W^T, ~float32
+            args.in_dim, args.xh = 0, xh.data_ptr()
+            rec.update(xh=xh, x_in=x_s, w=w_s)
         else:
-            x_in = prev_f32 if exact else prev_bf16
+            x_in = prev_bf16
             xh = F.linear(x_in, wts[i])
             args.in_dim, args.xh = 0, xh.data_ptr()
             rec.update(xh=xh, x_in=x_in, w=wts[i])
@@ -211,10 +239,12 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     b1 = net.edge_mlp[0].bias.detach()
     if exact:
         emb = prev_f32
-        head_w = fused._head_weights_exact(net)
         wn, wc, we, w2, b2 = head_w
-        p = F.linear(emb, wn)                                   # float32 [N, 2H]
-        c = torch.addmm(b1, ctx, wc)
+        emb_s, ctx_s = fused.split_bf16([emb, ctx])
+        wn_s, wc_s = wsplit[-2], wsplit[-1]                     # wn [2H, d], wc [H, 2d] (contiguous)
+        p = _mm3(emb_s, (wn_s[0].t(), wn_s[1].t()))             # ~float32 [N, 2H]
+        c = _mm3(ctx_s, (wc_s[0].t(), wc_s[1].t()), b1)
+        head_w = (wn, wc, we, w2, b2, emb_s, ctx_s, wn_s, wc_s)
     else:
         emb = prev_bf16
         head_w = fused._head_weights(net) if save else fused.prepared_head(net)
@@ -279,7 +309,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     layers = list(enc.layers)
     B, n, e = topo.B, topo.n, topo.e
     N = B * n
-    wn, wc, we, w2, b2 = cx.head_w
+    wn, wc, we, w2, b2 = cx.head_w[:5]
     Hd = wn.shape[0] // 2
     # ---- edge scorer (sac.py:42-44 factored): kernel + link-feature / weight products
     a = fused._edge_args(cx.p, cx.c, cx.ea, we, w2, b2, topo.src32, topo.dst32, B, n, e)
@@ -295,12 +325,15 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
                                         _lib.ptr(gwep), _lib.ptr(g_ea_head), stream), "trx_edge_head_backward")
     g_we = torch.empty(Hd, k, device=dev, dtype=torch.float32)
     _lib.check(L.trx_partial_sum(_lib.ptr(gwep), B, Hd * k, Hd * k, _lib.ptr(g_we), stream), "trx_partial_sum")
-    g_wn = _splitk_wgrad(g_p, cx.emb)                                   # [2H, embed] fp32
     if exact:
-        g_emb = g_p @ wn
-        g_wc = g_c.t() @ cx.ctx
-        g_ctx = g_c @ wc.t()
+        emb_s, ctx_s, wn_s, wc_s = cx.head_w[5:]
+        gp_s, gc_s = fused.split_bf16([g_p, g_c])
+        g_wn = _mm3((gp_s[0].t(), gp_s[1].t()), emb_s)                  # [2H, embed]
+        g_emb = _mm3(gp_s, wn_s)                                        # [N, embed]
+        g_wc = _mm3((gc_s[0].t(), gc_s[1].t()), ctx_s)                  # [H, 2*embed]
+        g_ctx = _mm3(gc_s, wc_s)                                        # [B, 2*embed]
     else:
+        g_wn = _splitk_wgrad(g_p, cx.emb)                               # [2H, embed] fp32
         g_emb = _mm32(g_p, wn)                                          # fp32 [N, embed]
         g_cb = g_c.to(torch.bfloat16)
         ctx_b = cx.ctx.to(torch.bfloat16)
@@ -372,7 +405,8 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             S = 4 if N % 4 == 0 else 1
             gw = sink.take(l.lin.weight.numel()).view_as(l.lin.weight)
             if exact:
-                torch.mm(g_xh.t(), x_in, out=gw)
+                gx_s = fused.split_bf16([g_xh])[0]
+                _mm3((gx_s[0].t(), gx_s[1].t()), x_in, out=gw)        # g_xh^T x_in
             else:
                 part_w = torch.bmm(g_xh.view(S, N // S, -1).transpose(1, 2), x_in.view(S, N // S, -1))
                 torch.sum(part_w, 0, dtype=torch.float32, out=gw)
@@ -380,7 +414,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             # the previous layer's output reaches this layer twice: bf16 through lin,
             # fp32 as the residual of a middle layer (gat_encoder.py:44-46)
             if exact:
-                gy_f32 = torch.addmm(g_res, g_xh, rec["w"]) if ba.residual == 1 else g_xh @ rec["w"]
+                gy_f32 = _mm3(gx_s, rec["w"], g_res if ba.residual == 1 else None)   # g_xh W (+ residual)
             else:
                 gy_f32 = _mm32(g_xh, rec["w"], g_res if ba.residual == 1 else None)
             gy_b16 = None
@@ -452,7 +486,9 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     xa, xc = (exact_nets(agent)[k] for k in ("actor", "critic"))
     with torch.no_grad():
         outs = agent._concurrent([
-            lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask, exact=xa)[0],
+            # the next-state probabilities only enter the critics' target: the
+            # critics' precision (bf16 unless the agent trains in float32)
+            lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask, exact=xc)[0],
             lambda: net_forward(agent.target1, nnx, nex, topo, save=False, exact=xc)[0],
             lambda: net_forward(agent.target2, nnx, nex, topo, save=False, exact=xc)[0]] +
             [lambda net=net, x=x: net_forward(net, nx, ex, topo, save=True, exact=x)

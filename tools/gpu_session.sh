@@ -45,8 +45,6 @@ for s in "$@"; do
         benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
         wgrad) step wgrad 200 python tools/wgrad_probe.py ;;
         opprobe) step op_probe 300 python tools/op_probe.py ;;
-        castprobe) step cast_probe 300 python tools/cast_probe.py ;;
-        perbench) step per_bench 200 rocprofv3 --kernel-trace --stats -d gpurun_out/perb -o run --output-format csv -- python3 tools/per_bench.py 50 ;;
         envtests) step env_tests 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sparse.py tests/test_gpu_fallback.py tests/test_torch_sp.py tests/test_rewards.py tests/test_replay_train.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         obstests) step obs_tests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_oracle_observe.py tests/test_gpu_gp.py tests/test_rewards.py tests/test_torch_sp.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
         largetests) step large_tests 400 python -u -m pytest tests/test_gpu_large.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
@@ -83,6 +81,9 @@ for s in "$@"; do
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         upd) step upd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/upd -o run --output-format csv -- python3 tools/agent_profile.py 4096 update ;;
         overlap) step overlap 300 python tools/overlap_probe.py 4096 ;;
+        updrace) step upd_race 300 python tools/update_graph_race.py 30 default &&
+                 step upd_race_fwd 300 python tools/update_graph_race.py 30 fwdserial &&
+                 step upd_race_nopatch 300 python tools/update_graph_race.py 30 nopatch ;;
         graphrace) step graph_race 200 python tools/graph_branch_race.py ;;
         gemmrace) step gemm_race 200 python tools/gemm_stream_race.py ;;
         updactor) TRX_FP32_ACTOR=0 step upd_bf16actor 300 python tools/agent_profile.py 4096 update &&
@@ -90,9 +91,6 @@ for s in "$@"; do
         updserial) step upd_default 300 python tools/agent_profile.py 4096 update &&
                    TRX_UPD_SERIAL=fwd step upd_fwdserial 300 python tools/agent_profile.py 4096 update ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
-        hostprobe) step hostprobe 300 python tools/cpu_bound_probe.py 4096 ;;
-        mm) step mm 200 python tools/mm_probe.py ;;
-        actmm) step actmm 200 python tools/act_gemm_probe.py ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
         copies) step copies 300 python tools/update_profile.py 60 copies ;;
         istamps) step istamps 300 python tools/infer_stamps.py 4096 ;;
@@ -103,7 +101,6 @@ for s in "$@"; do
         bigstats) step big_stats 300 python tools/big_stats.py 1024 fw ;;
         actab) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_l03.so; do [ -f $f ] || continue; n=$(basename $f .so); TRX_LIB=$PWD/$f step actab_$n 200 python tools/act_host_probe.py 4096 || exit 1; done
                grep -h "eager" gpurun_out/actab_*.log ;;
-        gemmlay) step gemm_layouts 200 python tools/act_gemm_layouts.py ;;
         actprobe) step act_probe 300 python tools/act_host_probe.py 4096 ;;
         graphtests) step graph_tests 400 python -u -m pytest tests/test_replay_train.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         fallback) step fallback_tests 400 python -u -m pytest tests/test_gpu_fallback.py -m gpu -x -v --timeout 300 --timeout-method thread ;;

@@ -1,0 +1,89 @@
+"""Is the captured fused SAC update a deterministic function of its inputs?
+
+One DiscreteSAC (the bench's hidden = embed = 256, bf16 autocast) and one
+fixed batch of 256 synthetic Sioux Falls graphs: compute_gradients is run
+eagerly (warm-up, side streams on), captured once with train.capture_graph
+(memset patch, pinned caches) and replayed; every replay's TD errors and
+flat gradient buffer are compared bitwise with the first replay's and with an
+eager call's.  No optimizer step: the inputs never change.
+
+usage: python tools/update_graph_race.py [replays] [mode]
+mode: default | fwdserial | bwdserial | serial | nopatch"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sac-gat-her_transportationrl_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    from test_gat import batched_graph
+    from trafficrl import _lib
+    from trafficrl.rl.sac import DiscreteSAC
+    from trafficrl import train as T
+
+    R = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    mode = sys.argv[2] if len(sys.argv) > 2 else "default"
+    dev = "cuda"
+    torch.manual_seed(0)
+    B = 256
+    ei, bv, N, E = batched_graph(B, dev)
+    g = torch.Generator(device=dev).manual_seed(1)
+    nx = torch.rand(B * N, 4, device=dev, generator=g)
+    ex = torch.rand(B * E, 6, device=dev, generator=g)
+    mask = (torch.rand(B * E, device=dev, generator=g) < 0.3).float()
+    mask.view(B, E)[:, 0] = 1
+    nnx = torch.rand(B * N, 4, device=dev, generator=g)
+    nex = torch.rand(B * E, 6, device=dev, generator=g)
+    nmask = (torch.rand(B * E, device=dev, generator=g) < 0.3).float()
+    nmask.view(B, E)[:, 0] = 1
+    a = torch.randint(0, E, (B,), device=dev, generator=g)
+    action = torch.arange(B, device=dev) * E + a
+    reward = torch.rand(B, device=dev, generator=g)
+    done = (torch.rand(B, device=dev, generator=g) < 0.1).float()
+    batch = (nx, ei, ex, mask, bv, action, reward, nnx, nex, nmask, bv, done)
+    w = torch.rand(B, device=dev, generator=g) * 0.5 + 0.5
+    ag = DiscreteSAC(4, 6, 256, 256, num_layers=3, lr=1e-4, grad_clip=1.0, share_critic_encoder=False,
+                     alpha_init=0.1, target_entropy_ratio=0.2, device=dev, amp_dtype=torch.bfloat16, capturable=True)
+    conc = ag._concurrent
+    if mode == "serial":
+        ag.concurrent = False
+    elif mode in ("fwdserial", "bwdserial"):
+        n_serial = 6 if mode == "fwdserial" else 3
+        ag._concurrent = lambda fns, streams=None: ([f() for f in fns] if len(fns) == n_serial
+                                                    else conc(fns, streams))
+    if mode == "nopatch":
+        _lib.patch_graph_memsets = lambda gr: 0
+
+    def snap(out):
+        return out["td_errors"].clone(), ag.grad_flat.clone()
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            out = ag.compute_gradients(batch, weights=w)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert ag.last_update_path == "fused", ag.last_update_path
+    eager = snap(out)
+    gr, out = T.capture_graph(lambda: ag.compute_gradients(batch, weights=w))
+    first = None
+    bad_first = bad_eager = 0
+    for r in range(R):
+        gr.replay()
+        torch.cuda.synchronize()
+        cur = snap(out)
+        if first is None:
+            first = cur
+        bad_first += int(not all(torch.equal(x, y) for x, y in zip(cur, first)))
+        bad_eager += int(not all(torch.equal(x, y) for x, y in zip(cur, eager)))
+    print(f"mode {mode}: {bad_first}/{R} replays differ from the first replay, {bad_eager}/{R} from the eager call",
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
