@@ -195,17 +195,16 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
             args.in_dim, args.x0, args.w0 = x0.shape[1], x0.data_ptr(), w0.data_ptr()
             args.residual, args.wp, args.bp = 2, wp.data_ptr(), bp.data_ptr()
             rec.update(w0=w0, wp=wp)
-        elif exact:
-            x_s = fused.split_bf16([prev_f32])[0]
-            w_s = wsplit[i - 1]
-            xh = _mm3(x_s, (w_s[0].t(), w_s[1].t()))              # x_in @ W^T, ~float32
-            args.in_dim, args.xh = 0, xh.data_ptr()
-            rec.update(xh=xh, x_in=x_s, w=w_s)
         else:
-            x_in = prev_bf16
-            xh = F.linear(x_in, wts[i])
+            if exact:
+                x_s = fused.split_bf16([prev_f32])[0]
+                w_s = wsplit[i - 1]
+                xh = _mm3(x_s, (w_s[0].t(), w_s[1].t()))          # x_in @ W^T, ~float32
+                rec.update(xh=xh, x_in=x_s, w=w_s)
+            else:
+                xh = F.linear(prev_bf16, wts[i])
+                rec.update(xh=xh, x_in=prev_bf16, w=wts[i])
             args.in_dim, args.xh = 0, xh.data_ptr()
-            rec.update(xh=xh, x_in=x_in, w=wts[i])
             if last:
                 args.residual = 0
             else:

@@ -41,6 +41,7 @@ for s in "$@"; do
                     step bench_env_torch 400 python bench.py --workload env --sp torch --steps 66 --warmup 22 --no-cpu ;;
         benchgreedy) step bench_greedy 400 python bench.py --workload greedy --iters 60 --cpu-seconds 5 &&
                      step bench_greedy30 400 python bench.py --workload greedy --iters 30 --cpu-seconds 5 ;;
+        benchfw) step bench_fw 400 python bench.py --method fw --steps 44 --warmup 22 --cpu-seconds 5 ;;
         benchana) step bench_ana 600 python bench.py --network anaheim --steps 10 --warmup 3 --cpu-seconds 5 ;;
         benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
         wgrad) step wgrad 200 python tools/wgrad_probe.py ;;
@@ -81,10 +82,13 @@ for s in "$@"; do
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         upd) step upd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/upd -o run --output-format csv -- python3 tools/agent_profile.py 4096 update ;;
         overlap) step overlap 300 python tools/overlap_probe.py 4096 ;;
-        updrace) step upd_race 300 python tools/update_graph_race.py 30 default &&
+        updrace) TRX_RACE_REC=0 step upd_race_norec 300 python tools/update_graph_race.py 30 default &&
+                 step upd_race 300 python tools/update_graph_race.py 30 default &&
                  step upd_race_fwd 300 python tools/update_graph_race.py 30 fwdserial &&
                  step upd_race_nopatch 300 python tools/update_graph_race.py 30 nopatch ;;
         graphrace) step graph_race 200 python tools/graph_branch_race.py ;;
+        trxchain) step trx_chain 300 python tools/trx_chain_race.py ;;
+        gemmcons) step gemm_cons 300 python tools/gemm_consumer_race.py ;;
         gemmrace) step gemm_race 200 python tools/gemm_stream_race.py ;;
         updactor) TRX_FP32_ACTOR=0 step upd_bf16actor 300 python tools/agent_profile.py 4096 update &&
                   TRX_FP32_ACTOR=1 step upd_fp32actor 300 python tools/agent_profile.py 4096 update ;;

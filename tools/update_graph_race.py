@@ -58,6 +58,31 @@ def main():
     if mode == "nopatch":
         _lib.patch_graph_memsets = lambda gr: 0
 
+    # every forward's outputs (logits, and with saves its per-layer tensors), by name,
+    # recorded at capture time: a replay-to-replay difference names the first corrupted one
+    from trafficrl.rl import fused_update as FU
+    rec = {}
+    orig_fwd = FU.net_forward
+    names = {id(ag.actor): "actor", id(ag.critic1): "critic1", id(ag.critic2): "critic2",
+             id(ag.target1): "target1", id(ag.target2): "target2"}
+
+    def fwd(net, *a, **k):
+        lg, cx = orig_fwd(net, *a, **k)
+        tag = names[id(net)] + ("_train" if k.get("save") else "_next")
+        rec[tag + ".logits"] = lg
+        if cx is not None:
+            for key in ("x0", "ea", "a_all", "emb", "ctx", "p", "c"):
+                t = getattr(cx, key)
+                if isinstance(t, torch.Tensor):
+                    rec[f"{tag}.{key}"] = t
+            for i, r in enumerate(cx.layers):
+                for key, t in r.items():
+                    if isinstance(t, torch.Tensor):
+                        rec[f"{tag}.L{i}.{key}"] = t
+        return lg, cx
+    if os.environ.get("TRX_RACE_REC", "1") == "1":   # 0: no references held (the allocator's own reuse)
+        FU.net_forward = fwd
+
     def snap(out):
         return out["td_errors"].clone(), ag.grad_flat.clone()
 
@@ -70,19 +95,32 @@ def main():
     torch.cuda.synchronize()
     assert ag.last_update_path == "fused", ag.last_update_path
     eager = snap(out)
+    rec.clear()
     gr, out = T.capture_graph(lambda: ag.compute_gradients(batch, weights=w))
+    captured = dict(rec)
+    first_int = None
+    diff_names = {}
     first = None
     bad_first = bad_eager = 0
     for r in range(R):
         gr.replay()
         torch.cuda.synchronize()
         cur = snap(out)
+        ints = {k: v.clone() for k, v in captured.items()}
+        if first_int is None:
+            first_int = ints
+        else:
+            for k in captured:   # in recording (computation) order
+                if not torch.equal(ints[k], first_int[k]):
+                    diff_names[k] = diff_names.get(k, 0) + 1
         if first is None:
             first = cur
         bad_first += int(not all(torch.equal(x, y) for x, y in zip(cur, first)))
         bad_eager += int(not all(torch.equal(x, y) for x, y in zip(cur, eager)))
     print(f"mode {mode}: {bad_first}/{R} replays differ from the first replay, {bad_eager}/{R} from the eager call",
           flush=True)
+    print("forward tensors that differ between replays (name: replays):",
+          [(k, n) for k, n in diff_names.items()][:40], flush=True)
 
 
 if __name__ == "__main__":
