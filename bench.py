@@ -601,7 +601,10 @@ def main():
                 "method": args.method, "assignment_iters": args.iters, "episode_len": ep_len,
                 "parallelism": f"env-sharded x{world}",
                 **({"gemm_kernels": ("TunableOp selection trafficrl/gemm_tuning_gfx950.csv (lookup only)"
-                                     if tr.tuned_gemms else "torch default")} if args.workload == "train" else {}),
+                                     if tr.tuned_gemms else "torch default"),
+                    "update_precision": ("critics bf16 autocast; actor training pass float32 (exact kernels, "
+                                         "three-product split-bf16 GEMMs)" if tr.agent.fp32_actor
+                                         else "bf16 autocast")} if args.workload == "train" else {}),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

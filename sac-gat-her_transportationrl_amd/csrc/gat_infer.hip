@@ -212,6 +212,13 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
     int* dlc = rp + n + 1;                               // [me] graph-local destination per CSR position
     float* x0l = reinterpret_cast<float*>(dlc + a.max_graph_edges);  // [n*IN]
     float* yt = x0l + n * IN;                            // [n][HC] (pool only)
+#ifdef TRX_LDS_CLEAR
+    {  // diagnostic build: zero the workgroup's whole LDS window first (uninitialised-read probe)
+        const int words = (int)((reinterpret_cast<char*>(yt + (a.pool ? n * HC : 0)) - smem) / 4);
+        for (int w = tid; w < words; w += kInferThreads) reinterpret_cast<float*>(smem)[w] = 0.0f;
+        __syncthreads();
+    }
+#endif
 
     // 0b. graph-local CSR slice, this layer's edge logits, layer-0 inputs: every
     //     load of the phase issued before the first LDS store (one HBM round trip)

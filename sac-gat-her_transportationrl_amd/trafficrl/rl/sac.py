@@ -374,8 +374,15 @@ class DiscreteSAC:
         self.fp32_actor = fp32_actor
         # data-parallel hook: called once per update with every gradient tensor
         self.grad_sync: Optional[Callable[[list], None]] = None
-        # independent forwards (and their backwards) on side streams (_concurrent)
+        # independent forwards (and their backwards) on side streams (_concurrent),
+        # at most max_streams at once (3: the fastest measured, tools/agent_profile.py).
+        # Concurrent branches make the captured update's GAT layer kernels differ
+        # from replay to replay in the last bits (tools/layer_concurrency_race.py:
+        # same inputs, different outputs; serialized streams reproducible; DESIGN
+        # §5): max_streams = 1 (Trainer deterministic_update) gives bitwise
+        # reproducible training
         self.concurrent = True
+        self.max_streams = 3
         self._side = None
         self._warm = False
         self.last_update_path = None   # "fused" (rl/fused_update.py) or "autograd"
@@ -569,15 +576,21 @@ class DiscreteSAC:
             return [fn() for fn in fns]
         main = torch.cuda.current_stream(dev)
         streams = list(range(len(fns))) if streams is None else list(streams)
-        if self._side is None or len(self._side) <= max(streams):
-            self._side = [torch.cuda.Stream(dev) for _ in range(max(6, max(streams) + 1))]
-        used = [self._side[k] for k in streams]
+        # logical stream k runs on side stream k % max_streams: at most max_streams
+        # branches at once (the calls of one side stream run in order)
+        width = max(1, int(self.max_streams))
+        if self._side is None or len(self._side) < width:
+            self._side = [torch.cuda.Stream(dev) for _ in range(width)]
+        used = [self._side[k % width] for k in streams]
         outs = []
+        forked = set()
         for st, fn in zip(used, fns):
-            st.wait_stream(main)
+            if id(st) not in forked:
+                st.wait_stream(main)
+                forked.add(id(st))
             with torch.cuda.stream(st):
                 outs.append(fn())
-        for st in used:
+        for st in {id(s): s for s in used}.values():
             main.wait_stream(st)
         for o in outs:   # consumed (and freed) on the main stream from here on
             for t in (o if isinstance(o, (tuple, list)) else (o,)):

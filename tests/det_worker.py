@@ -39,8 +39,11 @@ def main():
     cfg.update(num_envs=512, batch_start=512, batch_size=256, hidden_dim=256, embed_dim=256, eval_every=0,
                output_dir=os.path.join(os.path.dirname(out), "det_run"), update_every=1, update_unit="iterations",
                her_ratio=0.0, assignment_method="msa", assignment_iters=30, fixed_damage=True, fixed_damage_seed=42,
-               sp_backend="scipy", early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0, amp="bf16")
+               sp_backend="scipy", early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0, amp="bf16",
+               deterministic_update=os.environ.get("TRX_DET_CONCURRENT") != "1")
     tr = Trainer(cfg, device="cuda:0", log=False)
+    if os.environ.get("TRX_UPD_STREAMS"):   # concurrent side streams of the update (A/B)
+        tr.agent.max_streams = int(os.environ["TRX_UPD_STREAMS"])
     serial = os.environ.get("TRX_DET_SERIAL", "")
     if serial == "1":   # diagnostics: no side streams in the update
         tr.agent.concurrent = False

@@ -30,6 +30,8 @@ def main():
         conc, n_serial = tr.agent._concurrent, (6 if serial == "fwd" else 3)
         tr.agent._concurrent = lambda fns, streams=None: ([fn() for fn in fns] if len(fns) == n_serial
                                                          else conc(fns, streams))
+    if os.environ.get("TRX_UPD_STREAMS"):   # concurrent side streams of the update (A/B)
+        tr.agent.max_streams = int(os.environ["TRX_UPD_STREAMS"])
     tr._reset_envs(None)
     obs = tr.env.observe()
     for it in range(8):

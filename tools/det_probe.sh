@@ -8,6 +8,7 @@ mkdir -p gpurun_out/det
 for mode in ${DET_MODES:-default serial}; do
     for k in 1 2; do
         unset TRX_DET_SERIAL TRX_DET_FWD_GROUPS TRX_DET_NOGRAPH
+        export TRX_DET_CONCURRENT=1   # the probe studies the concurrent default
         fill=0
         case $mode in
             serial) export TRX_DET_SERIAL=1 ;;
