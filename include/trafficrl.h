@@ -745,7 +745,7 @@ int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, con
 
 /* ------------------------------------------------ multi-tensor bf16 round
  * dst[k] = bf16(src[k]) for up to TRX_MAX_ROUND row-major blocks in one launch
- * (src rows x cols float32 with row stride src_stride; dst contiguous;
+ * (src rows x cols float32 with row stride src_stride; dst rows dst_stride apart;
  * out_bf16[k] = 1: bf16 bits, 0: the bf16-rounded value as float32, 2: the
  * float32 value unrounded -- a plain strided copy, 3 (ABI 10): bf16 bits of
  * the remainder x - bf16(x), the low half of a two-term split x ~ hi + lo).
@@ -758,6 +758,8 @@ typedef struct trx_round_list {
     int64_t rows[TRX_MAX_ROUND], cols[TRX_MAX_ROUND], src_stride[TRX_MAX_ROUND];
     const float* src[TRX_MAX_ROUND];
     void* dst[TRX_MAX_ROUND];
+    int64_t dst_stride[TRX_MAX_ROUND];  /* ABI 10: dst row stride in elements (0: cols, contiguous) --
+                                           the column blocks of the split GEMM operands */
 } trx_round_list;
 int trx_bf16_round(const trx_round_list* l, void* stream);
 

@@ -78,15 +78,18 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     const uint32_t cols = (uint32_t)l.cols[k], n = (uint32_t)(l.rows[k] * l.cols[k]);
     const float* src = l.src[k];
     const int64_t ss = l.src_stride[k];
+    const uint32_t ds = l.dst_stride[k] > 0 ? (uint32_t)l.dst_stride[k] : cols;  // dst row stride (elements)
     // 0 bf16-rounded float32, 1 bf16 bits, 2 exact float32 copy, 3 bf16 bits of the
     // remainder x - bf16(x) (the low half of a two-term bf16 split)
     const int mode = l.out_bf16[k];
     const bool bf = mode == 1 || mode == 3;
     auto lo = [](float x, __bf16 h) -> __bf16 { return (__bf16)(x - (float)h); };
     const uint32_t step = gridDim.x * 256u;
-    if ((cols & 3u) == 0 && (ss & 3) == 0 && ((uintptr_t)src & 15) == 0) {
+    if ((cols & 3u) == 0 && (ss & 3) == 0 && (ds & 3u) == 0 && ((uintptr_t)src & 15) == 0 &&
+        ((uintptr_t)l.dst[k] & 15) == 0) {
         for (uint32_t q = blockIdx.x * 256u + threadIdx.x; 4 * q < n; q += step) {
-            const uint32_t i = 4 * q, r = i / cols, c = i - r * cols;
+            const uint32_t i0 = 4 * q, r = i0 / cols, c = i0 - r * cols;
+            const uint32_t i = r * ds + c;  // destination element
             const float4 v = *reinterpret_cast<const float4*>(src + r * ss + c);
             __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
             if (mode == 3) {
@@ -109,8 +112,8 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
         }
         return;
     }
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += step) {
-        const uint32_t r = i / cols, c = i - r * cols;
+    for (uint32_t i0 = blockIdx.x * 256u + threadIdx.x; i0 < n; i0 += step) {
+        const uint32_t r = i0 / cols, c = i0 - r * cols, i = r * ds + c;
         const float x = src[r * ss + c];
         const __bf16 h = mode == 3 ? lo(x, (__bf16)x) : (__bf16)x;
         if (bf)
@@ -125,7 +128,9 @@ hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream) {
     int64_t mx = 1;
     for (int k = 0; k < l.count; ++k) {
         const int64_t n = l.rows[k] * l.cols[k];
-        if (n >= ((int64_t)1 << 31) || l.rows[k] * l.src_stride[k] >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+        if (n >= ((int64_t)1 << 31) || l.rows[k] * l.src_stride[k] >= ((int64_t)1 << 31) ||
+            l.rows[k] * l.dst_stride[k] >= ((int64_t)1 << 31))
+            return hipErrorInvalidValue;
         mx = n > mx ? n : mx;
     }
     const int64_t blocks = (mx + 1023) / 1024;  // ~4 elements per thread

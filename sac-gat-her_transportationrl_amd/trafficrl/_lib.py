@@ -220,7 +220,7 @@ class TrxRoundList(ctypes.Structure):
     _fields_ = [
         ("count", _i32), ("out_bf16", _i32 * MAX_ROUND), ("rows", ctypes.c_int64 * MAX_ROUND),
         ("cols", ctypes.c_int64 * MAX_ROUND), ("src_stride", ctypes.c_int64 * MAX_ROUND),
-        ("src", _vp * MAX_ROUND), ("dst", _vp * MAX_ROUND),
+        ("src", _vp * MAX_ROUND), ("dst", _vp * MAX_ROUND), ("dst_stride", ctypes.c_int64 * MAX_ROUND),
     ]
 
 

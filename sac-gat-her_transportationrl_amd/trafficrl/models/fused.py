@@ -153,34 +153,41 @@ def _round_into(pairs):
     _lib.check(L.trx_bf16_round(lst, _lib.stream_ptr(dev)), "trx_bf16_round")
 
 
-def split_bf16(tensors):
-    """Two-term bf16 splits x ~ hi + lo (lo = bf16(x - bf16(x)): 16 mantissa
-    bits together) of float32 tensors with unit column stride, one
-    trx_bf16_round launch for up to 8 tensors: [(hi, lo)] contiguous bf16 of
-    the tensors' shapes.  The operands of the update's three-product float32
-    GEMMs (rl/fused_update.py _mm3)."""
-    assert len(tensors) <= 8
+def split3(specs):
+    """Three-term bf16 operands of a ~float32 product from one GEMM (the
+    update's float32 actor, rl/fused_update.py _mm3).  x ~ hi + lo with
+    hi = bf16(x), lo = bf16(x - hi) (16 mantissa bits together); a product
+    a b ~ a_hi b_lo + a_hi b_hi + a_lo b_hi is one bf16 GEMM over a tripled
+    contraction: the A operand's pieces in order "hhl", the B operand's "lhh".
+    specs: [(x, layout, order)] with x float32 [R, C] (unit column stride),
+    layout "cols" -> [R, 3C] (pieces side by side: contraction over columns)
+    or "rows" -> [3R, C] (stacked: contraction over rows), order a 3-letter
+    string of h / l.  One trx_bf16_round launch per 5 specs."""
     L = _lib.load()
-    lst = _lib.TrxRoundList()
-    lst.count = 2 * len(tensors)
-    out = []
-    dev = None
-    for k, t in enumerate(tensors):
-        t = t.detach()
-        t2 = t.reshape(1, -1) if t.dim() == 1 else t
-        assert t2.dtype == torch.float32 and t2.dim() == 2 and t2.stride(1) == 1
-        hi = torch.empty(t2.shape, device=t.device, dtype=torch.bfloat16)
-        lo = torch.empty(t2.shape, device=t.device, dtype=torch.bfloat16)
-        for j, (dst, mode) in enumerate(((hi, 1), (lo, 3))):
-            e = 2 * k + j
-            lst.out_bf16[e] = mode
-            lst.rows[e], lst.cols[e] = t2.shape
-            lst.src_stride[e] = t2.stride(0)
-            lst.src[e], lst.dst[e] = t2.data_ptr(), dst.data_ptr()
-        out.append((hi.view(t.shape), lo.view(t.shape)))
-        dev = t.device
-    _lib.check(L.trx_bf16_round(lst, _lib.stream_ptr(dev)), "trx_bf16_round")
-    return out
+    outs = []
+    for b0 in range(0, len(specs), 5):
+        lst = _lib.TrxRoundList()
+        e = 0
+        dev = None
+        for x, layout, order in specs[b0:b0 + 5]:
+            x = x.detach()
+            assert x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1 and len(order) == 3
+            R, C = x.shape
+            cols = layout == "cols"
+            out = torch.empty((R, 3 * C) if cols else (3 * R, C), device=x.device, dtype=torch.bfloat16)
+            for k, ch in enumerate(order):
+                lst.out_bf16[e] = 1 if ch == "h" else 3
+                lst.rows[e], lst.cols[e] = R, C
+                lst.src_stride[e] = x.stride(0)
+                lst.src[e] = x.data_ptr()
+                lst.dst[e] = out.data_ptr() + 2 * (k * C if cols else k * R * C)
+                lst.dst_stride[e] = 3 * C if cols else 0
+                e += 1
+            outs.append(out)
+            dev = x.device
+        lst.count = e
+        _lib.check(L.trx_bf16_round(lst, _lib.stream_ptr(dev)), "trx_bf16_round")
+    return outs
 
 
 def weights_changed():

@@ -100,21 +100,24 @@ def _mm32(a: torch.Tensor, b: torch.Tensor, add: Optional[torch.Tensor] = None) 
     return r if add is None else r + add
 
 
-def _mm3(a, b, add: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """a @ b (+ add) to ~float32 accuracy from two-term bf16 splits a = (a_hi,
-    a_lo), b = (b_hi, b_lo) (models/fused.py split_bf16): a_hi b_lo + a_lo b_hi
-    + a_hi b_hi on the bf16 MFMA path with float32 accumulation (the dropped
-    a_lo b_lo and the splits' rounding are ~2^-16 relative).  Three bf16 GEMMs
-    cost less than one float32 GEMM on gfx950 (no xf32: float32 matrix
-    throughput is 1/16 of bf16's)."""
-    (ah, al), (bh, bl) = a, b
-    c = _mm32(ah, bl, add)
-    c = torch.addmm(c, al, bh, out_dtype=torch.float32) if _MM32[0] else c + (al @ bh).float()
+def _mm3(a3: torch.Tensor, b3: torch.Tensor, add: Optional[torch.Tensor] = None,
+         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a @ b (+ add) to ~float32 accuracy as ONE bf16 GEMM over a tripled
+    contraction: a3 holds a's three-term pieces in order "hhl", b3 b's in
+    order "lhh" (models/fused.py split3), so a3 @ b3 = a_hi b_lo + a_hi b_hi +
+    a_lo b_hi with float32 accumulation (the dropped a_lo b_lo and the splits'
+    rounding are ~2^-16 relative; tools/addmm_out_probe.py).  gfx950 has no
+    xf32 and float32 matrix throughput is 1/16 of bf16's: three bf16 products
+    in one launch cost a fraction of one float32 GEMM."""
     if out is None:
-        return torch.addmm(c, ah, bh, out_dtype=torch.float32) if _MM32[0] else c + (ah @ bh).float()
+        return _mm32(a3, b3, add)
+    if _MM32[0] is None:
+        _mm32(a3[:2], b3)
     if _MM32[0]:
-        return torch.addmm(c, ah, bh, out_dtype=torch.float32, out=out)
-    return out.copy_(c + (ah @ bh).float())
+        if add is None:
+            return torch.mm(a3, b3, out_dtype=torch.float32, out=out)
+        return torch.addmm(add, a3, b3, out_dtype=torch.float32, out=out)
+    return out.copy_(_mm32(a3, b3, add))
 
 
 def _layer_args(l, norm, topo, a_all, off, stride, i, last):
@@ -154,7 +157,12 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         wts = [(layers[0].lin.weight.detach(), ip.weight.detach(), ip.bias.detach())] + \
               [l.lin.weight.detach() for l in layers[1:]]
         head_w = fused._head_weights_exact(net)
-        wsplit = fused.split_bf16([l.lin.weight for l in layers[1:]] + [head_w[0], head_w[1].t()])
+        wn_, wc_ = head_w[0], head_w[1].t()                    # [2H, d], [H, 2d] contiguous
+        lin_w = [l.lin.weight for l in layers[1:]]
+        ws = fused.split3([(w, "cols", "lhh") for w in lin_w] + [(w, "rows", "lhh") for w in lin_w] +
+                          [(wn_, "cols", "lhh"), (wn_, "rows", "lhh"), (wc_, "cols", "lhh"), (wc_, "rows", "lhh")])
+        nl = len(lin_w)
+        w_cols, w_rows, (wn_c, wn_r, wc_c, wc_r) = ws[:nl], ws[nl:2 * nl], ws[2 * nl:]
     else:
         wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
     lin0 = not save and not exact and fused.LAYER0_LINEAR and fused.layer0_supported(enc)
@@ -197,10 +205,9 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
             rec.update(w0=w0, wp=wp)
         else:
             if exact:
-                x_s = fused.split_bf16([prev_f32])[0]
-                w_s = wsplit[i - 1]
-                xh = _mm3(x_s, (w_s[0].t(), w_s[1].t()))          # x_in @ W^T, ~float32
-                rec.update(xh=xh, x_in=x_s, w=w_s)
+                x_c, x_r = fused.split3([(prev_f32, "cols", "hhl"), (prev_f32, "rows", "lhh")])
+                xh = _mm3(x_c, w_cols[i - 1].t())                  # x_in @ W^T, ~float32
+                rec.update(xh=xh, x_in=x_r, w=w_rows[i - 1])       # the backward's operands
             else:
                 xh = F.linear(prev_bf16, wts[i])
                 rec.update(xh=xh, x_in=prev_bf16, w=wts[i])
@@ -239,11 +246,11 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     if exact:
         emb = prev_f32
         wn, wc, we, w2, b2 = head_w
-        emb_s, ctx_s = fused.split_bf16([emb, ctx])
-        wn_s, wc_s = wsplit[-2], wsplit[-1]                     # wn [2H, d], wc [H, 2d] (contiguous)
-        p = _mm3(emb_s, (wn_s[0].t(), wn_s[1].t()))             # ~float32 [N, 2H]
-        c = _mm3(ctx_s, (wc_s[0].t(), wc_s[1].t()), b1)
-        head_w = (wn, wc, we, w2, b2, emb_s, ctx_s, wn_s, wc_s)
+        emb_c, emb_r, ctx_c, ctx_r = fused.split3([(emb, "cols", "hhl"), (emb, "rows", "lhh"),
+                                                   (ctx, "cols", "hhl"), (ctx, "rows", "lhh")])
+        p = _mm3(emb_c, wn_c.t())                               # ~float32 [N, 2H]
+        c = _mm3(ctx_c, wc_c.t(), b1)
+        head_w = (wn, wc, we, w2, b2, emb_r, ctx_r, wn_r, wc_r)
     else:
         emb = prev_bf16
         head_w = fused._head_weights(net) if save else fused.prepared_head(net)
@@ -325,12 +332,13 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     g_we = torch.empty(Hd, k, device=dev, dtype=torch.float32)
     _lib.check(L.trx_partial_sum(_lib.ptr(gwep), B, Hd * k, Hd * k, _lib.ptr(g_we), stream), "trx_partial_sum")
     if exact:
-        emb_s, ctx_s, wn_s, wc_s = cx.head_w[5:]
-        gp_s, gc_s = fused.split_bf16([g_p, g_c])
-        g_wn = _mm3((gp_s[0].t(), gp_s[1].t()), emb_s)                  # [2H, embed]
-        g_emb = _mm3(gp_s, wn_s)                                        # [N, embed]
-        g_wc = _mm3((gc_s[0].t(), gc_s[1].t()), ctx_s)                  # [H, 2*embed]
-        g_ctx = _mm3(gc_s, wc_s)                                        # [B, 2*embed]
+        emb_r, ctx_r, wn_r, wc_r = cx.head_w[5:]
+        gp_c, gp_r, gc_c, gc_r = fused.split3([(g_p, "cols", "hhl"), (g_p, "rows", "hhl"),
+                                               (g_c, "cols", "hhl"), (g_c, "rows", "hhl")])
+        g_wn = _mm3(gp_r.t(), emb_r)                                    # [2H, embed]
+        g_emb = _mm3(gp_c, wn_r)                                        # [N, embed]
+        g_wc = _mm3(gc_r.t(), ctx_r)                                    # [H, 2*embed]
+        g_ctx = _mm3(gc_c, wc_r)                                        # [B, 2*embed]
     else:
         g_wn = _splitk_wgrad(g_p, cx.emb)                               # [2H, embed] fp32
         g_emb = _mm32(g_p, wn)                                          # fp32 [N, embed]
@@ -404,8 +412,8 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             S = 4 if N % 4 == 0 else 1
             gw = sink.take(l.lin.weight.numel()).view_as(l.lin.weight)
             if exact:
-                gx_s = fused.split_bf16([g_xh])[0]
-                _mm3((gx_s[0].t(), gx_s[1].t()), x_in, out=gw)        # g_xh^T x_in
+                gx_c, gx_r = fused.split3([(g_xh, "cols", "hhl"), (g_xh, "rows", "hhl")])
+                _mm3(gx_r.t(), x_in, out=gw)                            # g_xh^T x_in
             else:
                 part_w = torch.bmm(g_xh.view(S, N // S, -1).transpose(1, 2), x_in.view(S, N // S, -1))
                 torch.sum(part_w, 0, dtype=torch.float32, out=gw)
@@ -413,7 +421,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             # the previous layer's output reaches this layer twice: bf16 through lin,
             # fp32 as the residual of a middle layer (gat_encoder.py:44-46)
             if exact:
-                gy_f32 = _mm3(gx_s, rec["w"], g_res if ba.residual == 1 else None)   # g_xh W (+ residual)
+                gy_f32 = _mm3(gx_c, rec["w"], g_res if ba.residual == 1 else None)   # g_xh W (+ residual)
             else:
                 gy_f32 = _mm32(g_xh, rec["w"], g_res if ba.residual == 1 else None)
             gy_b16 = None

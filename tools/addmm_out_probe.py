@@ -1,6 +1,6 @@
 """torch.mm / addmm(out_dtype=float32) from bf16 operands with transposed views,
-and the update's three-product split GEMM (rl/fused_update.py _mm3) against a
-float64 reference.  usage: python tools/addmm_out_probe.py"""
+and the update's three-term split GEMM (models/fused.py split3 +
+rl/fused_update.py _mm3) against a float64 reference.  usage: python tools/addmm_out_probe.py"""
 import os
 import sys
 
@@ -25,20 +25,16 @@ def main():
         r = torch.mm(ab, bb, out_dtype=torch.float32)
         want = ab.double() @ bb.double()
         print(f"mm out_dtype {name:10s} max err {float((r.double() - want).abs().max()):.3e}", flush=True)
-    for name, a, b in (("a b", A, Bm), ("a^T' b", At.t(), Bm), ("a b^T'", A, Bt.t()), ("a^T' b^T'", At.t(), Bt.t())):
-        src_a = At if a.stride(0) == 1 else A
-        src_b = Bt if b.stride(0) == 1 else Bm
-        sa, sb = fused.split_bf16([src_a, src_b])
-        if a.stride(0) == 1:
-            sa = (sa[0].t(), sa[1].t())
-        if b.stride(0) == 1:
-            sb = (sb[0].t(), sb[1].t())
-        r = FU._mm3(sa, sb)
-        rel = float((r.double() - ref).abs().max() / ref.abs().max())
-        print(f"_mm3 {name:10s} max rel err {rel:.3e}", flush=True)
-    hi, lo = fused.split_bf16([A])[0]
-    print("split: hi exact", bool(torch.equal(hi, A.bfloat16())), "residual rel",
-          float(((hi.double() + lo.double()) - A.double()).abs().max() / A.abs().max()), flush=True)
+    # the three-term operands: a [M, K] by columns ("hhl"), b [K, N] by rows ("lhh"); and the
+    # transposed forms the update uses (a = x^T from x's row stack, b = W^T from W's columns)
+    a3, b3 = fused.split3([(A, "cols", "hhl"), (Bm, "rows", "lhh")])
+    at3, bt3 = fused.split3([(At, "rows", "hhl"), (Bt, "cols", "lhh")])
+    for name, x, y in (("a3 b3", a3, b3), ("at3^T bt3^T", at3.t(), bt3.t()), ("a3 bt3^T", a3, bt3.t())):
+        r = FU._mm3(x, y)
+        print(f"_mm3 {name:12s} max rel err {float((r.double() - ref).abs().max() / ref.abs().max()):.3e}", flush=True)
+    o = torch.empty(M, N, device="cuda")
+    FU._mm3(a3, b3, out=o)
+    print(f"_mm3 out=      max rel err {float((o.double() - ref).abs().max() / ref.abs().max()):.3e}", flush=True)
 
 
 if __name__ == "__main__":

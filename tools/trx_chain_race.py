@@ -36,7 +36,8 @@ def main():
                 y = torch.empty_like(xs[k])
                 fused._round_into([(xs[k], y, True)])          # trx kernel: copy
                 z = y * 0.5 + 1.0                               # torch kernel
-                hi, lo = fused.split_bf16([z])[0]               # trx kernel
+                z3 = fused.split3([(z, "cols", "hhl")])[0]     # trx kernel
+                hi, lo = z3[:, :K], z3[:, 2 * K:]
                 g = F.linear(hi, ws[k])                         # hipBLASLt
                 u = torch.empty(N, K, device=dev)
                 fused._round_into([(g.float(), u, True)])       # torch cast, trx copy
