@@ -120,6 +120,22 @@ def _mm3(a3: torch.Tensor, b3: torch.Tensor, add: Optional[torch.Tensor] = None,
     return out.copy_(_mm32(a3, b3, add))
 
 
+def _wgrad3(g_rows: torch.Tensor, x_rows: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out = g^T x to ~float32 accuracy from the row-stacked three-term pieces
+    (g_rows [3K, M] in order "hhl", x_rows [3K, N] in order "lhh"; K = the
+    batch's node / graph rows): split-K over the tripled contraction -- S
+    float32 partial products in one batched bf16 GEMM, summed in order -- so
+    the small [M, N] output still fills the chip (one plain GEMM of K = 18432
+    ran at ~10 % of the bf16 peak)."""
+    K3, M = g_rows.shape
+    N = x_rows.shape[1]
+    S = next((s for s in (12, 8, 6, 4, 3, 2) if K3 % s == 0 and K3 // s >= 512), 1)
+    if S == 1 or not _MM32[0]:
+        return _mm3(g_rows.t(), x_rows, out=out)
+    part = torch.bmm(g_rows.view(S, K3 // S, M).transpose(1, 2), x_rows.view(S, K3 // S, N), out_dtype=torch.float32)
+    return torch.sum(part, 0, out=out)
+
+
 def _layer_args(l, norm, topo, a_all, off, stride, i, last):
     args = _lib.TrxGatLayerArgs()
     args.num_graphs, args.nodes_per_graph, args.heads, args.channels = topo.B, topo.n, l.heads, l.out_channels
@@ -165,7 +181,9 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
         w_cols, w_rows, (wn_c, wn_r, wc_c, wc_r) = ws[:nl], ws[nl:2 * nl], ws[2 * nl:]
     else:
         wts = fused._encoder_weights(enc, layers) if save else fused.prepared_encoder(enc, layers)
-    lin0 = not save and not exact and fused.LAYER0_LINEAR and fused.layer0_supported(enc)
+    # the linear-form layer 0 pays for its per-update weight preparation
+    # (trx_gat_layer0_prepare, ~40 us on H + 1 workgroups) only at acting sizes
+    lin0 = (not save and not exact and topo.B >= 1024 and fused.LAYER0_LINEAR and fused.layer0_supported(enc))
     mid = lin0 and fused.MID_REGEN and fused.mid_supported(enc)
     keep = []
     recs = []
@@ -335,7 +353,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         emb_r, ctx_r, wn_r, wc_r = cx.head_w[5:]
         gp_c, gp_r, gc_c, gc_r = fused.split3([(g_p, "cols", "hhl"), (g_p, "rows", "hhl"),
                                                (g_c, "cols", "hhl"), (g_c, "rows", "hhl")])
-        g_wn = _mm3(gp_r.t(), emb_r)                                    # [2H, embed]
+        g_wn = _wgrad3(gp_r, emb_r, torch.empty(gp_r.shape[1], emb_r.shape[1], device=dev))   # [2H, embed]
         g_emb = _mm3(gp_c, wn_r)                                        # [N, embed]
         g_wc = _mm3(gc_r.t(), ctx_r)                                    # [H, 2*embed]
         g_ctx = _mm3(gc_c, wc_r)                                        # [B, 2*embed]
@@ -413,7 +431,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             gw = sink.take(l.lin.weight.numel()).view_as(l.lin.weight)
             if exact:
                 gx_c, gx_r = fused.split3([(g_xh, "cols", "hhl"), (g_xh, "rows", "hhl")])
-                _mm3(gx_r.t(), x_in, out=gw)                            # g_xh^T x_in
+                _wgrad3(gx_r, x_in, gw)                                 # g_xh^T x_in
             else:
                 part_w = torch.bmm(g_xh.view(S, N // S, -1).transpose(1, 2), x_in.view(S, N // S, -1))
                 torch.sum(part_w, 0, dtype=torch.float32, out=gw)
