@@ -87,6 +87,8 @@ for s in "$@"; do
                  step upd_race_fwd 300 python tools/update_graph_race.py 30 fwdserial &&
                  step upd_race_nopatch 300 python tools/update_graph_race.py 30 nopatch ;;
         graphrace) step graph_race 200 python tools/graph_branch_race.py ;;
+        layerrace5) TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race6_fences 300 python tools/layer_concurrency_race.py 6 20 train &&
+                    TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race3_fences 300 python tools/layer_concurrency_race.py 3 20 train ;;
         layerrace4) GPU_MAX_HW_QUEUES=8 step layer_race6_q8 300 python tools/layer_concurrency_race.py 6 20 train &&
                     GPU_MAX_HW_QUEUES=16 step layer_race6_q16 300 python tools/layer_concurrency_race.py 6 20 train &&
                     GPU_MAX_HW_QUEUES=2 step layer_race6_q2 300 python tools/layer_concurrency_race.py 6 20 train ;;
