@@ -628,7 +628,11 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
         eal[v] = j < D ? a.ea[((int64_t)g * E + e) * D + j] : 0.0f;
     }
     constexpr int DC = DK > 0 ? DK : ED;
-    float we_r[MQ][4][DC], w2_r[MQ][4], c_r[MQ][4];
+    // a lane's four hidden units as two pairs: the per-unit arithmetic below runs on
+    // packed float32 pairs (v_pk_mul_f32 / v_pk_add_f32), the same IEEE operations
+    // in the same order per unit as scalar code (bit-identical), half the VALU issue
+    trx_f2 we2[MQ][2][DC], c2[MQ][2];
+    float w2_r[MQ][4];
 #pragma unroll
     for (int m = 0; m < MQ; ++m)
 #pragma unroll
@@ -636,9 +640,9 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
             const int k = 256 * m + 4 * lane + r;
             const bool ok = k < Hd;
             w2_r[m][r] = ok ? a.w2[k] : 0.0f;
-            c_r[m][r] = ok ? a.c[(int64_t)g * Hd + k] : 0.0f;
+            c2[m][r >> 1][r & 1] = ok ? a.c[(int64_t)g * Hd + k] : 0.0f;
 #pragma unroll
-            for (int j = 0; j < DC; ++j) we_r[m][r][j] = (ok && (DK > 0 || j < D)) ? a.we[k * D + j] : 0.0f;
+            for (int j = 0; j < DC; ++j) we2[m][r >> 1][j][r & 1] = (ok && (DK > 0 || j < D)) ? a.we[k * D + j] : 0.0f;
         }
     const float b2 = a.b2[0];
     if (badf) *badl = 1;
@@ -672,18 +676,19 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
                 const int k0 = 256 * m + 4 * lane;
                 if (k0 < Hd) {
                     const float4 s4 = xld4<XF>(ps + k0), d4 = xld4<XF>(pd + k0);
-                    const float psv[4] = {s4.x, s4.y, s4.z, s4.w};
-                    const float pdv[4] = {d4.x, d4.y, d4.z, d4.w};
+                    const trx_f2 psv[2] = {{s4.x, s4.y}, {s4.z, s4.w}};
+                    const trx_f2 pdv[2] = {{d4.x, d4.y}, {d4.z, d4.w}};
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float ew = 0.0f;
+                    for (int rp = 0; rp < 2; ++rp) {
+                        trx_f2 ew = {0.0f, 0.0f};
 #pragma unroll
                         for (int j = 0; j < DC; ++j)
-                            if (DK > 0 || j < D) ew += ear[j] * we_r[m][r][j];
-                        // fp32 from the bf16 GEMM outputs on: the link's hidden unit and
-                        // its share of the 256 -> 1 product
-                        const float z = ((psv[r] + pdv[r]) + ew) + c_r[m][r];
-                        part[u] += fmaxf(z, 0.0f) * w2_r[m][r];
+                            if (DK > 0 || j < D) ew += (trx_f2){ear[j], ear[j]} * we2[m][rp][j];
+                        // fp32 from the bf16 GEMM outputs on: the link's hidden units and
+                        // their shares of the 256 -> 1 product (units in order)
+                        const trx_f2 z = ((psv[rp] + pdv[rp]) + ew) + c2[m][rp];
+                        part[u] += fmaxf(z.x, 0.0f) * w2_r[m][2 * rp];
+                        part[u] += fmaxf(z.y, 0.0f) * w2_r[m][2 * rp + 1];
                     }
                 }
             }

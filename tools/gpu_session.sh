@@ -87,6 +87,10 @@ for s in "$@"; do
                  step upd_race_fwd 300 python tools/update_graph_race.py 30 fwdserial &&
                  step upd_race_nopatch 300 python tools/update_graph_race.py 30 nopatch ;;
         graphrace) step graph_race 200 python tools/graph_branch_race.py ;;
+        ehab) step eh_cs_a 200 env TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so python tools/act_checksum.py 4096 &&
+              step eh_cs_b 200 python tools/act_checksum.py 4096 &&
+              TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act &&
+              step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         layerrace5) TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race6_fences 300 python tools/layer_concurrency_race.py 6 20 train &&
                     TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race3_fences 300 python tools/layer_concurrency_race.py 3 20 train ;;
         layerrace4) GPU_MAX_HW_QUEUES=8 step layer_race6_q8 300 python tools/layer_concurrency_race.py 6 20 train &&
