@@ -512,6 +512,20 @@ int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream);
 int64_t trx_gat_layer_backward_part_floats(int32_t heads, int32_t channels, int32_t in_dim);
 /* out[k] = sum over r < rows (ascending) of part[r * stride + k], k < width. */
 int trx_partial_sum(const float* part, int32_t rows, int32_t width, int64_t stride, float* out, void* stream);
+/* ABI 10: up to TRX_MAX_PSUM such column sums (same rows) in one launch, same
+ * order per column; out index k -> out + (k / out_cols) * out_ld + k % out_cols
+ * when out_cols > 0 (a column block of a larger matrix), else out + k. */
+#define TRX_MAX_PSUM 32
+typedef struct trx_psum_list {
+    int32_t count, rows;
+    int32_t width[TRX_MAX_PSUM];
+    int32_t out_cols[TRX_MAX_PSUM];
+    int64_t stride[TRX_MAX_PSUM];
+    int64_t out_ld[TRX_MAX_PSUM];
+    const float* part[TRX_MAX_PSUM];
+    float* out[TRX_MAX_PSUM];
+} trx_psum_list;
+int trx_partial_sum_multi(const trx_psum_list* l, void* stream);
 
 /* trx_gat_prologue_backward: backward of trx_gat_prologue_infer (input
  * LayerNorms, PyG mean self-loop attrs, every layer's a_edge) from g_a_edge

@@ -1032,6 +1032,19 @@ int trx_partial_sum(const float* part, int32_t rows, int32_t width, int64_t stri
     return TRX_OK;
 }
 
+int trx_partial_sum_multi(const trx_psum_list* l, void* stream) {
+    if (!l || l->count < 0 || l->count > TRX_MAX_PSUM || l->rows < 0)
+        return fail(TRX_EINVAL, "partial_sum_multi: count 0..%d, rows >= 0", TRX_MAX_PSUM);
+    for (int e = 0; e < l->count; ++e)
+        if (!l->part[e] || !l->out[e] || l->width[e] < 0 || l->stride[e] < l->width[e] || l->out_cols[e] < 0 ||
+            (l->out_cols[e] > 0 && l->out_ld[e] < l->out_cols[e]))
+            return fail(TRX_EINVAL, "partial_sum_multi: bad entry %d", e);
+    if (l->count == 0 || l->rows == 0) return TRX_OK;
+    hipError_t e = trx::launch_partial_sum_multi(*l, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "partial_sum_multi launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_edge_att_weights_backward(const trx_gat_prologue_args* a, const float* g_m, int32_t g_m_stride, float* out,
                                   void* stream) {
     if (!a || !g_m || !out) return fail(TRX_EINVAL, "edge_att_weights_backward: NULL argument");

@@ -577,8 +577,9 @@ hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t str
 // 16 waves per 64 columns, wave w sums rows w, w+16, ... (loads four rows
 // ahead), then wave 0 adds the 16 wave sums in wave order.
 constexpr int kPsWaves = 16;
-__global__ void __launch_bounds__(kW * kPsWaves) partial_sum_kernel(const float* __restrict__ part, int rows, int width,
-                                                                    int64_t stride, float* __restrict__ out) {
+// out index k -> out + (k / out_cols) * out_ld + k % out_cols (out_cols 0: out + k)
+__device__ __forceinline__ void partial_sum_block(const float* __restrict__ part, int rows, int width, int64_t stride,
+                                                  float* __restrict__ out, int out_cols, int64_t out_ld) {
     __shared__ float red[kPsWaves][kW];
     const int lane = threadIdx.x & (kW - 1), w = threadIdx.x / kW;
     const int k = blockIdx.x * kW + lane;
@@ -603,14 +604,34 @@ __global__ void __launch_bounds__(kW * kPsWaves) partial_sum_kernel(const float*
         float t = red[0][lane];
 #pragma unroll
         for (int j = 1; j < kPsWaves; ++j) t += red[j][lane];
-        out[k] = t;
+        out[out_cols > 0 ? (int64_t)(k / out_cols) * out_ld + k % out_cols : (int64_t)k] = t;
     }
+}
+
+__global__ void __launch_bounds__(kW * kPsWaves) partial_sum_kernel(const float* __restrict__ part, int rows, int width,
+                                                                    int64_t stride, float* __restrict__ out) {
+    partial_sum_block(part, rows, width, stride, out, 0, 0);
+}
+
+// several column-sum problems in one launch (blockIdx.y = problem): the fused update's
+// per-network parameter partials, same summation order as partial_sum_kernel
+__global__ void __launch_bounds__(kW * kPsWaves) partial_sum_multi_kernel(trx_psum_list l) {
+    const int e = blockIdx.y;
+    if (e >= l.count || (int)blockIdx.x * kW >= l.width[e]) return;  // block-uniform
+    partial_sum_block(l.part[e], l.rows, l.width[e], l.stride[e], l.out[e], l.out_cols[e], l.out_ld[e]);
 }
 
 hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t stride, float* out,
                               hipStream_t stream) {
     hipLaunchKernelGGL(partial_sum_kernel, dim3((width + kW - 1) / kW), dim3(kW * kPsWaves), 0, stream, part, rows,
                        width, stride, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_partial_sum_multi(const trx_psum_list& l, hipStream_t stream) {
+    int mx = 1;
+    for (int e = 0; e < l.count; ++e) mx = l.width[e] > mx ? l.width[e] : mx;
+    hipLaunchKernelGGL(partial_sum_multi_kernel, dim3((mx + kW - 1) / kW, l.count), dim3(kW * kPsWaves), 0, stream, l);
     return hipGetLastError();
 }
 

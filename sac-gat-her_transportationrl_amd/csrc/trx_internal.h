@@ -230,6 +230,7 @@ hipError_t patch_graph_memsets(hipGraph_t graph, int* n_patched);
 size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a);
 hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t stream);
 hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t stride, float* out, hipStream_t stream);
+hipError_t launch_partial_sum_multi(const trx_psum_list& l, hipStream_t stream);
 hipError_t launch_edge_att_weights_bwd(const trx_gat_prologue_args& a, const float* gm, int gm_stride, float* out,
                                        hipStream_t stream);
 size_t gat_prologue_bwd_smem(const trx_gat_prologue_bwd_args& a);

@@ -31,7 +31,8 @@ EXPORTS = (
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
     "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
-    "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_gat_prologue_backward",
+    "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_partial_sum_multi",
+    "trx_gat_prologue_backward",
     "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
     "trx_gat_layer0_infer", "trx_gat_layer0_prepare", "trx_gat_mid_infer",
 )
@@ -224,6 +225,18 @@ class TrxRoundList(ctypes.Structure):
     ]
 
 
+MAX_PSUM = 32
+
+
+class TrxPsumList(ctypes.Structure):
+    """trx_psum_list (include/trafficrl.h)."""
+    _fields_ = [
+        ("count", _i32), ("rows", _i32), ("width", _i32 * MAX_PSUM), ("out_cols", _i32 * MAX_PSUM),
+        ("stride", ctypes.c_int64 * MAX_PSUM), ("out_ld", ctypes.c_int64 * MAX_PSUM),
+        ("part", _vp * MAX_PSUM), ("out", _vp * MAX_PSUM),
+    ]
+
+
 MAX_COPY = 16
 
 
@@ -282,6 +295,7 @@ def load():
     L.trx_gat_layer_backward_part_floats.argtypes = [_i32, _i32, _i32]
     L.trx_gat_layer_backward_part_floats.restype = ctypes.c_int64
     L.trx_partial_sum.argtypes = [_vp, _i32, _i32, ctypes.c_int64, _vp, _vp]
+    L.trx_partial_sum_multi.argtypes = [ctypes.POINTER(TrxPsumList), _vp]
     L.trx_gat_prologue_backward.argtypes = [ctypes.POINTER(TrxGatPrologueBwdArgs), _vp]
     L.trx_sac_loss.argtypes = [ctypes.POINTER(TrxSacLossArgs), _vp]
     L.trx_sac_adam.argtypes = [ctypes.POINTER(TrxAdamArgs), _vp]
@@ -355,7 +369,7 @@ def load():
                  "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
                  "trx_episode_step", "trx_gat_layer_backward", "trx_partial_sum", "trx_gat_prologue_backward",
                  "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
-                 "trx_gat_layer0_infer", "trx_gat_layer0_prepare", "trx_gat_mid_infer"):
+                 "trx_gat_layer0_infer", "trx_gat_layer0_prepare", "trx_gat_mid_infer", "trx_partial_sum_multi"):
         getattr(L, name).restype = ctypes.c_int
     if L.trx_abi_version() != ABI_VERSION:
         raise ImportError(f"libtrafficrl ABI {L.trx_abi_version()} != {ABI_VERSION}")

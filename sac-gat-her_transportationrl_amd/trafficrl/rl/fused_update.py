@@ -20,6 +20,7 @@ it against the autograd path and the fp32 restatement.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -322,10 +323,48 @@ def _grad(param, g):
     param.grad = g.view_as(param) if g.shape != param.shape else g
 
 
-def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: GradFlat, exact: bool = False):
+class PartialSums:
+    """The per-graph parameter partials of one update's backwards, column-summed
+    by ONE trx_partial_sum_multi launch at the end (each sum in the fixed order of
+    trx_partial_sum; 21 launches -> 1), and the work that needs the sums."""
+
+    def __init__(self, rows: int):
+        self.rows, self.entries, self.after, self.used = rows, [], [], []
+
+    def add(self, part: torch.Tensor, width: int, stride: int, out: torch.Tensor, out_cols: int = 0,
+            out_ld: int = 0):
+        self.entries.append((part, width, stride, out, out_cols, out_ld))
+
+    def flush(self, stream):
+        """Run on the stream that joined the backwards: every buffer a side stream
+        allocated is recorded as used here before its last reference drops."""
+        L = _lib.load()
+        cur = torch.cuda.current_stream()
+        for t in [x for e in self.entries for x in (e[0], e[3])] + self.used:
+            t.record_stream(cur)
+        for b0 in range(0, len(self.entries), _lib.MAX_PSUM):
+            lst = _lib.TrxPsumList()
+            chunk = self.entries[b0:b0 + _lib.MAX_PSUM]
+            lst.count, lst.rows = len(chunk), self.rows
+            for e, (part, width, stride, out, oc, ld) in enumerate(chunk):
+                lst.part[e], lst.width[e], lst.stride[e] = part.data_ptr(), width, stride
+                lst.out[e], lst.out_cols[e], lst.out_ld[e] = out.data_ptr(), oc, ld
+            _lib.check(L.trx_partial_sum_multi(ctypes.byref(lst), stream), "trx_partial_sum_multi")
+        for fn in self.after:
+            fn()
+        self.entries, self.after, self.used = [], [], []
+
+
+def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: GradFlat, exact: bool = False,
+                 sums: Optional[PartialSums] = None):
     """Gradients of every parameter of `net` from dL/dlogits [B*e] fp32,
     written into `sink` and handed to the parameters as views (exact: the
-    backward of net_forward(..., exact=True), float32 throughout)."""
+    backward of net_forward(..., exact=True), float32 throughout).  With
+    `sums` the column sums of the per-graph partials are left to sums.flush()
+    (after every network's backward); without, they run here."""
+    own = sums is None
+    if own:
+        sums = PartialSums(topo.B)
     L = _lib.load()
     dev = g_logits.device
     stream = _lib.stream_ptr(dev)
@@ -348,7 +387,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     _lib.check(L.trx_edge_head_backward(a, _lib.ptr(gl), _lib.ptr(g_p), _lib.ptr(g_c), None, _lib.ptr(gw2p),
                                         _lib.ptr(gwep), _lib.ptr(g_ea_head), stream), "trx_edge_head_backward")
     g_we = torch.empty(Hd, k, device=dev, dtype=torch.float32)
-    _lib.check(L.trx_partial_sum(_lib.ptr(gwep), B, Hd * k, Hd * k, _lib.ptr(g_we), stream), "trx_partial_sum")
+    sums.add(gwep, Hd * k, Hd * k, g_we)
     if exact:
         emb_r, ctx_r, wn_r, wc_r = cx.head_w[5:]
         gp_c, gp_r, gc_c, gc_r = fused.split3([(g_p, "cols", "hhl"), (g_p, "rows", "hhl"),
@@ -366,11 +405,12 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         g_ctx = _mm32(g_cb, wc.t())                                     # [B, 2*embed]
     W1 = net.edge_mlp[0].weight
     gW1 = sink.take(W1.numel()).view_as(W1)
-    torch.cat([g_wn[:Hd], g_wn[Hd:], g_we, g_wc], 1, out=gW1)
+    sums.after.append(lambda: torch.cat([g_wn[:Hd], g_wn[Hd:], g_we, g_wc], 1, out=gW1))
+    sums.used += [g_wn, g_wc, gW1]
     _grad(W1, gW1)
     for prm, src in ((net.edge_mlp[0].bias, g_c), (net.edge_mlp[2].weight, gw2p)):
         dst = sink.take(prm.numel())      # column sums over the graphs, fixed order
-        _lib.check(L.trx_partial_sum(_lib.ptr(src), B, Hd, Hd, _lib.ptr(dst), stream), "trx_partial_sum")
+        sums.add(src, Hd, Hd, dst)
         _grad(prm, dst)
     gb2 = sink.take(1)
     torch.sum(gl, 0, keepdim=True, out=gb2)
@@ -414,7 +454,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         ba.g_xh, ba.g_res, ba.g_a_edge, ba.part = g_xh.data_ptr(), g_res.data_ptr(), g_a_all.data_ptr(), part.data_ptr()
         _lib.check(L.trx_gat_layer_backward(ba, stream), "trx_gat_layer_backward")
         pg = sink.take(PW)
-        _lib.check(L.trx_partial_sum(_lib.ptr(part), B, PW, PW, _lib.ptr(pg), stream), "trx_partial_sum")
+        sums.add(part, PW, PW, pg)
         _grad(l.bias, pg[:HC])
         _grad(norm.weight, pg[HC:2 * HC])
         _grad(norm.bias, pg[2 * HC:3 * HC])
@@ -465,7 +505,7 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
     pa.exact = int(exact)
     _lib.check(L.trx_gat_prologue_backward(pa, stream), "trx_gat_prologue_backward")
     pp = sink.take(PP)
-    _lib.check(L.trx_partial_sum(_lib.ptr(ppart), B, PP, PP, _lib.ptr(pp), stream), "trx_partial_sum")
+    sums.add(ppart, PP, PP, pp)
     ed, nd = cx.edge_x.shape[1], cx.node_x.shape[1]
     _grad(net.edge_norm.weight, pp[8 * A:8 * A + ed])
     _grad(net.edge_norm.bias, pp[8 * A + 8:8 * A + 8 + ed])
@@ -483,15 +523,20 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         ea_args.lin_edge_w[i], ea_args.att_edge[i] = w.data_ptr(), at.data_ptr()
     tot = sum(l.heads * l.out_channels * (ed + 1) for l in layers)
     gout = sink.take(tot)
-    _lib.check(L.trx_edge_att_weights_backward(ea_args, _lib.ptr(pp), 8, _lib.ptr(gout), stream),
-               "trx_edge_att_weights_backward")
-    del keep
+
+    def att_weights():   # needs the summed prologue partials (pp)
+        _lib.check(L.trx_edge_att_weights_backward(ea_args, _lib.ptr(pp), 8, _lib.ptr(gout),
+                                                   _lib.stream_ptr(dev)), "trx_edge_att_weights_backward")
+    sums.after.append(att_weights)
+    sums.used += [gout] + keep
     off = 0
     for l in layers:
         HC = l.heads * l.out_channels
         _grad(l.lin_edge.weight, gout[off:off + HC * ed].view(HC, ed))
         _grad(l.att_edge, gout[off + HC * ed:off + HC * (ed + 1)])
         off += HC * (ed + 1)
+    if own:
+        sums.flush(stream)
 
 
 def compute_gradients_fused(agent, batch, weights, topo: Topology):
@@ -567,9 +612,12 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     agent.alpha_opt.zero_grad(set_to_none=True)
     # each network's backward on the stream its training forward ran on: the
     # saved tensors are read on the stream that allocated them
-    agent._concurrent([lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc),
-                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc),
-                       lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa)], streams=(3, 4, 5))
+    sums = PartialSums(B)
+    agent._concurrent([lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc, sums=sums),
+                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc, sums=sums),
+                       lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums)],
+                      streams=(3, 4, 5))
+    sums.flush(_lib.stream_ptr(dev))   # every network's column sums in one launch, on the joined stream
     agent.log_alpha.grad = g_la.view_as(agent.log_alpha)
     agent.grad_flat = flat        # every gradient of this update is a view of it (GradAllReduce)
     agent._warm = True
