@@ -164,13 +164,16 @@ def test_batch_damage_sampler_matches_numpy_generator(net):
 
 
 def test_fused_args_layout_matches_header(tmp_path):
-    """Every field offset of trx_gat_layer_args / trx_edge_head_args as the C
+    """Every field offset of the fused kernels' argument structs (incl. ABI
+    10's exact fields, the round list's dst_stride and trx_psum_list) as the C
     compiler lays them out equals the ctypes mirror in trafficrl/_lib.py."""
     from trafficrl import _lib
     lines = []
     structs = (("trx_gat_layer_args", _lib.TrxGatLayerArgs), ("trx_edge_head_args", _lib.TrxEdgeHeadArgs),
                ("trx_gat_prologue_args", _lib.TrxGatPrologueArgs), ("trx_gat_layer0_args", _lib.TrxGatLayer0Args),
-               ("trx_gat_mid_args", _lib.TrxGatMidArgs))
+               ("trx_gat_mid_args", _lib.TrxGatMidArgs), ("trx_gat_layer_bwd_args", _lib.TrxGatLayerBwdArgs),
+               ("trx_gat_prologue_bwd_args", _lib.TrxGatPrologueBwdArgs), ("trx_round_list", _lib.TrxRoundList),
+               ("trx_psum_list", _lib.TrxPsumList))
     for cname, cls in structs:
         lines.append(f'printf("%zu\\n", sizeof({cname}));')
         for f, _ in cls._fields_:
@@ -186,6 +189,31 @@ def test_fused_args_layout_matches_header(tmp_path):
         want.append(ctypes.sizeof(cls))
         want += [getattr(cls, f).offset for f, _ in cls._fields_]
     assert vals == want
+
+
+def test_round_and_psum_lists_validated_without_gpu():
+    """trx_bf16_round (modes 0-3, dst_stride) and trx_partial_sum_multi refuse
+    malformed lists before any HIP call; empty lists are no-ops."""
+    from trafficrl import _lib
+    L = _lib.load()
+    lst = _lib.TrxRoundList()
+    lst.count = 1
+    lst.rows[0], lst.cols[0], lst.src_stride[0] = 2, 8, 8
+    lst.src[0], lst.dst[0] = 16, 16          # never dereferenced: refused first
+    lst.out_bf16[0] = 4
+    assert L.trx_bf16_round(ctypes.byref(lst), None) == -1
+    lst.out_bf16[0], lst.dst_stride[0] = 3, 4  # dst rows narrower than the block
+    assert L.trx_bf16_round(ctypes.byref(lst), None) == -1
+    lst.count = 0
+    assert L.trx_bf16_round(ctypes.byref(lst), None) == 0
+    ps = _lib.TrxPsumList()
+    ps.count = _lib.MAX_PSUM + 1
+    assert L.trx_partial_sum_multi(ctypes.byref(ps), None) == -1
+    ps.count, ps.rows = 1, 4
+    ps.part[0], ps.out[0], ps.width[0], ps.stride[0] = 16, 16, 8, 4   # stride < width
+    assert L.trx_partial_sum_multi(ctypes.byref(ps), None) == -1
+    ps.count = 0
+    assert L.trx_partial_sum_multi(ctypes.byref(ps), None) == 0
 
 
 def test_fused_infer_validation_without_gpu():

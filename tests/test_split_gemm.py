@@ -1,0 +1,72 @@
+"""The float32 actor's building blocks (rl/fused_update.py, models/fused.py):
+three-term bf16 splits (trx_bf16_round modes 1 / 3 with a destination row
+stride), the tripled-contraction GEMM and its split-K weight-gradient form,
+against float64; and trx_partial_sum_multi against trx_partial_sum (same
+summation order: bit-identical) with a column-block destination."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_split3_pieces_exact():
+    from trafficrl.models import fused
+    torch.manual_seed(0)
+    x = torch.randn(96, 64, device="cuda") * 3.0
+    c, r = fused.split3([(x, "cols", "hhl"), (x, "rows", "lhh")])
+    hi = x.bfloat16()
+    lo = (x - hi.float()).bfloat16()
+    assert torch.equal(c[:, :64], hi) and torch.equal(c[:, 64:128], hi) and torch.equal(c[:, 128:], lo)
+    assert torch.equal(r[:96], lo) and torch.equal(r[96:192], hi) and torch.equal(r[192:], hi)
+    # hi + lo carries 16 mantissa bits
+    rel = float(((hi.double() + lo.double()) - x.double()).abs().max() / x.abs().max())
+    assert rel < 2 ** -15
+
+
+def test_tripled_contraction_gemm_and_split_k():
+    from trafficrl.models import fused
+    from trafficrl.rl import fused_update as FU
+    torch.manual_seed(1)
+    x = torch.randn(6144, 256, device="cuda")
+    w = torch.randn(512, 256, device="cuda") * 0.05
+    x_c, x_r = fused.split3([(x, "cols", "hhl"), (x, "rows", "lhh")])
+    w_c, = fused.split3([(w, "cols", "lhh")])
+    y = FU._mm3(x_c, w_c.t())                       # x @ w^T
+    ref = x.double() @ w.double().t()
+    assert float((y.double() - ref).abs().max() / ref.abs().max()) < 2e-5
+    g = torch.randn(6144, 512, device="cuda")
+    g_r, = fused.split3([(g, "rows", "hhl")])
+    out = torch.empty(512, 256, device="cuda")
+    FU._wgrad3(g_r, x_r, out)                        # g^T x, split-K
+    ref = g.double().t() @ x.double()
+    assert float((out.double() - ref).abs().max() / ref.abs().max()) < 2e-5
+
+
+def test_partial_sum_multi_matches_single():
+    from trafficrl import _lib
+    from trafficrl.rl.fused_update import PartialSums
+    L = _lib.load()
+    torch.manual_seed(2)
+    B = 256
+    parts = [torch.randn(B, w, device="cuda") for w in (1, 77, 256, 1030)]
+    want = []
+    for p in parts:
+        o = torch.empty(p.shape[1], device="cuda")
+        _lib.check(L.trx_partial_sum(_lib.ptr(p), B, p.shape[1], p.shape[1], _lib.ptr(o), _lib.stream_ptr()),
+                   "trx_partial_sum")
+        want.append(o)
+    sums = PartialSums(B)
+    got = [torch.empty(p.shape[1], device="cuda") for p in parts]
+    for p, o in zip(parts, got):
+        sums.add(p, p.shape[1], p.shape[1], o)
+    # a column block of a [16, 40] matrix: 16 x 6 sums into columns 20..25
+    blk = torch.randn(B, 96, device="cuda")
+    mat = torch.zeros(16, 40, device="cuda")
+    sums.add(blk, 96, 96, mat[:, 20:], out_cols=6, out_ld=40)
+    sums.flush(_lib.stream_ptr())
+    torch.cuda.synchronize()
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
+    ref = blk.sum(0).view(16, 6)
+    torch.testing.assert_close(mat[:, 20:26], ref, rtol=1e-5, atol=1e-4)
+    assert float(mat[:, :20].abs().sum()) == 0 and float(mat[:, 26:].abs().sum()) == 0

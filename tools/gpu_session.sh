@@ -122,7 +122,7 @@ for s in "$@"; do
         abact) TRX_LIB=${TRX_LIB_A:-} step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act
                TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         abk) step ab_quad 200 env TRX_KERNEL=quad python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
-        fused) step fused_tests 600 python -u -m pytest tests/test_flat_adam.py tests/test_fused_update.py tests/test_sac_e2e.py tests/test_sac.py -m gpu -v -s --timeout 300 --timeout-method thread ;;
+        fused) step fused_tests 600 python -u -m pytest tests/test_split_gemm.py tests/test_flat_adam.py tests/test_fused_update.py tests/test_sac_e2e.py tests/test_sac.py -m gpu -v -s --timeout 300 --timeout-method thread ;;
         bigstats) step big_stats 300 python tools/big_stats.py 1024 fw ;;
         actab) for f in sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_l03.so; do [ -f $f ] || continue; n=$(basename $f .so); TRX_LIB=$PWD/$f step actab_$n 200 python tools/act_host_probe.py 4096 || exit 1; done
                grep -h "eager" gpurun_out/actab_*.log ;;
