@@ -942,7 +942,10 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
     }
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     const dim3 grid(a.num_graphs);
-    const bool wide = a.num_graphs < 2048;
+#ifndef TRX_WIDE_GRAPHS
+#define TRX_WIDE_GRAPHS 2048
+#endif
+    const bool wide = a.num_graphs < TRX_WIDE_GRAPHS;
 #define TRX_LAYER_CASE(HCV, INV, XFV)                                                                          \
     if (HC == HCV && a.in_dim == INV && (a.exact != 0) == XFV) {                                               \
         if (wide)                                                                                              \
