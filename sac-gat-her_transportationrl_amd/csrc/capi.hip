@@ -774,6 +774,8 @@ int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
     if (a->nodes_per_graph < 1 || (int64_t)a->nodes_per_graph * a->hidden > 32768)
         return fail(TRX_EUNSUP, "edge_head_infer: nodes_per_graph must be 1..32768/hidden");
     if (a->hidden % 4) return fail(TRX_EUNSUP, "edge_head_infer: hidden must be a multiple of 4");
+    if (((uintptr_t)a->c | (uintptr_t)a->w2 | (uintptr_t)a->we) & 15)
+        return fail(TRX_EINVAL, "edge_head_infer: c, w2 and we must be 16-byte aligned (16-byte loads)");
     if (trx::edge_head_infer_smem(*a) > 160 * 1024)
         return fail(TRX_EUNSUP, "edge_head_infer: graph too large for LDS (nodes_per_graph, edges_per_graph)");
     if (!a->src || !a->dst || !a->p || !a->c || !a->ea || !a->we || !a->w2 || !a->b2 || !a->out || (a->softmax && !a->mask))

@@ -634,16 +634,41 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
     trx_f2 we2[MQ][2][DC], c2[MQ][2];
     float w2_r[MQ][4];
 #pragma unroll
-    for (int m = 0; m < MQ; ++m)
+    for (int m = 0; m < MQ; ++m) {
+        const int k0 = 256 * m + 4 * lane;
+        if (k0 < Hd) {  // hidden % 4 == 0: the lane's four units are all valid; 16-byte loads
+            const float4 w2v = *reinterpret_cast<const float4*>(a.w2 + k0);
+            const float4 cv = *reinterpret_cast<const float4*>(a.c + (int64_t)g * Hd + k0);
+            w2_r[m][0] = w2v.x, w2_r[m][1] = w2v.y, w2_r[m][2] = w2v.z, w2_r[m][3] = w2v.w;
+            c2[m][0] = (trx_f2){cv.x, cv.y};
+            c2[m][1] = (trx_f2){cv.z, cv.w};
+            if constexpr (DK == 6) {  // the four units' link-feature rows: 24 contiguous floats
+                float wv[24];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int k = 256 * m + 4 * lane + r;
-            const bool ok = k < Hd;
-            w2_r[m][r] = ok ? a.w2[k] : 0.0f;
-            c2[m][r >> 1][r & 1] = ok ? a.c[(int64_t)g * Hd + k] : 0.0f;
+                for (int q = 0; q < 6; ++q) {
+                    const float4 t = *reinterpret_cast<const float4*>(a.we + (size_t)k0 * 6 + 4 * q);
+                    wv[4 * q] = t.x, wv[4 * q + 1] = t.y, wv[4 * q + 2] = t.z, wv[4 * q + 3] = t.w;
+                }
 #pragma unroll
-            for (int j = 0; j < DC; ++j) we2[m][r >> 1][j][r & 1] = (ok && (DK > 0 || j < D)) ? a.we[k * D + j] : 0.0f;
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < 6; ++j) we2[m][r >> 1][j][r & 1] = wv[r * 6 + j];
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int j = 0; j < DC; ++j) we2[m][r >> 1][j][r & 1] = j < D ? a.we[(k0 + r) * D + j] : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                w2_r[m][r] = 0.0f;
+                c2[m][r >> 1][r & 1] = 0.0f;
+#pragma unroll
+                for (int j = 0; j < DC; ++j) we2[m][r >> 1][j][r & 1] = 0.0f;
+            }
         }
+    }
     const float b2 = a.b2[0];
     if (badf) *badl = 1;
     __syncthreads();
