@@ -680,6 +680,15 @@ int trx_per32_update(float* tree, int64_t capacity, const int64_t* idx, const do
                      double* max_priority, double eps, double alpha, void* stream);
 int trx_per32_sample(const float* tree, int64_t capacity, const double* u, int32_t n, int64_t* out_idx,
                      float* out_priority, void* stream);
+/* trx_per32_sample_weighted: trx_per32_sample plus ReplayBuffer.sample's
+ *   importance weights (train.py:80-82) in float32, as the device path states
+ *   them: w_k = (fl32(*size) * (out_priority[k] / tree[1])) ** (float)-beta,
+ *   then w /= max(w) when that max is > 0 -- one launch (one workgroup) instead
+ *   of the sample kernel and eight elementwise / reduction launches.  *size is
+ *   the buffer's current fill (float64, device memory, read at run time so a
+ *   captured graph sees the live value).                                    */
+int trx_per32_sample_weighted(const float* tree, int64_t capacity, const double* u, int32_t n, const double* size,
+                              double beta, int64_t* out_idx, float* out_priority, float* out_weight, void* stream);
 
 /* ------------------------------------------------------- damage draws (host)
  * RepairEnv.reset's damage draw (src/env/repair_env.py:167-192) for num_envs

@@ -633,6 +633,16 @@ int trx_per32_sample(const float* tree, int64_t capacity, const double* u, int32
     return TRX_OK;
 }
 
+int trx_per32_sample_weighted(const float* tree, int64_t capacity, const double* u, int32_t n, const double* size,
+                              double beta, int64_t* out_idx, float* out_priority, float* out_weight, void* stream) {
+    if (!tree || capacity < 1 || n < 0 || (n > 0 && (!u || !size || !out_idx || !out_priority || !out_weight)))
+        return fail(TRX_EINVAL, "per32_sample_weighted args");
+    hipError_t e = trx::launch_per32_sample_weighted(tree, capacity, u, n, size, beta, out_idx, out_priority,
+                                                     out_weight, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(TRX_EHIP, "per32_sample_weighted launch: %s", hipGetErrorString(e));
+    return TRX_OK;
+}
+
 int trx_gat_layer0_infer(const trx_gat_layer0_args* a, void* stream) {
     if (!a) return fail(TRX_EINVAL, "gat_layer0_infer: NULL args");
     const int HC = a->heads * a->channels;

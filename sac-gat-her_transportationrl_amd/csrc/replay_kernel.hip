@@ -418,6 +418,68 @@ __global__ void per32_sample_kernel(const float* __restrict__ tree, int64_t capa
     out_pri[k] = tree[node];
 }
 
+// float32 x ** e as torch's pow_tensor_scalar (the weights' op on the device):
+// exponents 2, 3, -2, -1, 0.5 and -0.5 by their closed forms, every other by powf
+__device__ __forceinline__ float pow_scalar_f32(float x, float e) {
+    if (e == 2.0f) return x * x;
+    if (e == 3.0f) return x * x * x;
+    if (e == -2.0f) return 1.0f / (x * x);
+    if (e == -1.0f) return 1.0f / x;
+    if (e == 0.5f) return sqrtf(x);
+    if (e == -0.5f) return rsqrtf(x);
+    return powf(x, e);
+}
+
+// sample + importance weights in ONE workgroup (train.py:61-84 in float32):
+// the descent above for every k, then w_k = (size * (pri_k / total)) ** -beta
+// and w /= max(w) when that max is > 0 (a NaN max leaves w unscaled, as
+// torch.where(wmax > 0, wmax, 1) does).  One block so the max needs no second
+// launch; a batch of n samples takes ceil(n / 1024) descents per lane.
+__global__ void __launch_bounds__(1024) per32_sample_weighted_kernel(const float* __restrict__ tree, int64_t capacity,
+                                                                     const double* __restrict__ u, int n,
+                                                                     const double* __restrict__ size, float neg_beta,
+                                                                     int64_t* __restrict__ out_idx,
+                                                                     float* __restrict__ out_pri,
+                                                                     float* __restrict__ out_w) {
+    __shared__ float wmax[16];
+    const float total = tree[1];
+    const float sz = (float)size[0];
+    float m = -INFINITY;
+    bool nan = false;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        float r = (float)(u[k] * (double)total);
+        int64_t node = 1;
+        while (node < capacity) {
+            const int64_t left = 2 * node;
+            const float tl = tree[left];
+            if (r <= tl) {
+                node = left;
+            } else {
+                r = r - tl;
+                node = left + 1;
+            }
+        }
+        const float pri = tree[node];
+        out_idx[k] = node - capacity;
+        out_pri[k] = pri;
+        const float w = pow_scalar_f32(sz * (pri / total), neg_beta);
+        out_w[k] = w;
+        nan |= w != w;
+        m = fmaxf(m, w);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        m = fmaxf(m, __shfl_xor(m, o, 64));
+        nan |= __shfl_xor((int)nan, o, 64) != 0;
+    }
+    const int wave = threadIdx.x >> 6, waves = (blockDim.x + 63) >> 6;
+    if ((threadIdx.x & 63) == 0) wmax[wave] = nan ? __int_as_float(0x7fc00000) : m;
+    __syncthreads();
+    float mx = wmax[0];
+    for (int w = 1; w < waves; ++w) mx = (mx != mx || wmax[w] != wmax[w]) ? __int_as_float(0x7fc00000) : fmaxf(mx, wmax[w]);
+    const float d = mx > 0.0f ? mx : 1.0f;
+    for (int k = threadIdx.x; k < n; k += blockDim.x) out_w[k] = out_w[k] / d;   // this lane's own stores
+}
+
 static int tree_levels(int64_t capacity) {   // internal bit lengths 1 .. d2-1
     int d2 = 0;
     while ((2 * capacity - 1) >> d2) ++d2;
@@ -461,6 +523,16 @@ hipError_t launch_per32_sample(const float* tree, int64_t capacity, const double
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(per32_sample_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, tree, capacity, u, n,
                        out_idx, out_pri);
+    return hipGetLastError();
+}
+
+hipError_t launch_per32_sample_weighted(const float* tree, int64_t capacity, const double* u, int n, const double* size,
+                                        double beta, int64_t* out_idx, float* out_pri, float* out_w,
+                                        hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int threads = n >= 1024 ? 1024 : ((n + 63) / 64) * 64;
+    hipLaunchKernelGGL(per32_sample_weighted_kernel, dim3(1), dim3(threads), 0, stream, tree, capacity, u, n, size,
+                       (float)(-beta), out_idx, out_pri, out_w);
     return hipGetLastError();
 }
 

@@ -251,5 +251,8 @@ hipError_t launch_per32_update(float* tree, int64_t capacity, const int64_t* idx
                                double* max_priority, double eps, double alpha, hipStream_t stream);
 hipError_t launch_per32_sample(const float* tree, int64_t capacity, const double* u, int n, int64_t* out_idx,
                                float* out_pri, hipStream_t stream);
+hipError_t launch_per32_sample_weighted(const float* tree, int64_t capacity, const double* u, int n, const double* size,
+                                        double beta, int64_t* out_idx, float* out_pri, float* out_w,
+                                        hipStream_t stream);
 
 }  // namespace trx

@@ -30,7 +30,7 @@ EXPORTS = (
     "trx_small_ln_forward", "trx_small_ln_workspace_floats", "trx_small_ln_backward", "trx_edge_head_backward",
     "trx_graph_pool_forward", "trx_graph_pool_backward", "trx_bf16_round", "trx_multi_copy",
     "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update", "trx_per32_sample",
-    "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
+    "trx_per32_sample_weighted", "trx_damage_sample", "trx_multi_gather", "trx_episode_step", "trx_env_kernel_name",
     "trx_gat_layer_backward", "trx_gat_layer_backward_part_floats", "trx_partial_sum", "trx_partial_sum_multi",
     "trx_gat_prologue_backward",
     "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
@@ -341,6 +341,7 @@ def load():
                                       ctypes.c_double, _vp]
     L.trx_per32_update.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _i32, _vp, ctypes.c_double, ctypes.c_double, _vp]
     L.trx_per32_sample.argtypes = [_vp, ctypes.c_int64, _vp, _i32, _vp, _vp, _vp]
+    L.trx_per32_sample_weighted.argtypes = [_vp, ctypes.c_int64, _vp, _i32, _vp, ctypes.c_double, _vp, _vp, _vp, _vp]
     L.trx_episode_step.argtypes = [_i32, _vp, _vp, _vp, ctypes.c_double, ctypes.c_int64] + [_vp] * 9 + [_vp]
     L.trx_multi_gather.argtypes = [ctypes.POINTER(TrxCopyList), _vp, _i32, _vp]
     L.trx_damage_sample.argtypes = [_i32, _i32, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32]
@@ -366,7 +367,7 @@ def load():
                  "trx_edge_head_backward", "trx_graph_pool_forward", "trx_graph_pool_backward",
                  "trx_bf16_round", "trx_multi_copy",
                  "trx_per_update_range", "trx_per_add_range", "trx_per32_add_range", "trx_per32_update",
-                 "trx_per32_sample", "trx_damage_sample", "trx_multi_gather",
+                 "trx_per32_sample", "trx_per32_sample_weighted", "trx_damage_sample", "trx_multi_gather",
                  "trx_episode_step", "trx_gat_layer_backward", "trx_partial_sum", "trx_gat_prologue_backward",
                  "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
                  "trx_gat_layer0_infer", "trx_gat_layer0_prepare", "trx_gat_mid_infer", "trx_partial_sum_multi"):

@@ -549,22 +549,25 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     dev = reward.device
     nx, ex = node_x.float().contiguous(), edge_attr.float().contiguous()
     nnx, nex = next_node_x.float().contiguous(), next_edge_attr.float().contiguous()
-    # the no-grad next-state passes (sac.py:184-191: next actor probs, two target
-    # critics) and the training forwards of the two critics and the actor (raw
-    # logits, with saves) are independent: six streams at once (each network's
-    # kernels fill a fraction of the GPU at batch 256)
+    # the training forwards of the actor and the two critics (raw logits, with
+    # saves) and the no-grad next-state passes (sac.py:184-191: next actor probs,
+    # two target critics) are independent: six branches on the side streams
+    # (each network's kernels fill a fraction of the GPU at batch 256).  The
+    # actor's training pass is issued first on every stream: its float32
+    # forward + backward is the update's longest chain, and a replayed graph
+    # starts its branches in issue order, ~0.2 ms apart
     xa, xc = (exact_nets(agent)[k] for k in ("actor", "critic"))
     with torch.no_grad():
-        outs = agent._concurrent([
-            # the next-state probabilities only enter the critics' target: the
-            # critics' precision (bf16 unless the agent trains in float32)
-            lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask, exact=xc)[0],
-            lambda: net_forward(agent.target1, nnx, nex, topo, save=False, exact=xc)[0],
-            lambda: net_forward(agent.target2, nnx, nex, topo, save=False, exact=xc)[0]] +
+        outs = agent._concurrent(
             [lambda net=net, x=x: net_forward(net, nx, ex, topo, save=True, exact=x)
-             for net, x in ((agent.critic1, xc), (agent.critic2, xc), (agent.actor, xa))])
-    nprobs, qt1, qt2 = outs[:3]
-    (q1, c1), (q2, c2), (lg, ca) = outs[3:]
+             for net, x in ((agent.actor, xa), (agent.critic1, xc), (agent.critic2, xc))] + [
+                # the next-state probabilities only enter the critics' target: the
+                # critics' precision (bf16 unless the agent trains in float32)
+                lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask, exact=xc)[0],
+                lambda: net_forward(agent.target1, nnx, nex, topo, save=False, exact=xc)[0],
+                lambda: net_forward(agent.target2, nnx, nex, topo, save=False, exact=xc)[0]])
+    (lg, ca), (q1, c1), (q2, c2) = outs[:3]
+    nprobs, qt1, qt2 = outs[3:]
     L = _lib.load()
     la = agent.log_alpha.detach().reshape(1)
     act_local = action % E      # the batch tuple carries graph offsets (arange(B) * E + action)
@@ -613,10 +616,9 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     # each network's backward on the stream its training forward ran on: the
     # saved tensors are read on the stream that allocated them
     sums = PartialSums(B)
-    agent._concurrent([lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc, sums=sums),
-                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc, sums=sums),
-                       lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums)],
-                      streams=(3, 4, 5))
+    agent._concurrent([lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
+                       lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc, sums=sums),
+                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc, sums=sums)])
     sums.flush(_lib.stream_ptr(dev))   # every network's column sums in one launch, on the joined stream
     agent.log_alpha.grad = g_la.view_as(agent.log_alpha)
     agent.grad_flat = flat        # every gradient of this update is a view of it (GradAllReduce)

@@ -200,14 +200,13 @@ class DeviceReplay:
         pri = torch.empty(batch_size, dtype=self.tree.dtype, device=self.device)
         L = _lib.load()
         if self.tree_dtype == "float32":
-            # train.py:80-82 in float32: probs = pri / total, (size * probs) ** -beta, / max
-            _lib.check(L.trx_per32_sample(_lib.ptr(self.tree), self.capacity, _lib.ptr(u.contiguous()), batch_size,
-                                          _lib.ptr(idx), _lib.ptr(pri), _lib.stream_ptr(self.device)),
-                       "trx_per32_sample")
-            probs = pri / self.total
-            w = (self.size_t.float() * probs) ** (-self.beta)
-            wmax = w.max()
-            w = w / torch.where(wmax > 0, wmax, torch.ones_like(wmax))
+            # train.py:80-82 in float32: probs = pri / total, (size * probs) ** -beta, / max,
+            # in the descent's launch (one workgroup; size_t read on the device)
+            w = torch.empty(batch_size, dtype=torch.float32, device=self.device)
+            _lib.check(L.trx_per32_sample_weighted(_lib.ptr(self.tree), self.capacity, _lib.ptr(u.contiguous()),
+                                                   batch_size, _lib.ptr(self.size_t), float(self.beta), _lib.ptr(idx),
+                                                   _lib.ptr(pri), _lib.ptr(w), _lib.stream_ptr(self.device)),
+                       "trx_per32_sample_weighted")
         else:
             _lib.check(L.trx_per_sample(_lib.ptr(self.tree), self.capacity, _lib.ptr(u), batch_size, _lib.ptr(idx),
                                         _lib.ptr(pri), _lib.stream_ptr(self.device)), "trx_per_sample")

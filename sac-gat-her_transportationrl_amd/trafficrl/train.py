@@ -382,6 +382,7 @@ class Trainer:
         self.act_ei, self.act_batch = batched_topology(ei, self.N, B)
         bs = int(cfg["batch_size"])
         self.upd_ei, self.upd_batch = batched_topology(ei, self.N, bs)
+        self.upd_act_off = torch.arange(bs, device=self.device) * self.E   # graph offsets of the batch's actions
         self.fixed_mask = None
         # per-env episode accumulators (device)
         self.ep_reward = torch.zeros(B, dtype=torch.float64, device=self.device)
@@ -467,7 +468,7 @@ class Trainer:
         s = her_relabel(s, cfg["her_ratio"], cfg["reward_mode"], cfg["reward_scale"], cfg["reward_alpha"],
                         cfg["reward_beta"], cfg["reward_gamma"], cfg["reward_clip"], u=her_u)
         E, N = self.E, self.N
-        action = torch.arange(bs, device=self.device) * E + s.action
+        action = self.upd_act_off + s.action
         batch = (s.node_x.reshape(bs * N, -1), self.upd_ei, s.edge_x.reshape(bs * E, -1), s.mask.reshape(-1),
                  self.upd_batch, action, s.reward, s.next_node_x.reshape(bs * N, -1), s.next_edge_x.reshape(bs * E, -1),
                  s.next_mask.reshape(-1), self.upd_batch, s.done)

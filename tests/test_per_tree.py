@@ -127,3 +127,33 @@ def test_device_tree_at_reference_buffer_size():
         ref.update_priorities(idx_u, td.astype(np.float64))
         np.testing.assert_array_equal(rb.tree.cpu().numpy(), ref.tree)
         assert rb.max_priority.item() == ref.max_p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("beta", [0.4, 1.0, 0.5, 2.0])
+@pytest.mark.parametrize("n", [256, 3000])
+def test_weighted_sample_matches_descent_and_torch_weights(beta, n):
+    """trx_per32_sample_weighted (the sample + weights launch DeviceReplay.sample
+    uses) against trx_per32_sample and the weights as torch ops state them
+    (probs = pri / total, (size * probs) ** -beta, / max): indices and
+    priorities bit-exact, weights within 2 float32 ulps (torch's powf build vs
+    ours); n = 3000 takes the multi-pass (n > 1024 lanes) path; beta 1.0 / 0.5 /
+    2.0 hit torch's closed-form exponents (-1, -0.5, -2)."""
+    from trafficrl import _lib
+    cap = 1000
+    rb = _device_replay(cap)
+    _adds(rb, 700)
+    L = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(n)
+    u = torch.rand(n, dtype=torch.float64, device="cuda", generator=g)
+    idx0 = torch.empty(n, dtype=torch.int64, device="cuda")
+    pri0 = torch.empty(n, dtype=torch.float32, device="cuda")
+    _lib.check(L.trx_per32_sample(_lib.ptr(rb.tree), cap, _lib.ptr(u), n, _lib.ptr(idx0), _lib.ptr(pri0), None),
+               "trx_per32_sample")
+    idx, pri, w = (torch.empty(n, dtype=t, device="cuda") for t in (torch.int64, torch.float32, torch.float32))
+    _lib.check(L.trx_per32_sample_weighted(_lib.ptr(rb.tree), cap, _lib.ptr(u), n, _lib.ptr(rb.size_t), beta,
+                                           _lib.ptr(idx), _lib.ptr(pri), _lib.ptr(w), None), "trx_per32_sample_weighted")
+    assert torch.equal(idx, idx0) and torch.equal(pri, pri0)
+    ref = (rb.size_t.float() * (pri0 / rb.total)) ** (-beta)
+    ref = ref / torch.where(ref.max() > 0, ref.max(), torch.ones_like(ref.max()))
+    assert _ulps32(w.cpu().numpy(), ref.cpu().numpy()).max() <= 2

@@ -115,6 +115,11 @@ for s in "$@"; do
                     TRX_UPD_STREAMS=1 step upd_s1 300 python tools/agent_profile.py 4096 update ;;
         updserial) step upd_default 300 python tools/agent_profile.py 4096 update &&
                    TRX_UPD_SERIAL=fwd step upd_fwdserial 300 python tools/agent_profile.py 4096 update ;;
+        hwq) for q in 4 8 16; do GPU_MAX_HW_QUEUES=$q step upd_q$q 300 python tools/agent_profile.py 4096 update || exit 1; done
+             DEBUG_HIP_FORCE_GRAPH_QUEUES=6 step upd_gq6 300 python tools/agent_profile.py 4096 update &&
+             DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 step upd_nopc 300 python tools/agent_profile.py 4096 update &&
+             step upd_log 300 bash -c "AMD_LOG_LEVEL=3 python tools/agent_profile.py 4096 update 2>&1 | grep -a -m 20 -E 'parallel streams|update wall'" ;;
+        updt) step upd_time 300 python tools/upd_time.py ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
         copies) step copies 300 python tools/update_profile.py 60 copies ;;
