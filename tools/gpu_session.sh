@@ -119,6 +119,9 @@ for s in "$@"; do
              DEBUG_HIP_FORCE_GRAPH_QUEUES=6 step upd_gq6 300 python tools/agent_profile.py 4096 update &&
              DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 step upd_nopc 300 python tools/agent_profile.py 4096 update &&
              step upd_log 300 bash -c "AMD_LOG_LEVEL=3 python tools/agent_profile.py 4096 update 2>&1 | grep -a -m 20 -E 'parallel streams|update wall'" ;;
+        bigab) L=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so
+               step abbig_a 300 python tools/ab_big.py $L 1024 && step abbig_b 300 python tools/ab_big.py $L 1024 &&
+               step profana 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profana -o run --output-format csv -- python3 bench.py --network anaheim --steps 6 --warmup 2 --no-cpu ;;
         updt) step upd_time 300 python tools/upd_time.py ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
