@@ -42,5 +42,3 @@ print(f"{dt * 1e3:.2f} ms/step  trees/step {trees / 3:.0f}  "
       f"sweeps/tree {buf[1] / max(trees, 1):.2f}  exact replays {buf[2]}")
 print(f"per tree (s_memtime ticks, 100 MHz): sweeps {buf[3] / max(trees, 1):.0f}  preds {buf[4] / max(trees, 1):.0f}  "
       f"walks {buf[5] / max(trees, 1):.0f}")
-print(f"warm (TRX_BIG_WARM={os.environ.get('TRX_BIG_WARM', 'default')}): waves restarted cold {buf[6]}, "
-      f"waves settled warm {buf[7]}")
