@@ -212,7 +212,8 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
     int* rp = cl + a.max_graph_edges;                    // [n+1] graph-local row pointers
     int* dlc = rp + n + 1;                               // [me] graph-local destination per CSR position
     float* x0l = reinterpret_cast<float*>(dlc + a.max_graph_edges);  // [n*IN]
-    float* yt = x0l + n * IN;                            // [n][HC] (pool only)
+    float* yt = reinterpret_cast<float*>(smem + ((reinterpret_cast<char*>(x0l + n * IN) - smem + 15) &
+                                                 ~(ptrdiff_t)15));  // [n][HC] (pool only), 16-byte aligned
 #ifdef TRX_LDS_CLEAR
     {  // diagnostic build: zero the workgroup's whole LDS window first (uninitialised-read probe)
         const int words = (int)((reinterpret_cast<char*>(yt + (a.pool ? n * HC : 0)) - smem) / 4);
@@ -516,8 +517,10 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
                 else
                     y = y <= 0.0f ? (expf(y) - 1.0f) : y;
                 y4[r] = y;
-                if (a.pool) yt[i * HC + f0 + r] = y;
             }
+            // one 16-byte store per lane (four scalar stores at a 4-word lane stride hit
+            // the same banks from lanes 16 apart)
+            if (a.pool) *reinterpret_cast<float4*>(yt + i * HC + f0) = make_float4(y4[0], y4[1], y4[2], y4[3]);
             if (a.out_f32)
                 *reinterpret_cast<float4*>(a.out_f32 + (size_t)node * HC + f0) = make_float4(y4[0], y4[1], y4[2], y4[3]);
             if (a.out_bf16) {
@@ -921,7 +924,7 @@ size_t gat_layer_infer_smem(const trx_gat_layer_args& a) {
     const size_t alsz = (size_t)me * H;
     size_t b = (a.exact ? (size_t)n * (HC + 4) * 4 : (size_t)n * (HC + 8) * 2) + 2 * (size_t)n * H * 4 + alsz * 4 + (size_t)me * 4 * 2 + (size_t)(n + 1) * 4 +
                (size_t)n * a.in_dim * 4;
-    if (a.pool) b += (size_t)n * HC * 4;
+    if (a.pool) b += (size_t)n * HC * 4 + 12;  // + the 16-byte alignment of the pool rows
     return b;
 }
 

@@ -87,9 +87,9 @@ for s in "$@"; do
                  step upd_race_fwd 300 python tools/update_graph_race.py 30 fwdserial &&
                  step upd_race_nopatch 300 python tools/update_graph_race.py 30 nopatch ;;
         graphrace) step graph_race 200 python tools/graph_branch_race.py ;;
-        ehab) step eh_cs_a 200 env TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so python tools/act_checksum.py 4096 &&
+        ehab) step eh_cs_a 200 env TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_old.so python tools/act_checksum.py 4096 &&
               step eh_cs_b 200 python tools/act_checksum.py 4096 &&
-              TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act &&
+              TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_old.so step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act &&
               step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         layerrace5) TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race6_fences 300 python tools/layer_concurrency_race.py 6 20 train &&
                     TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race3_fences 300 python tools/layer_concurrency_race.py 3 20 train ;;
@@ -122,13 +122,14 @@ for s in "$@"; do
         bigab) L=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so
                step abbig_a 300 python tools/ab_big.py $L 1024 && step abbig_b 300 python tools/ab_big.py $L 1024 &&
                step profana 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profana -o run --output-format csv -- python3 bench.py --network anaheim --steps 6 --warmup 2 --no-cpu ;;
+        poolab) step fused_tests 600 python -u -m pytest tests/test_split_gemm.py tests/test_fused_update.py tests/test_sac_e2e.py tests/test_sac.py tests/test_gat_infer.py tests/test_gat.py tests/test_gat_tail.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
         updt) step upd_time 300 python tools/upd_time.py ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
         copies) step copies 300 python tools/update_profile.py 60 copies ;;
         istamps) step istamps 300 python tools/infer_stamps.py 4096 ;;
         abact) TRX_LIB=${TRX_LIB_A:-} step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act
-               TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_b.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
+               TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_old.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         abk) step ab_quad 200 env TRX_KERNEL=quad python tools/ab_env.py sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl.so 4096 30 ;;
         fused) step fused_tests 600 python -u -m pytest tests/test_split_gemm.py tests/test_flat_adam.py tests/test_fused_update.py tests/test_sac_e2e.py tests/test_sac.py -m gpu -v -s --timeout 300 --timeout-method thread ;;
         bigstats) step big_stats 300 python tools/big_stats.py 1024 fw ;;
