@@ -216,6 +216,20 @@ def test_round_and_psum_lists_validated_without_gpu():
     assert L.trx_partial_sum_multi(ctypes.byref(ps), None) == 0
 
 
+def test_weighted_sample_validated_without_gpu():
+    """trx_per32_sample_weighted refuses missing buffers / a bad capacity before
+    any HIP call; an empty batch is a no-op."""
+    from trafficrl import _lib
+    L = _lib.load()
+    f = L.trx_per32_sample_weighted
+    assert f(None, 8, 16, 4, 16, 0.4, 16, 16, 16, None) == -1          # no tree
+    assert f(16, 0, 16, 4, 16, 0.4, 16, 16, 16, None) == -1            # capacity < 1
+    assert f(16, 8, 16, 4, None, 0.4, 16, 16, 16, None) == -1          # no size
+    assert f(16, 8, 16, 4, 16, 0.4, 16, 16, None, None) == -1          # no weight output
+    assert f(16, 8, 16, -1, 16, 0.4, 16, 16, 16, None) == -1           # n < 0
+    assert f(16, 8, None, 0, None, 0.4, None, None, None, None) == 0   # empty batch
+
+
 def test_fused_infer_validation_without_gpu():
     """Argument checks run before any HIP call: unsupported shapes are refused
     with TRX_EUNSUP / TRX_EINVAL and a message."""
