@@ -23,6 +23,7 @@ relabelled `done` = is_goal_complete(1 - mask', mask') is always 1.
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass
 from typing import Optional
 
@@ -100,6 +101,20 @@ class DeviceReplay:
         self.ptr = 0
         self.size = 0
         self.size_t = torch.zeros((), dtype=torch.float64, device=dev)  # device copy for graph-captured sampling
+        # overlap_adds (the trainer sets it): the float32 tree's ring adds run on a side
+        # stream of their own, beside the next acting pass (they read only the tree and
+        # max_priority); sync_adds() joins them before anything reads those again
+        self.overlap_adds = False
+        self._add_stream = None
+        self._adds_pending = False
+
+    def sync_adds(self):
+        """Make the current stream wait for the side-stream tree adds (no-op when
+        none is pending).  Call outside graph capture, before sample /
+        update_priorities / reading the tree."""
+        if self._adds_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self._add_stream)
+            self._adds_pending = False
 
     def _ring_idx(self, B: int) -> torch.Tensor:
         return (self.ptr + torch.arange(B, device=self.device)) % self.capacity
@@ -153,12 +168,19 @@ class DeviceReplay:
         # k sequential reference adds: priority_k = max_p + (k+1)*eps (train.py:50-58)
         if self.tree_dtype == "float32":
             L, lo, left = _lib.load(), self.ptr, B
-            while left > 0:          # ring order: [ptr, capacity) then from 0 (each piece one launch)
-                n = min(left, self.capacity - lo)
-                _lib.check(L.trx_per32_add_range(_lib.ptr(self.tree), self.capacity, lo, n,
-                                                 _lib.ptr(self.max_priority), float(self.eps), float(self.alpha),
-                                                 _lib.stream_ptr(self.device)), "trx_per32_add_range")
-                lo, left = (lo + n) % self.capacity, left - n
+            side = self.overlap_adds and self.device.type == "cuda" and not torch.cuda.is_current_stream_capturing()
+            if side:
+                if self._add_stream is None:
+                    self._add_stream = torch.cuda.Stream(self.device)
+                self._add_stream.wait_stream(torch.cuda.current_stream(self.device))   # after every earlier write
+                self._adds_pending = True
+            with torch.cuda.stream(self._add_stream) if side else contextlib.nullcontext():
+                while left > 0:          # ring order: [ptr, capacity) then from 0 (each piece one launch)
+                    n = min(left, self.capacity - lo)
+                    _lib.check(L.trx_per32_add_range(_lib.ptr(self.tree), self.capacity, lo, n,
+                                                     _lib.ptr(self.max_priority), float(self.eps), float(self.alpha),
+                                                     _lib.stream_ptr(self.device)), "trx_per32_add_range")
+                    lo, left = (lo + n) % self.capacity, left - n
         elif self.ptr + B <= self.capacity and self.device.type == "cuda":
             L = _lib.load()     # one launch: leaves, ancestors and max_priority (updated in place)
             _lib.check(L.trx_per_add_range(_lib.ptr(self.tree), self.capacity, self.ptr, B, _lib.ptr(self.max_priority),
@@ -194,6 +216,8 @@ class DeviceReplay:
         HIP-graph trainer fills it outside the captured region."""
         if self.size == 0:
             raise ValueError("Cannot sample from an empty replay buffer.")
+        if not torch.cuda.is_available() or not torch.cuda.is_current_stream_capturing():
+            self.sync_adds()
         if u is None:
             u = torch.rand(batch_size, dtype=torch.float64, device=self.device, generator=generator)
         idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
@@ -223,6 +247,8 @@ class DeviceReplay:
         return Sample(idx, w.float(), *rows, pri)
 
     def update_priorities(self, idx: torch.Tensor, td_errors: torch.Tensor):
+        if not torch.cuda.is_available() or not torch.cuda.is_current_stream_capturing():
+            self.sync_adds()
         if self.tree_dtype == "float32":
             err = td_errors.detach().to(torch.float64).contiguous()
             idx = idx.contiguous()

@@ -378,6 +378,10 @@ class Trainer:
         cap = min(int(cfg["buffer_size"]), max(int(cfg["buffer_size"]) // world, B))
         self.replay = DeviceReplay(cap, self.N, self.E, alpha=cfg["per_alpha"], beta=cfg["per_beta"],
                                    eps=cfg["per_eps"], device=self.device, tree_dtype=cfg["per_tree"])
+        # the float32 tree's ring adds beside the next acting pass (same results: the adds
+        # keep their order on their own stream; updates join them first)
+        self.replay.overlap_adds = self.device.type == "cuda" and bool(cfg.get("overlap_per_adds", True)) and \
+            os.environ.get("TRX_PER_OVERLAP", "1") != "0"
         ei = self.env.edge_index
         self.act_ei, self.act_batch = batched_topology(ei, self.N, B)
         bs = int(cfg["batch_size"])
@@ -440,6 +444,7 @@ class Trainer:
     # ------------------------------------------------------------ update
     def update(self):
         """One SAC update on a PER batch (src/train.py:954-1024 update block)."""
+        self.replay.sync_adds()   # the tree adds of the last iterations (side stream) before the sample
         if self._graphed is not None:
             out = self._graphed()
         else:

@@ -123,6 +123,9 @@ for s in "$@"; do
                step abbig_a 300 python tools/ab_big.py $L 1024 && step abbig_b 300 python tools/ab_big.py $L 1024 &&
                step profana 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profana -o run --output-format csv -- python3 bench.py --network anaheim --steps 6 --warmup 2 --no-cpu ;;
         poolab) step fused_tests 600 python -u -m pytest tests/test_split_gemm.py tests/test_fused_update.py tests/test_sac_e2e.py tests/test_sac.py tests/test_gat_infer.py tests/test_gat.py tests/test_gat_tail.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
+        perov) step per_tests 400 python -u -m pytest tests/test_per_tree.py tests/test_replay_train.py tests/test_determinism.py -m gpu -x -q --timeout 300 --timeout-method thread &&
+               TRX_PER_OVERLAP=0 step bench_pov0 400 python bench.py --steps 44 --warmup 22 --no-cpu && step bench_pov1 400 python bench.py --steps 44 --warmup 22 --no-cpu &&
+               TRX_PER_OVERLAP=0 step bench_pov0b 400 python bench.py --steps 44 --warmup 22 --no-cpu && step bench_pov1b 400 python bench.py --steps 44 --warmup 22 --no-cpu ;;
         updt) step upd_time 300 python tools/upd_time.py ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
