@@ -55,7 +55,11 @@ class VecObs:
     node_x: torch.Tensor     # [B, N, 4]
     edge_x: torch.Tensor     # [B, E, 6]
     action_mask: torch.Tensor  # [B, E]
-    log_tstt: torch.Tensor   # [B] float64
+    tstt: torch.Tensor       # [B] float64, the env's TSTT buffer (valid until the next step, like the rest)
+
+    @property
+    def log_tstt(self) -> torch.Tensor:   # [B] float64, evaluated on access (no per-step launch)
+        return torch.log10(torch.clamp(self.tstt, min=1.0))
 
 
 class VecRepairEnv:
@@ -300,7 +304,9 @@ class VecRepairEnv:
                               _lib.ptr(a), _lib.ptr(self.reward), _lib.ptr(self.done), _lib.ptr(self.valid),
                               _lib.ptr(self.workspace), self._stream()), "trx_step")
         obs = self.observe() if observe else None
-        return obs, self.reward, self.done.bool(), {"tstt": self.tstt, "valid": self.valid.bool()}
+        # done / valid are 0/1 bytes: bool views of the env's buffers (no cast launch; valid
+        # until the next step, like reward and the observation buffers)
+        return obs, self.reward, self.done.view(torch.bool), {"tstt": self.tstt, "valid": self.valid.view(torch.bool)}
 
     def observe(self) -> VecObs:
         L = _lib.load()
@@ -308,8 +314,7 @@ class VecRepairEnv:
         _lib.check(L.trx_observe(self.graph.handle, self.num_envs, ctypes.byref(self._state), _lib.ptr(node_x),
                                  _lib.ptr(edge_x), _lib.ptr(mask), _lib.ptr(self.workspace), self._stream()),
                    "trx_observe")
-        log_tstt = torch.log10(torch.clamp(self.tstt, min=1.0))
-        return VecObs(node_x, edge_x, mask, log_tstt)
+        return VecObs(node_x, edge_x, mask, self.tstt)
 
     # ------------------------------------------------------ GP path sets
     def _gp_rows(self):

@@ -107,14 +107,19 @@ class DeviceReplay:
         self.overlap_adds = False
         self._add_stream = None
         self._adds_pending = False
+        self._size_dirty = False
 
     def sync_adds(self):
-        """Make the current stream wait for the side-stream tree adds (no-op when
-        none is pending).  Call outside graph capture, before sample /
-        update_priorities / reading the tree."""
+        """Make the current stream wait for the side-stream tree adds and refresh
+        the device copy of the fill level (no-op when nothing is pending).  Call
+        outside graph capture, before sample / update_priorities / reading the
+        tree or size_t."""
         if self._adds_pending:
             torch.cuda.current_stream(self.device).wait_stream(self._add_stream)
             self._adds_pending = False
+        if self._size_dirty:
+            self.size_t.fill_(float(self.size))
+            self._size_dirty = False
 
     def _ring_idx(self, B: int) -> torch.Tensor:
         return (self.ptr + torch.arange(B, device=self.device)) % self.capacity
@@ -193,7 +198,10 @@ class DeviceReplay:
             self._set(idx, pr ** self.alpha, distinct=B <= self.capacity)
         self.ptr = (self.ptr + B) % self.capacity
         self.size = min(self.size + B, self.capacity)
-        self.size_t.fill_(float(self.size))
+        if self.overlap_adds:
+            self._size_dirty = True   # refreshed by sync_adds(), before any sample
+        else:
+            self.size_t.fill_(float(self.size))
 
     @property
     def total(self) -> torch.Tensor:
