@@ -161,7 +161,6 @@ extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
 template <int HC, int IN, int NT, bool XF>
 __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TRX_KFENCE_ACQ();
     typedef typename XElem<XF>::T XE;
     constexpr int EV = 16 / sizeof(XE);  // row elements per 16-byte piece
     constexpr int kInferThreads = NT, kInferWaves = NT / kWave;  // this instance's workgroup
@@ -214,13 +213,6 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
     float* x0l = reinterpret_cast<float*>(dlc + a.max_graph_edges);  // [n*IN]
     float* yt = reinterpret_cast<float*>(smem + ((reinterpret_cast<char*>(x0l + n * IN) - smem + 15) &
                                                  ~(ptrdiff_t)15));  // [n][HC] (pool only), 16-byte aligned
-#ifdef TRX_LDS_CLEAR
-    {  // diagnostic build: zero the workgroup's whole LDS window first (uninitialised-read probe)
-        const int words = (int)((reinterpret_cast<char*>(yt + (a.pool ? n * HC : 0)) - smem) / 4);
-        for (int w = tid; w < words; w += kInferThreads) reinterpret_cast<float*>(smem)[w] = 0.0f;
-        __syncthreads();
-    }
-#endif
 
     // 0b. graph-local CSR slice, this layer's edge logits, layer-0 inputs: every
     //     load of the phase issued before the first LDS store (one HBM round trip)
@@ -547,7 +539,6 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args 
         }
         TRX_ISTAMP(7);
     }
-    TRX_KFENCE_REL();
 }
 
 // --------------------------------------------------------- edge scorer
@@ -789,7 +780,6 @@ __global__ void __launch_bounds__(kWave) edge_att_weights_kernel(trx_gat_prologu
     for (int c = lane; c < C; c += kWave) s += a.lin_edge_w[l][(size_t)(h * C + c) * D + j] * a.att_edge[l][h * C + c];
     s = wave_sum_f(s);
     if (lane == 0) a.m_work[(row0 + h) * D + j] = s;
-    TRX_KFENCE_REL();
 }
 
 constexpr int kProMD = 8;  // node_dim, edge_dim <= 8; LDS rows padded to 8 floats
@@ -823,7 +813,6 @@ __device__ __forceinline__ void layer_norm_row(float (&x)[kProMD], int d, const 
 template <int NT>
 __global__ void __launch_bounds__(NT) gat_prologue_kernel(trx_gat_prologue_args a, int A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    TRX_KFENCE_ACQ();
     constexpr int MD = kProMD;
     const int g = blockIdx.x, tid = threadIdx.x;
     const int n = a.nodes_per_graph, E = a.edges_per_graph, ND = a.node_dim, D = a.edge_dim;
@@ -894,7 +883,6 @@ __global__ void __launch_bounds__(NT) gat_prologue_kernel(trx_gat_prologue_args 
             a.a_edge[(size_t)p * A + k] = ok ? (a.exact ? acc : bf16r(acc)) : __builtin_nanf("");
         }
     }
-    TRX_KFENCE_REL();
 }
 
 size_t gat_prologue_smem(const trx_gat_prologue_args& a) {

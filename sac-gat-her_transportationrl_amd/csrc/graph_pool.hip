@@ -73,7 +73,6 @@ namespace {
 __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     const int k = blockIdx.y;
     if (k >= l.count) return;
-    TRX_KFENCE_ACQ();
     // 32-bit index arithmetic (every tensor < 2^31 elements, checked at launch);
     // four consecutive elements of one row per thread when the row length allows
     const uint32_t cols = (uint32_t)l.cols[k], n = (uint32_t)(l.rows[k] * l.cols[k]);
@@ -111,7 +110,6 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
                     make_float4((float)h0, (float)h1, (float)h2, (float)h3);
             }
         }
-        TRX_KFENCE_REL();
         return;
     }
     for (uint32_t i0 = blockIdx.x * 256u + threadIdx.x; i0 < n; i0 += step) {
@@ -123,7 +121,6 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
         else
             static_cast<float*>(l.dst[k])[i] = mode == 2 ? x : (float)h;
     }
-    TRX_KFENCE_REL();
 }
 }  // namespace
 

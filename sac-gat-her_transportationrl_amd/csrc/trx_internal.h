@@ -6,19 +6,6 @@
 
 #include "trafficrl.h"
 
-// Diagnostic build only (make fences): agent-scope acquire at kernel entry and
-// release at exit in the fused GAT kernels (graph-replay coherence probe).
-#ifdef TRX_FENCES
-#define TRX_KFENCE_ACQ() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
-#define TRX_KFENCE_REL() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
-#else
-#define TRX_KFENCE_ACQ() \
-    do {                 \
-    } while (0)
-#define TRX_KFENCE_REL() \
-    do {                 \
-    } while (0)
-#endif
 
 namespace trx {
 

@@ -52,6 +52,8 @@ def resolve_sp_rule(sp_backend: Optional[str], num_nodes: int, force_gpu_sp: boo
 
 @dataclass
 class VecObs:
+    """A step's observation as VIEWS of the env's persistent buffers: valid
+    until the next step / reset / observe overwrites them (clone to keep)."""
     node_x: torch.Tensor     # [B, N, 4]
     edge_x: torch.Tensor     # [B, E, 6]
     action_mask: torch.Tensor  # [B, E]
@@ -290,7 +292,12 @@ class VecRepairEnv:
         return self.observe() if observe else None
 
     def step(self, actions: torch.Tensor, observe: bool = True, check: bool = True):
-        """Batched RepairEnv.step.  Returns (obs, reward[B] f64, done[B] bool, info)."""
+        """Batched RepairEnv.step.  Returns (obs, reward[B] f64, done[B] bool, info).
+
+        The returned tensors ALIAS the env's own buffers, overwritten by the next
+        step: reward, done / info["valid"] (bool views of the byte buffers),
+        info["tstt"] and the observation buffers (VecObs.log_tstt is computed
+        from the live tstt on access).  Clone what must outlive the step."""
         a = actions.to(device=self.device, dtype=torch.int32).contiguous()
         if a.numel() != self.num_envs:
             raise ValueError(f"expected {self.num_envs} actions, got {a.numel()}")
@@ -401,9 +408,10 @@ class DamagePrefetch:
         self.restart(env.damaged_ratio)
 
     def restart(self, ratio):
-        """(Re)start the draw of the next masks from the envs' current states."""
-        if self.job is not None:
-            self.job[2].result()     # never two draws into one buffer
+        """(Re)start the draw of the next masks from the envs' current states.
+        Never blocks: a stale draw still running (a partial reset discarded it)
+        is left to finish -- the pool's single worker runs draws in submission
+        order, so two draws never write one buffer at the same time."""
         env, k = self.env, self.which
         states = np.ascontiguousarray(env._rng_states).copy()
         ev = self.copied[k]
@@ -420,9 +428,11 @@ class DamagePrefetch:
     def take(self, ids, ratio) -> Optional[torch.Tensor]:
         env = self.env
         k, r, fut = self.job
-        states = fut.result()
         if r != ratio or len(ids) != env.num_envs or list(ids) != list(range(env.num_envs)):
-            return None              # not committed: the caller's synchronous draw restarts us
+            # not committed, and not waited for: the caller draws synchronously from the
+            # envs' true states and restarts us (the stale draw finishes on its own)
+            return None
+        states = fut.result()
         env._rng_states[:] = states
         dev = self.bufs[k].to(env.device, non_blocking=True)
         ev = torch.cuda.Event()

@@ -80,24 +80,37 @@ class NetCtx:
     head_w: tuple
 
 
-_MM32 = [None]   # torch.mm(..., out_dtype=torch.float32) available on this build (probed once, eagerly)
+_MM32 = [None]   # torch.mm(..., out_dtype=torch.float32) available on this build (probe_mm32)
+
+
+def probe_mm32(device) -> bool:
+    """Probe torch.mm(bf16, bf16, out_dtype=float32) once, eagerly (DiscreteSAC
+    construction): the first update may run inside a graph capture, where a
+    failing probe call cannot be made."""
+    if _MM32[0] is None:
+        try:
+            a = torch.zeros(2, 2, device=device, dtype=torch.bfloat16)
+            _MM32[0] = torch.mm(a, a, out_dtype=torch.float32).dtype == torch.float32
+        except (RuntimeError, TypeError):
+            _MM32[0] = False
+    return _MM32[0]
 
 
 def _mm32(a: torch.Tensor, b: torch.Tensor, add: Optional[torch.Tensor] = None) -> torch.Tensor:
     """a @ b (+ add) from bf16 operands with the float32 accumulator as the
     result (no bf16 rounding of the product: the update's gradients flow in
-    fp32 between the layer kernels, and no cast kernel runs)."""
-    if _MM32[0] is None and not torch.cuda.is_current_stream_capturing():
-        try:
-            t = torch.mm(a[:2], b, out_dtype=torch.float32)
-            _MM32[0] = t.dtype == torch.float32
-        except (RuntimeError, TypeError):
-            _MM32[0] = False
+    fp32 between the layer kernels, and no cast kernel runs).  Without
+    out_dtype support: a float32 GEMM of the same bf16 values (exact products,
+    float32 sums) -- never a bf16-rounded product."""
+    if _MM32[0] is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("fused_update.probe_mm32 must run before the update is captured")
+        probe_mm32(a.device)
     if _MM32[0]:
         if add is None:
             return torch.mm(a, b, out_dtype=torch.float32)
         return torch.addmm(add, a, b, out_dtype=torch.float32)
-    r = (a @ b).float()
+    r = torch.mm(a.float(), b.float())
     return r if add is None else r + add
 
 
@@ -113,7 +126,7 @@ def _mm3(a3: torch.Tensor, b3: torch.Tensor, add: Optional[torch.Tensor] = None,
     if out is None:
         return _mm32(a3, b3, add)
     if _MM32[0] is None:
-        _mm32(a3[:2], b3)
+        probe_mm32(a3.device)
     if _MM32[0]:
         if add is None:
             return torch.mm(a3, b3, out_dtype=torch.float32, out=out)

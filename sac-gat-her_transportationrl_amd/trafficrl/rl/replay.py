@@ -205,6 +205,11 @@ class DeviceReplay:
 
     @property
     def total(self) -> torch.Tensor:
+        """The sum tree's root; joins pending side-stream adds first (outside a
+        capture).  Direct reads of `tree` / `max_priority` / `size_t` need
+        sync_adds() the same way when overlap_adds is on."""
+        if not (torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()):
+            self.sync_adds()
         return self.tree[1]
 
     def add_batch(self, node_x, edge_x, mask, action, reward, next_node_x, next_edge_x, next_mask, done, goal,

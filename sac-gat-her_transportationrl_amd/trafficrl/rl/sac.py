@@ -362,6 +362,9 @@ class DiscreteSAC:
         self.critic_opt = torch.optim.Adam(critic_params, lr=critic_lr, **adam)
         dev = device if device is not None else "cpu"
         self.log_alpha = torch.tensor(float(np.log(max(alpha_init, 1e-8))), requires_grad=True, device=dev)
+        if self.log_alpha.is_cuda:   # before any update can be captured (fused_update._mm32)
+            from . import fused_update
+            fused_update.probe_mm32(self.log_alpha.device)
         self.alpha_opt = torch.optim.Adam([self.log_alpha], lr=alpha_lr, **adam)
         self.gamma = gamma
         self.target_tau = target_tau
@@ -376,11 +379,9 @@ class DiscreteSAC:
         self.grad_sync: Optional[Callable[[list], None]] = None
         # independent forwards (and their backwards) on side streams (_concurrent),
         # at most max_streams at once (3: the fastest measured, tools/agent_profile.py).
-        # Concurrent branches make the captured update's GAT layer kernels differ
-        # from replay to replay in the last bits (tools/layer_concurrency_race.py:
-        # same inputs, different outputs; serialized streams reproducible; DESIGN
-        # §5): max_streams = 1 (Trainer deterministic_update) gives bitwise
-        # reproducible training
+        # The result is the same bit for bit as with max_streams = 1
+        # (tests/test_concurrent_update.py; the round-4 replay-to-replay differences
+        # were a gfx950 packed-FP32 hazard under CU sharing, compiled out: DESIGN §5)
         self.concurrent = True
         self.max_streams = 3
         self._side = None

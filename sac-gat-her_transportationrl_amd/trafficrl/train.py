@@ -365,7 +365,7 @@ class Trainer:
             share_critic_encoder=cfg["share_critic_encoder"], alpha_init=cfg["alpha_init"],
             target_entropy_ratio=cfg["target_entropy_ratio"], device=self.device, amp_dtype=amp,
             capturable=self.use_graphs, fp32_actor=bool(cfg.get("fp32_actor", True)))
-        if cfg.get("deterministic_update"):   # bitwise reproducible updates: one stream
+        if cfg.get("deterministic_update"):   # the update on one stream (same bits as the default, slower)
             self.agent.max_streams = 1
         if world > 1:
             import torch.distributed as dist

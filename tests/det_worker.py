@@ -1,6 +1,7 @@
 """Worker for tests/test_determinism.py: one single-rank Trainer run at the
 bench's network sizes (hidden = embed = 256: the fused acting pass and the
-fused, graphed SAC update) from fixed seeds; writes per-iteration checksums
+fused, graphed SAC update on its default concurrent side streams) from fixed
+seeds; writes per-iteration checksums
 (actions, flows, the update's TD errors) and the final parameters.
 
 Usage: python det_worker.py <out.pt> <iters> [fill_nan]
@@ -39,37 +40,8 @@ def main():
     cfg.update(num_envs=512, batch_start=512, batch_size=256, hidden_dim=256, embed_dim=256, eval_every=0,
                output_dir=os.path.join(os.path.dirname(out), "det_run"), update_every=1, update_unit="iterations",
                her_ratio=0.0, assignment_method="msa", assignment_iters=30, fixed_damage=True, fixed_damage_seed=42,
-               sp_backend="scipy", early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0, amp="bf16",
-               deterministic_update=os.environ.get("TRX_DET_CONCURRENT") != "1")
+               sp_backend="scipy", early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0, amp="bf16")
     tr = Trainer(cfg, device="cuda:0", log=False)
-    if os.environ.get("TRX_UPD_STREAMS"):   # concurrent side streams of the update (A/B)
-        tr.agent.max_streams = int(os.environ["TRX_UPD_STREAMS"])
-    serial = os.environ.get("TRX_DET_SERIAL", "")
-    if serial == "1":   # diagnostics: no side streams in the update
-        tr.agent.concurrent = False
-    elif serial in ("fwd", "bwd"):   # only the fused update's forward (6 calls) or backward (3) phase serial
-        conc = tr.agent._concurrent
-        n_serial = 6 if serial == "fwd" else 3
-
-        def phase(fns, streams=None):
-            return [fn() for fn in fns] if len(fns) == n_serial else conc(fns, streams)
-        tr.agent._concurrent = phase
-    if os.environ.get("TRX_DET_NOGRAPH") == "1":   # diagnostics: eager updates throughout
-        tr._graphed = None
-    groups = os.environ.get("TRX_DET_FWD_GROUPS", "")   # e.g. "012|345": forward passes concurrent per group
-    if groups:
-        conc = tr.agent._concurrent
-        order = [[int(c) for c in g] for g in groups.split("|")]
-
-        def grouped(fns, streams=None):
-            if len(fns) != 6:
-                return conc(fns, streams)
-            outs = [None] * 6
-            for grp in order:
-                for i, o in zip(grp, conc([fns[i] for i in grp]) if len(grp) > 1 else [fns[grp[0]]()]):
-                    outs[i] = o
-            return outs
-        tr.agent._concurrent = grouped
     tr._reset_envs(None)
     obs = tr.env.observe()
     trace = []

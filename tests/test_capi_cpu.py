@@ -254,3 +254,28 @@ def test_fused_infer_validation_without_gpu():
     h.edge_dim, h.nodes_per_graph = 6, 200             # p rows of one graph would not fit in LDS
     assert L.trx_edge_head_infer(h, None) == -3
     assert b"nodes_per_graph" in L.trx_last_error()
+
+
+def test_no_packed_fp32_instructions(tmp_path):
+    """The library is built without packed-FP32 VALU instructions (Makefile
+    -target-feature -packed-fp32-ops): on gfx950 their results can reach a DPP
+    or packed consumer two wait states later without the last 16 lanes while
+    another kernel's waves share the CU -- the round-4 nondeterminism of the
+    concurrently replayed SAC update (tests/test_concurrent_update.py)."""
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    from trafficrl import codeobj
+    cos = codeobj._code_objects(open(LIB, "rb").read())
+    assert cos, "no gfx950 code objects in the library"
+    hits = {}
+    for k, co in enumerate(cos):
+        path = tmp_path / f"co{k}.o"
+        path.write_bytes(co)
+        asm = subprocess.run([objdump, "-d", "--mcpu=gfx950", str(path)], check=True, capture_output=True,
+                             text=True).stdout
+        n = len(re.findall(r"\bv_pk_(?:add|mul|fma)_f32\b", asm))
+        assert "s_endpgm" in asm
+        if n:
+            hits[k] = n
+    assert not hits, f"packed-FP32 instructions in code objects {hits}"

@@ -1,12 +1,12 @@
 """Cross-process determinism of training (round-3 verdict: two identical
-single-rank runs ended ~3e-4 apart in parameters).  Two processes run the
-same seeds through acting (fused, graphed), env steps and graphed fused SAC
-updates at the bench's network sizes with deterministic_update=True (the
-update's passes on one stream: with concurrent side streams the captured
-update's layer kernels differ in the last bits from replay to replay,
-tools/layer_concurrency_race.py); every iteration's actions,
-flows, TD errors and parameters must be bit-identical, and so must the final
-parameters.  A third run poisons fresh device allocations with NaN: no
+single-rank runs ended ~3e-4 apart in parameters; round 4: only with
+deterministic_update=True).  Two processes run the same seeds through acting
+(fused, graphed), env steps and graphed fused SAC updates at the bench's
+network sizes with the trainer's defaults -- the update's passes on three
+concurrent side streams (the round-4 race was a gfx950 packed-FP32 hazard, now
+compiled out: DESIGN §5, tests/test_concurrent_update.py); every iteration's
+actions, flows, TD errors and parameters must be bit-identical, and so must the
+final parameters.  A third run poisons fresh device allocations with NaN: no
 kernel may read memory nothing wrote."""
 import os
 import subprocess

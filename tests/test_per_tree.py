@@ -157,3 +157,37 @@ def test_weighted_sample_matches_descent_and_torch_weights(beta, n):
     ref = (rb.size_t.float() * (pri0 / rb.total)) ** (-beta)
     ref = ref / torch.where(ref.max() > 0, ref.max(), torch.ones_like(ref.max()))
     assert _ulps32(w.cpu().numpy(), ref.cpu().numpy()).max() <= 2
+
+
+@pytest.mark.gpu
+def test_overlapped_adds_match_in_order_adds():
+    """overlap_adds (the trainer's default: the float32 tree's ring adds on a
+    side stream beside the next acting pass) gives the same tree, max priority
+    and device fill level as in-order adds, after add-only iterations and after
+    a sample + priority update; `total` joins the pending adds itself."""
+    cap = 50_000
+    rbs = [_device_replay(cap), _device_replay(cap)]
+    rbs[1].overlap_adds = True
+    rng = np.random.default_rng(11)
+    for B in (4096, 4096, 4096):
+        for rb in rbs:
+            _adds(rb, B)
+    totals = [float(rb.total) for rb in rbs]
+    assert totals[0] == totals[1]
+    rbs[1].sync_adds()
+    for a, b in ((rbs[0].tree, rbs[1].tree), (rbs[0].max_priority, rbs[1].max_priority),
+                 (rbs[0].size_t, rbs[1].size_t)):
+        assert torch.equal(a, b)
+    for _ in range(2):
+        for rb in rbs:
+            _adds(rb, 1000)
+        u = torch.tensor(rng.random(256), device="cuda")
+        td = torch.tensor((rng.standard_normal(256) * 3).astype(np.float32), device="cuda")
+        s = [rb.sample(256, u=u) for rb in rbs]
+        assert torch.equal(s[0].idx, s[1].idx) and torch.equal(s[0].weights, s[1].weights)
+        for rb, sm in zip(rbs, s):
+            rb.update_priorities(sm.idx, td)
+    rbs[1].sync_adds()
+    torch.cuda.synchronize()
+    assert torch.equal(rbs[0].tree, rbs[1].tree) and torch.equal(rbs[0].max_priority, rbs[1].max_priority)
+    assert torch.equal(rbs[0].size_t, rbs[1].size_t)

@@ -82,31 +82,10 @@ for s in "$@"; do
         act) step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
         upd) step upd 300 rocprofv3 --kernel-trace --stats -d gpurun_out/upd -o run --output-format csv -- python3 tools/agent_profile.py 4096 update ;;
         overlap) step overlap 300 python tools/overlap_probe.py 4096 ;;
-        updrace) TRX_RACE_REC=0 step upd_race_norec 300 python tools/update_graph_race.py 30 default &&
-                 step upd_race 300 python tools/update_graph_race.py 30 default &&
-                 step upd_race_fwd 300 python tools/update_graph_race.py 30 fwdserial &&
-                 step upd_race_nopatch 300 python tools/update_graph_race.py 30 nopatch ;;
-        graphrace) step graph_race 200 python tools/graph_branch_race.py ;;
         ehab) step eh_cs_a 200 env TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_old.so python tools/act_checksum.py 4096 &&
               step eh_cs_b 200 python tools/act_checksum.py 4096 &&
               TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_old.so step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act &&
               step act 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
-        layerrace5) TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race6_fences 300 python tools/layer_concurrency_race.py 6 20 train &&
-                    TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_fences.so step layer_race3_fences 300 python tools/layer_concurrency_race.py 3 20 train ;;
-        layerrace4) GPU_MAX_HW_QUEUES=8 step layer_race6_q8 300 python tools/layer_concurrency_race.py 6 20 train &&
-                    GPU_MAX_HW_QUEUES=16 step layer_race6_q16 300 python tools/layer_concurrency_race.py 6 20 train &&
-                    GPU_MAX_HW_QUEUES=2 step layer_race6_q2 300 python tools/layer_concurrency_race.py 6 20 train ;;
-        layerrace3) step layer_race2 300 python tools/layer_concurrency_race.py 2 20 train &&
-                    step layer_race3 300 python tools/layer_concurrency_race.py 3 20 train &&
-                    TRX_RACE_CHAIN=1 step layer_race6_chain 300 python tools/layer_concurrency_race.py 6 20 train ;;
-        layerrace2) TRX_RACE_HOLD=1 step layer_race6_hold 300 python tools/layer_concurrency_race.py 6 20 train &&
-                    TRX_LIB=$PWD/sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_ldsclear.so step layer_race6_ldsclear 300 python tools/layer_concurrency_race.py 6 20 train ;;
-        layerrace) step layer_race6 300 python tools/layer_concurrency_race.py 6 20 train &&
-                   step layer_race1 300 python tools/layer_concurrency_race.py 1 20 train &&
-                   step layer_race6n 300 python tools/layer_concurrency_race.py 6 20 next ;;
-        trxchain) step trx_chain 300 python tools/trx_chain_race.py ;;
-        gemmcons) step gemm_cons 300 python tools/gemm_consumer_race.py ;;
-        gemmrace) step gemm_race 200 python tools/gemm_stream_race.py ;;
         updactor) TRX_FP32_ACTOR=0 step upd_bf16actor 300 python tools/agent_profile.py 4096 update &&
                   TRX_FP32_ACTOR=1 step upd_fp32actor 300 python tools/agent_profile.py 4096 update ;;
         updstreams) TRX_UPD_STREAMS=2 step upd_s2 300 python tools/agent_profile.py 4096 update &&
