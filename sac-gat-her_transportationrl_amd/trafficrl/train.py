@@ -400,6 +400,7 @@ class Trainer:
         self._done32 = torch.zeros(B, dtype=torch.float32, device=self.device)
         self._finished = torch.zeros(B, dtype=torch.uint8, device=self.device)
         self.episodes_done = 0
+        self.updates_done = 0
         self.history = []
         self.last_losses: Dict = {}
         self._u = torch.empty(bs, dtype=torch.float64, device=self.device)      # PER draws
@@ -451,6 +452,7 @@ class Trainer:
             out = self._update_once(*self._draw_update_randoms())
         fused.weights_changed()   # a graph replay changes parameters without bumping their versions
         self.last_losses = out
+        self.updates_done += 1
         return out
 
     def _draw_update_randoms(self):

@@ -1,7 +1,10 @@
 """Worker for tests/test_dist_gpu.py: one rank of a data-parallel Trainer run
 on a shared GPU over gloo (TRX_DIST_BACKEND rehearsal of the RCCL path), or a
 single rank over nccl (RCCL) itself.  TRX_WORKER_HIDDEN sets hidden = embed
-(32: the autograd update path; 256: the fused update and its flat buffer).
+(32: the autograd update path; 256: the fused update and its flat buffer);
+TRX_WORKER_UNIT / TRX_WORKER_EVERY set update_unit / update_every
+("transitions" with random damage: per-env episode lengths differ, so the
+ranks' due-update counts differ and train.updates_due must deal them out).
 
 Each rank trains `iters` vector iterations with HIP-graph updates (3 eager
 warm-ups, then the update captured as two graphs around the eager gradient
@@ -32,7 +35,8 @@ def main():
     from trafficrl.train import Trainer, sf_config
     cfg = sf_config()
     cfg.update(num_envs=64, batch_start=64, batch_size=32, hidden_dim=hid, embed_dim=hid, eval_every=0,
-               output_dir=os.path.join(out, f"run{rank}"), update_every=1, update_unit="iterations",
+               output_dir=os.path.join(out, f"run{rank}"), update_every=int(os.environ.get("TRX_WORKER_EVERY", "1")),
+               update_unit=os.environ.get("TRX_WORKER_UNIT", "iterations"),
                her_ratio=0.5, assignment_method=method, assignment_iters=10, fixed_damage=False,
                early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0)
     tr = Trainer(cfg, device="cuda:0", rank=rank, world=world if sync else 1, log=False)
@@ -53,7 +57,8 @@ def main():
     sd = {f"{m}.{k}": v.detach().cpu() for m in ("actor", "critic1", "critic2", "target1", "target2")
           for k, v in getattr(tr.agent, m).state_dict().items()}
     sd["log_alpha"] = tr.agent.log_alpha.detach().cpu()
-    torch.save({"params": sd, "episodes": tr.episodes_done, "history": len(hist),
+    torch.save({"params": sd, "episodes": tr.episodes_done, "history": len(hist), "updates": tr.updates_done,
+                "transitions": tr._transitions,
                 "graphed": tr._graphed is not None and tr._graphed.g_grads is not None,
                 "split": tr._graphed is not None and tr._graphed.g_apply is not None,
                 "reduce_calls": dict(tr.agent.grad_sync.calls) if tr.agent.grad_sync is not None else None,

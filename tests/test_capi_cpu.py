@@ -279,3 +279,23 @@ def test_no_packed_fp32_instructions(tmp_path):
         if n:
             hits[k] = n
     assert not hits, f"packed-FP32 instructions in code objects {hits}"
+
+
+def test_integration_snippet_matches_abi():
+    """INTEGRATION.md §2's reference-side ctypes binding stays in step with the
+    header: its ABI assertion is the library's version and its TrxParams /
+    TrxState fields have the layouts of trafficrl._lib's (checked against the
+    header by test_struct_layout_matches_header)."""
+    import ctypes as C
+    from trafficrl import _lib
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = re.search(r"trx_abi_version\(\) == (\d+)", doc)
+    assert m and int(m.group(1)) == _lib.ABI_VERSION == ctypes.CDLL(LIB).trx_abi_version()
+    code = doc[doc.index("class TrxParams"):doc.index("g = ctypes.c_void_p()")]
+    ns = {"ctypes": C}
+    exec(code, ns)   # the two Structure definitions of the snippet
+    for name, ref in (("TrxParams", _lib.TrxParams), ("TrxState", _lib.TrxState)):
+        mine = ns[name]
+        assert C.sizeof(mine) == C.sizeof(ref), name
+        assert [(f[0], getattr(mine, f[0]).offset) for f in mine._fields_ if not f[0].startswith("_")] == \
+               [(f[0], getattr(ref, f[0]).offset) for f in ref._fields_ if not f[0].startswith("_")], name

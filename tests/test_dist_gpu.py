@@ -67,6 +67,21 @@ def test_two_ranks_stay_identical_with_graphed_updates(tmp_path):
     assert moved > 0
 
 
+def test_two_ranks_transition_schedule_random_damage(tmp_path):
+    """update_unit "transitions" (the reference's per-env schedule, update_every
+    4) with random damage: the ranks' envs finish episodes at different steps,
+    so their due-update counts differ every iteration; train.updates_due sums
+    them over the ranks and deals them out evenly, so both ranks run the same
+    number of updates (each one all-reduces) and end bit-identical."""
+    extra = {"TRX_WORKER_UNIT": "transitions", "TRX_WORKER_EVERY": "4"}
+    res = _run(tmp_path, sync=True, iters=14, extra=extra)
+    assert res[0]["updates"] == res[1]["updates"] > 20, (res[0]["updates"], res[1]["updates"])
+    assert all(r["graphed"] and r["split"] for r in res)
+    for k in res[0]["params"]:
+        assert torch.equal(res[0]["params"][k], res[1]["params"][k]), k
+    assert res[0]["episodes"] == res[1]["episodes"]
+
+
 def test_two_ranks_diverge_without_allreduce(tmp_path):
     res = _run(tmp_path, sync=False, iters=8)
     p0, p1 = res[0]["params"], res[1]["params"]
@@ -79,9 +94,7 @@ def test_rccl_single_rank_flat_all_reduce(tmp_path):
     reduced in place in the flat buffer by RCCL (GradAllReduce's flat path,
     never the bucket) between the two captured update graphs; a final reduce
     of the last flat buffer hands every value back unchanged (one rank: the
-    identity).  Runs are not compared bit for bit with a run without the
-    reduce: training is not bitwise reproducible across processes (measured:
-    two identical runs ~3e-4 apart in parameters after 10 iterations)."""
+    identity)."""
     extra = {"TRX_DIST_BACKEND": "nccl", "TRX_WORKER_HIDDEN": "256"}
     a = _run(tmp_path, sync=True, iters=10, world=1, extra=extra)[0]
     assert a["graphed"] and a["split"], (a["graphed"], a["split"])
