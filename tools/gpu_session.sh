@@ -109,6 +109,7 @@ for s in "$@"; do
                python tools/upd_timeline.py report $(ls gpurun_out/updtl/*/run_kernel_trace.csv gpurun_out/updtl/run_kernel_trace.csv 2>/dev/null | head -1) > gpurun_out/updtl_report.txt 2>&1 ;;
         disttests) step dist_tests 600 python -u -m pytest tests/test_dist_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         dist2) step bench_dist2 600 env TRX_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 44 --warmup 22 --no-cpu ;;
+        branchprobe) step branch_probe3 300 python tools/branch_probe.py 3 && step branch_probe6 300 python tools/branch_probe.py 6 ;;
         updt) step upd_time 300 python tools/upd_time.py ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
