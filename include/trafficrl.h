@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 10  /* 10: `exact` (float32) mode of the fused forward/backward kernels;
+#define TRX_ABI_VERSION 11  /* 11: *_multi entry points (several networks' passes per launch);
+                                 10: `exact` (float32) mode of the fused forward/backward kernels;
                                   9: fp32 edge scorer after its p GEMM; trx_gat_layer0_* */
 
 /* error codes */
@@ -250,6 +251,15 @@ typedef struct trx_gat_layer_args {
                                    <= 1024); 0 = the bf16-autocast rounding points above */
 } trx_gat_layer_args;
 int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream);
+/* ABI 11: the same layer for `count` (1..TRX_MAX_NETS) networks in ONE launch
+ * (workgroup (g, k) = graph g of network k): a[k] are complete argument
+ * blocks that must agree in num_graphs, nodes_per_graph, heads, channels,
+ * max_graph_edges, in_dim, exact and the presence of pool; every buffer is
+ * per network.  Results equal `count` separate trx_gat_layer_infer calls --
+ * the SAC update evaluates its same-shaped networks (the next-state actor and
+ * target critics, the two critics) this way. */
+#define TRX_MAX_NETS 6
+int trx_gat_layer_infer_multi(const trx_gat_layer_args* a, int32_t count, void* stream);
 
 /* Layer 0 of GATEncoder for inference (no saved intermediates), in its linear
  * form (gat_layer0.hip): 4 raw features per node, heads*channels = 256, 512 or
@@ -352,6 +362,9 @@ typedef struct trx_edge_head_args {
     int32_t exact;              /* ABI 10: 1 = p is float [N, 2*hidden] (and the backward's grad_p float) */
 } trx_edge_head_args;
 int trx_edge_head_infer(const trx_edge_head_args* a, void* stream);
+/* ABI 11: `count` networks in one launch (same num_graphs, edges_per_graph,
+ * nodes_per_graph, hidden, edge_dim, exact, softmax and draw). */
+int trx_edge_head_infer_multi(const trx_edge_head_args* a, int32_t count, void* stream);
 
 /* Fused tail of the Actor/Critic inference pass (ABI 8): the last GATConv of
  * GATEncoder (src/models/gat_encoder.py:22-25, 47-53: heads 1, concat False,
@@ -412,6 +425,19 @@ int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream);
  * _EdgeHead.edge_scores). */
 int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
                            void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea, void* stream);
+/* ABI 11: trx_edge_head_backward for `count` networks in one launch; io[k]
+ * holds network k's gradient buffers (the arguments of the single call). */
+typedef struct trx_edge_head_bwd_io {
+    const float* grad_logits;
+    void* grad_p;
+    float* grad_c;
+    void* grad_z;
+    float* grad_w2_part;
+    float* grad_we_part;
+    float* grad_ea;
+} trx_edge_head_bwd_io;
+int trx_edge_head_backward_multi(const trx_edge_head_args* a, const trx_edge_head_bwd_io* io, int32_t count,
+                                 void* stream);
 
 /* Input stage of Actor/Critic (src/rl/sac.py:36-37) plus every layer's edge
  * attention logits (src/models/gat_encoder.py:36-52: PyG GATConv with
@@ -452,6 +478,8 @@ typedef struct trx_gat_prologue_args {
     int32_t exact;              /* ABI 10: 1 = M rows, link / loop features and a_edge unrounded (fp32) */
 } trx_gat_prologue_args;
 int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream);
+/* ABI 11: `count` networks in one launch (same sizes, layer shapes and exact). */
+int trx_gat_prologue_infer_multi(const trx_gat_prologue_args* a, int32_t count, void* stream);
 
 /* ------------------------------------------ fused SAC-update backward
  * The SAC update (src/rl/sac.py:157-243) runs its training forwards through
@@ -509,6 +537,9 @@ typedef struct trx_gat_layer_bwd_args {
                                    is read from global memory, layer 0 recomputes it) */
 } trx_gat_layer_bwd_args;
 int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream);
+/* ABI 11: `count` networks in one launch (same sizes, in_dim, residual,
+ * activation, exact and pooling). */
+int trx_gat_layer_backward_multi(const trx_gat_layer_bwd_args* a, int32_t count, void* stream);
 int64_t trx_gat_layer_backward_part_floats(int32_t heads, int32_t channels, int32_t in_dim);
 /* out[k] = sum over r < rows (ascending) of part[r * stride + k], k < width. */
 int trx_partial_sum(const float* part, int32_t rows, int32_t width, int64_t stride, float* out, void* stream);
@@ -556,6 +587,8 @@ typedef struct trx_gat_prologue_bwd_args {
     int32_t exact;              /* ABI 10: backward of the exact prologue (no bf16 rounding) */
 } trx_gat_prologue_bwd_args;
 int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream);
+/* ABI 11: `count` networks in one launch (same sizes and exact). */
+int trx_gat_prologue_backward_multi(const trx_gat_prologue_bwd_args* a, int32_t count, void* stream);
 /* Backward of every layer's edge-attention rows M (trx_gat_prologue_infer's
  * M_l[h, :] = sum_c lin_edge_l.weight[h*C + c, :] * att_edge_l[h, c]; PyG
  * GATConv's lin_edge + att_edge, src/models/gat_encoder.py:22-25) from
@@ -774,7 +807,7 @@ int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, con
  * the remainder x - bf16(x), the low half of a two-term split x ~ hi + lo).
  * Used to prepare the small weight blocks of the fused inference passes and
  * the split operands of the update's three-product float32 GEMMs.          */
-#define TRX_MAX_ROUND 16
+#define TRX_MAX_ROUND 48  /* ABI 11: 48 (was 16): every weight block of five networks in one launch */
 typedef struct trx_round_list {
     int32_t count;
     int32_t out_bf16[TRX_MAX_ROUND];

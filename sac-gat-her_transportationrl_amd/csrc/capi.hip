@@ -714,7 +714,19 @@ int trx_gat_layer0_prepare(int32_t heads, int32_t channels, const float* w0, con
     return TRX_OK;
 }
 
-int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream) {
+// networks of one *_multi launch: same sizes, shapes and mode (their buffers differ)
+static bool same_shape(const trx_gat_layer_args& x, const trx_gat_layer_args& y) {
+    return x.num_graphs == y.num_graphs &&
+           x.nodes_per_graph == y.nodes_per_graph &&
+           x.heads == y.heads &&
+           x.channels == y.channels &&
+           x.max_graph_edges == y.max_graph_edges &&
+           x.in_dim == y.in_dim &&
+           x.exact == y.exact &&
+           (x.pool != nullptr) == (y.pool != nullptr);
+}
+
+static int check_gat_layer_infer(const trx_gat_layer_args* a) {
     if (!a) return fail(TRX_EINVAL, "gat_layer_infer: NULL args");
     const int HC = a->heads * a->channels;
     if (a->num_graphs < 0) return fail(TRX_EINVAL, "gat_layer_infer: num_graphs < 0");
@@ -740,10 +752,28 @@ int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream) {
     if (a->activation != 0 && a->activation != 1) return fail(TRX_EINVAL, "gat_layer_infer: activation 0|1");
     if (!a->out_f32 && !a->out_bf16 && !a->pool) return fail(TRX_EINVAL, "gat_layer_infer: no output");
     if (trx::gat_layer_infer_smem(*a) > 160 * 1024) return fail(TRX_EUNSUP, "gat_layer_infer: LDS > 160 KB");
+    return TRX_OK;
+}
+
+int trx_gat_layer_infer_multi(const trx_gat_layer_args* a, int32_t count, void* stream) {
+    if (!a || count < 1 || count > TRX_MAX_NETS)
+        return fail(TRX_EINVAL, "gat_layer_infer_multi: 1..%d networks", TRX_MAX_NETS);
+    for (int k = 0; k < count; ++k) {
+        const int rc = check_gat_layer_infer(a + k);
+        if (rc != TRX_OK) return rc;
+        const trx_gat_layer_args& b = a[k];
+        if (!same_shape(b, *a))
+            return fail(TRX_EINVAL, "gat_layer_infer_multi: network %d differs from network 0 in shape or mode", k);
+    }
     if (a->num_graphs == 0) return TRX_OK;
-    hipError_t e = trx::launch_gat_layer_infer(*a, static_cast<hipStream_t>(stream));
+    hipError_t e = trx::launch_gat_layer_infer(a, count, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "gat_layer_infer launch: %s", hipGetErrorString(e));
     return TRX_OK;
+}
+
+int trx_gat_layer_infer(const trx_gat_layer_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_layer_infer: NULL args");
+    return trx_gat_layer_infer_multi(a, 1, stream);
 }
 
 int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream) {
@@ -775,7 +805,19 @@ int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream) {
     return TRX_OK;
 }
 
-int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
+// networks of one *_multi launch: same sizes, shapes and mode (their buffers differ)
+static bool same_shape(const trx_edge_head_args& x, const trx_edge_head_args& y) {
+    return x.num_graphs == y.num_graphs &&
+           x.edges_per_graph == y.edges_per_graph &&
+           x.nodes_per_graph == y.nodes_per_graph &&
+           x.hidden == y.hidden &&
+           x.edge_dim == y.edge_dim &&
+           x.exact == y.exact &&
+           x.softmax == y.softmax &&
+           (x.u != nullptr) == (y.u != nullptr);
+}
+
+static int check_edge_head_infer(const trx_edge_head_args* a) {
     if (!a) return fail(TRX_EINVAL, "edge_head_infer: NULL args");
     if (a->num_graphs < 0 || a->edges_per_graph < 1 || a->edges_per_graph > 4096)
         return fail(TRX_EUNSUP, "edge_head_infer: edges_per_graph must be 1..4096");
@@ -791,32 +833,91 @@ int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
     if (!a->src || !a->dst || !a->p || !a->c || !a->ea || !a->we || !a->w2 || !a->b2 || !a->out || (a->softmax && !a->mask))
         return fail(TRX_EINVAL, "edge_head_infer: NULL buffer");
     if (a->u && (!a->softmax || !a->action)) return fail(TRX_EINVAL, "edge_head_infer: u needs softmax and action");
+    return TRX_OK;
+}
+
+int trx_edge_head_infer_multi(const trx_edge_head_args* a, int32_t count, void* stream) {
+    if (!a || count < 1 || count > TRX_MAX_NETS)
+        return fail(TRX_EINVAL, "edge_head_infer_multi: 1..%d networks", TRX_MAX_NETS);
+    for (int k = 0; k < count; ++k) {
+        const int rc = check_edge_head_infer(a + k);
+        if (rc != TRX_OK) return rc;
+        const trx_edge_head_args& b = a[k];
+        if (!same_shape(b, *a))
+            return fail(TRX_EINVAL, "edge_head_infer_multi: network %d differs from network 0 in shape or mode", k);
+    }
     if (a->num_graphs == 0) return TRX_OK;
-    hipError_t e = trx::launch_edge_head_infer(*a, static_cast<hipStream_t>(stream));
+    hipError_t e = trx::launch_edge_head_infer(a, count, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "edge_head_infer launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
 
-int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
-                           void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea, void* stream) {
-    if (!a) return fail(TRX_EINVAL, "edge_head_backward: NULL args");
+int trx_edge_head_infer(const trx_edge_head_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "edge_head_infer: NULL args");
+    return trx_edge_head_infer_multi(a, 1, stream);
+}
+
+static int check_edge_head_backward(const trx_edge_head_args* a, const trx_edge_head_bwd_io* io) {
+    if (!a || !io) return fail(TRX_EINVAL, "edge_head_backward: NULL args");
     if (a->num_graphs < 0 || a->edges_per_graph < 1 || a->edges_per_graph > 4096)
         return fail(TRX_EUNSUP, "edge_head_backward: edges_per_graph must be 1..4096");
     if (a->hidden < 1 || a->hidden > 256 || a->hidden % 4 || a->edge_dim < 1 || a->edge_dim > 8)
         return fail(TRX_EUNSUP, "edge_head_backward: hidden 4..256 (multiple of 4), edge_dim 1..8");
     if (a->nodes_per_graph < 1 || trx::edge_head_bwd_smem(*a) > 160 * 1024)
         return fail(TRX_EUNSUP, "edge_head_backward: graph too large for LDS (nodes_per_graph, edges_per_graph)");
-    if (!a->src || !a->dst || !a->p || !a->c || !a->ea || !a->we || !a->w2 || !grad_logits || !grad_p || !grad_c ||
-        !grad_w2_part || !grad_we_part || !grad_ea)
+    if (!a->src || !a->dst || !a->p || !a->c || !a->ea || !a->we || !a->w2 || !io->grad_logits || !io->grad_p ||
+        !io->grad_c || !io->grad_w2_part || !io->grad_we_part || !io->grad_ea)
         return fail(TRX_EINVAL, "edge_head_backward: NULL buffer");
+    return TRX_OK;
+}
+
+int trx_edge_head_backward_multi(const trx_edge_head_args* a, const trx_edge_head_bwd_io* io, int32_t count,
+                                 void* stream) {
+    if (!a || !io || count < 1 || count > TRX_MAX_NETS)
+        return fail(TRX_EINVAL, "edge_head_backward_multi: 1..%d networks", TRX_MAX_NETS);
+    trx::EdgeHeadBwdItem items[TRX_MAX_NETS];
+    for (int k = 0; k < count; ++k) {
+        const int rc = check_edge_head_backward(a + k, io + k);
+        if (rc != TRX_OK) return rc;
+        const trx_edge_head_args& b = a[k];
+        if (!(b.num_graphs == a->num_graphs && b.edges_per_graph == a->edges_per_graph &&
+              b.nodes_per_graph == a->nodes_per_graph && b.hidden == a->hidden && b.edge_dim == a->edge_dim &&
+              b.exact == a->exact))
+            return fail(TRX_EINVAL, "edge_head_backward_multi: network %d differs from network 0 in shape or mode", k);
+        items[k].a = a[k];
+        items[k].io = io[k];
+    }
     if (a->num_graphs == 0) return TRX_OK;
-    hipError_t e = trx::launch_edge_head_bwd(*a, grad_logits, grad_p, grad_c, grad_z, grad_w2_part, grad_we_part,
-                                             grad_ea, static_cast<hipStream_t>(stream));
+    hipError_t e = trx::launch_edge_head_bwd(items, count, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "edge_head_backward launch: %s", hipGetErrorString(e));
     return TRX_OK;
 }
 
-int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream) {
+int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
+                           void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea, void* stream) {
+    const trx_edge_head_bwd_io io{grad_logits, grad_p, grad_c, grad_z, grad_w2_part, grad_we_part, grad_ea};
+    return trx_edge_head_backward_multi(a, &io, 1, stream);
+}
+
+static bool same_heads(const trx_gat_prologue_args& x, const trx_gat_prologue_args& y) {
+    for (int l = 0; l < x.num_layers && l < TRX_MAX_GAT_LAYERS; ++l)
+        if (x.heads[l] != y.heads[l] || x.channels[l] != y.channels[l]) return false;
+    return true;
+}
+
+// networks of one *_multi launch: same sizes, shapes and mode (their buffers differ)
+static bool same_shape(const trx_gat_prologue_args& x, const trx_gat_prologue_args& y) {
+    return x.num_graphs == y.num_graphs &&
+           x.nodes_per_graph == y.nodes_per_graph &&
+           x.edges_per_graph == y.edges_per_graph &&
+           x.node_dim == y.node_dim &&
+           x.edge_dim == y.edge_dim &&
+           x.num_layers == y.num_layers &&
+           x.exact == y.exact &&
+           same_heads(x, y);
+}
+
+static int check_gat_prologue_infer(const trx_gat_prologue_args* a) {
     if (!a) return fail(TRX_EINVAL, "gat_prologue_infer: NULL args");
     if (a->num_graphs < 0) return fail(TRX_EINVAL, "gat_prologue_infer: num_graphs < 0");
     if (a->nodes_per_graph < 1 || a->nodes_per_graph > 64 || a->edges_per_graph < 0 || a->edges_per_graph > 1024)
@@ -835,10 +936,28 @@ int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream) {
     if (!a->node_x || !a->edge_x || !a->node_ln_w || !a->node_ln_b || !a->edge_ln_w || !a->edge_ln_b || !a->src ||
         !a->dst || !a->rowptr || !a->pos_src || !a->m_work || !a->x0 || !a->ea || !a->a_edge)
         return fail(TRX_EINVAL, "gat_prologue_infer: NULL buffer");
+    return TRX_OK;
+}
+
+int trx_gat_prologue_infer_multi(const trx_gat_prologue_args* a, int32_t count, void* stream) {
+    if (!a || count < 1 || count > TRX_MAX_NETS)
+        return fail(TRX_EINVAL, "gat_prologue_infer_multi: 1..%d networks", TRX_MAX_NETS);
+    for (int k = 0; k < count; ++k) {
+        const int rc = check_gat_prologue_infer(a + k);
+        if (rc != TRX_OK) return rc;
+        const trx_gat_prologue_args& b = a[k];
+        if (!same_shape(b, *a))
+            return fail(TRX_EINVAL, "gat_prologue_infer_multi: network %d differs from network 0 in shape or mode", k);
+    }
     if (a->num_graphs == 0) return TRX_OK;
-    hipError_t e = trx::launch_gat_prologue(*a, static_cast<hipStream_t>(stream));
+    hipError_t e = trx::launch_gat_prologue(a, count, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "gat_prologue_infer launch: %s", hipGetErrorString(e));
     return TRX_OK;
+}
+
+int trx_gat_prologue_infer(const trx_gat_prologue_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_prologue_infer: NULL args");
+    return trx_gat_prologue_infer_multi(a, 1, stream);
 }
 
 int trx_layer_tail_forward(int32_t N, int32_t F, int32_t act, int32_t res_dtype, const float* out, const float* bias,
@@ -957,7 +1076,7 @@ int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, con
 }
 
 int trx_bf16_round(const trx_round_list* l, void* stream) {
-    if (!l || l->count < 0 || l->count > TRX_MAX_ROUND) return fail(TRX_EINVAL, "bf16_round: count must be 0..16");
+    if (!l || l->count < 0 || l->count > TRX_MAX_ROUND) return fail(TRX_EINVAL, "bf16_round: count must be 0..%d", TRX_MAX_ROUND);
     for (int k = 0; k < l->count; ++k)
         if (!l->src[k] || !l->dst[k] || l->rows[k] < 0 || l->cols[k] < 0 || l->src_stride[k] < l->cols[k] ||
             l->out_bf16[k] < 0 || l->out_bf16[k] > 3 || (l->dst_stride[k] != 0 && l->dst_stride[k] < l->cols[k]))
@@ -1009,7 +1128,21 @@ int64_t trx_gat_layer_backward_part_floats(int32_t heads, int32_t channels, int3
     return (int64_t)heads * channels * (in_dim > 0 ? 14 : 5);
 }
 
-int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream) {
+// networks of one *_multi launch: same sizes, shapes and mode (their buffers differ)
+static bool same_shape(const trx_gat_layer_bwd_args& x, const trx_gat_layer_bwd_args& y) {
+    return x.num_graphs == y.num_graphs &&
+           x.nodes_per_graph == y.nodes_per_graph &&
+           x.heads == y.heads &&
+           x.channels == y.channels &&
+           x.max_graph_edges == y.max_graph_edges &&
+           x.in_dim == y.in_dim &&
+           x.exact == y.exact &&
+           x.activation == y.activation &&
+           x.residual == y.residual &&
+           (x.g_pool != nullptr) == (y.g_pool != nullptr);
+}
+
+static int check_gat_layer_backward(const trx_gat_layer_bwd_args* a) {
     if (!a) return fail(TRX_EINVAL, "gat_layer_backward: NULL args");
     const int HC = a->heads * a->channels;
     if (a->num_graphs < 0 || a->nodes_per_graph < 1 || a->nodes_per_graph > 32)
@@ -1030,10 +1163,28 @@ int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream) {
     if (a->a_edge_offset < 0 || a->a_edge_stride < a->a_edge_offset + a->heads)
         return fail(TRX_EINVAL, "gat_layer_backward: a_edge stride/offset");
     if (trx::gat_layer_bwd_smem(*a) > 160 * 1024) return fail(TRX_EUNSUP, "gat_layer_backward: LDS > 160 KB");
+    return TRX_OK;
+}
+
+int trx_gat_layer_backward_multi(const trx_gat_layer_bwd_args* a, int32_t count, void* stream) {
+    if (!a || count < 1 || count > TRX_MAX_NETS)
+        return fail(TRX_EINVAL, "gat_layer_backward_multi: 1..%d networks", TRX_MAX_NETS);
+    for (int k = 0; k < count; ++k) {
+        const int rc = check_gat_layer_backward(a + k);
+        if (rc != TRX_OK) return rc;
+        const trx_gat_layer_bwd_args& b = a[k];
+        if (!same_shape(b, *a))
+            return fail(TRX_EINVAL, "gat_layer_backward_multi: network %d differs from network 0 in shape or mode", k);
+    }
     if (a->num_graphs == 0) return TRX_OK;
-    hipError_t e = trx::launch_gat_layer_bwd(*a, static_cast<hipStream_t>(stream));
+    hipError_t e = trx::launch_gat_layer_bwd(a, count, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "gat_layer_backward launch: %s", hipGetErrorString(e));
     return TRX_OK;
+}
+
+int trx_gat_layer_backward(const trx_gat_layer_bwd_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_layer_backward: NULL args");
+    return trx_gat_layer_backward_multi(a, 1, stream);
 }
 
 int trx_partial_sum(const float* part, int32_t rows, int32_t width, int64_t stride, float* out, void* stream) {
@@ -1071,7 +1222,18 @@ int trx_edge_att_weights_backward(const trx_gat_prologue_args* a, const float* g
     return TRX_OK;
 }
 
-int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream) {
+// networks of one *_multi launch: same sizes, shapes and mode (their buffers differ)
+static bool same_shape(const trx_gat_prologue_bwd_args& x, const trx_gat_prologue_bwd_args& y) {
+    return x.num_graphs == y.num_graphs &&
+           x.nodes_per_graph == y.nodes_per_graph &&
+           x.edges_per_graph == y.edges_per_graph &&
+           x.node_dim == y.node_dim &&
+           x.edge_dim == y.edge_dim &&
+           x.A == y.A &&
+           x.exact == y.exact;
+}
+
+static int check_gat_prologue_backward(const trx_gat_prologue_bwd_args* a) {
     if (!a) return fail(TRX_EINVAL, "gat_prologue_backward: NULL args");
     if (a->num_graphs < 0 || a->nodes_per_graph < 1 || a->nodes_per_graph > 64 || a->edges_per_graph < 0 ||
         a->edges_per_graph > 1024 || a->node_dim < 1 || a->node_dim > 8 || a->edge_dim < 1 || a->edge_dim > 8 ||
@@ -1080,10 +1242,28 @@ int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream) 
     if (!a->node_x || !a->edge_x || !a->node_ln_w || !a->node_ln_b || !a->edge_ln_w || !a->edge_ln_b || !a->src ||
         !a->dst || !a->rowptr || !a->pos_src || !a->m_work || !a->g_a_edge || !a->g_x0 || !a->part)
         return fail(TRX_EINVAL, "gat_prologue_backward: NULL buffer");
+    return TRX_OK;
+}
+
+int trx_gat_prologue_backward_multi(const trx_gat_prologue_bwd_args* a, int32_t count, void* stream) {
+    if (!a || count < 1 || count > TRX_MAX_NETS)
+        return fail(TRX_EINVAL, "gat_prologue_backward_multi: 1..%d networks", TRX_MAX_NETS);
+    for (int k = 0; k < count; ++k) {
+        const int rc = check_gat_prologue_backward(a + k);
+        if (rc != TRX_OK) return rc;
+        const trx_gat_prologue_bwd_args& b = a[k];
+        if (!same_shape(b, *a))
+            return fail(TRX_EINVAL, "gat_prologue_backward_multi: network %d differs from network 0 in shape or mode", k);
+    }
     if (a->num_graphs == 0) return TRX_OK;
-    hipError_t e = trx::launch_gat_prologue_bwd(*a, static_cast<hipStream_t>(stream));
+    hipError_t e = trx::launch_gat_prologue_bwd(a, count, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(TRX_EHIP, "gat_prologue_backward launch: %s", hipGetErrorString(e));
     return TRX_OK;
+}
+
+int trx_gat_prologue_backward(const trx_gat_prologue_bwd_args* a, void* stream) {
+    if (!a) return fail(TRX_EINVAL, "gat_prologue_backward: NULL args");
+    return trx_gat_prologue_backward_multi(a, 1, stream);
 }
 
 int trx_sac_loss(const trx_sac_loss_args* a, void* stream) {

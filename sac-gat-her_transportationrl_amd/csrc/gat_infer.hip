@@ -159,8 +159,9 @@ extern "C" int trx_debug_infer_cycles(unsigned long long* out, int reset) {
 // IN: 0 = xh given (layers >= 1), else the layer-0 input width (4).
 // XF: the exact mode -- xh float32 (staged as float rows), no bf16 rounding.
 template <int HC, int IN, int NT, bool XF>
-__global__ void __launch_bounds__(NT) gat_layer_infer_kernel(trx_gat_layer_args a) {
+__global__ void __launch_bounds__(NT) gat_layer_infer_kernel(const NetList<trx_gat_layer_args> nets) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    const trx_gat_layer_args& a = nets.a[blockIdx.y];  // network blockIdx.y (*_multi launches)
     typedef typename XElem<XF>::T XE;
     constexpr int EV = 16 / sizeof(XE);  // row elements per 16-byte piece
     constexpr int kInferThreads = NT, kInferWaves = NT / kWave;  // this instance's workgroup
@@ -553,7 +554,8 @@ constexpr int kEdgeED = 8;  // edge_dim <= 8
 // per-term edge_dim test and no padding terms in the link-feature product), 0 = any
 // edge_dim <= kEdgeED.  The same terms in the same order either way.
 template <int MQ, int DK, bool XF>  // hidden <= 256 * MQ, hidden % 4 == 0; XF: p float (exact mode)
-__global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge_head_args a) {
+__global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(const NetList<trx_edge_head_args> nets) {
+    const trx_edge_head_args& a = nets.a[blockIdx.y];
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename XElem<XF>::T XE;
     constexpr int EV = 16 / sizeof(XE);
@@ -767,7 +769,8 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(trx_edge
 
 // -------------------------------------------------------------- prologue
 // M rows of every layer: one wave per (layer, head, feature), lanes over channels.
-__global__ void __launch_bounds__(kWave) edge_att_weights_kernel(trx_gat_prologue_args a) {
+__global__ void __launch_bounds__(kWave) edge_att_weights_kernel(const NetList<trx_gat_prologue_args> nets) {
+    const trx_gat_prologue_args& a = nets.a[blockIdx.y];
     const int lane = threadIdx.x, D = a.edge_dim;
     int l = 0, oo = blockIdx.x, row0 = 0;
     while (oo >= a.heads[l] * D) {
@@ -811,7 +814,8 @@ __device__ __forceinline__ void layer_norm_row(float (&x)[kProMD], int d, const 
 // row.  NT threads per graph: 128 for the acting pass, 256 for the 256-graph
 // update batches (one workgroup per CU either way has work for every SIMD).
 template <int NT>
-__global__ void __launch_bounds__(NT) gat_prologue_kernel(trx_gat_prologue_args a, int A) {
+__global__ void __launch_bounds__(NT) gat_prologue_kernel(const NetList<trx_gat_prologue_args> nets, int A) {
+    const trx_gat_prologue_args& a = nets.a[blockIdx.y];
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MD = kProMD;
     const int g = blockIdx.x, tid = threadIdx.x;
@@ -892,14 +896,19 @@ size_t gat_prologue_smem(const trx_gat_prologue_args& a) {
             a.edges_per_graph) * 4;
 }
 
-hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t stream) {
+// networks k < count (the same sizes and layer shapes: checked by the C ABI)
+hipError_t launch_gat_prologue(const trx_gat_prologue_args* a, int count, hipStream_t stream) {
+    const trx_gat_prologue_args& a0 = a[0];
+    const NetList<trx_gat_prologue_args> l = net_list(a, count);
     int A = 0;
-    for (int l = 0; l < a.num_layers; ++l) A += a.heads[l];
-    hipLaunchKernelGGL(edge_att_weights_kernel, dim3(A * a.edge_dim), dim3(kWave), 0, stream, a);
-    if (a.num_graphs < 2048)
-        hipLaunchKernelGGL(gat_prologue_kernel<256>, dim3(a.num_graphs), dim3(256), gat_prologue_smem(a), stream, a, A);
+    for (int k = 0; k < a0.num_layers; ++k) A += a0.heads[k];
+    hipLaunchKernelGGL(edge_att_weights_kernel, dim3(A * a0.edge_dim, count), dim3(kWave), 0, stream, l);
+    if (a0.num_graphs * count < 2048)
+        hipLaunchKernelGGL(gat_prologue_kernel<256>, dim3(a0.num_graphs, count), dim3(256), gat_prologue_smem(a0),
+                           stream, l, A);
     else
-        hipLaunchKernelGGL(gat_prologue_kernel<128>, dim3(a.num_graphs), dim3(128), gat_prologue_smem(a), stream, a, A);
+        hipLaunchKernelGGL(gat_prologue_kernel<128>, dim3(a0.num_graphs, count), dim3(128), gat_prologue_smem(a0),
+                           stream, l, A);
     return hipGetLastError();
 }
 
@@ -925,7 +934,9 @@ static void set_lds_attr() {
 // One workgroup per graph.  The acting pass (4096 graphs) fills the CUs with
 // 4-wave workgroups; the SAC update's passes (256 graphs: one workgroup per
 // CU) take 8-wave workgroups, so each CU still has two waves per SIMD.
-hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream) {
+hipError_t launch_gat_layer_infer(const trx_gat_layer_args* al, int count, hipStream_t stream) {
+    const trx_gat_layer_args& a = al[0];
+    const NetList<trx_gat_layer_args> l = net_list(al, count);
     const int HC = a.heads * a.channels;
     const size_t smem = gat_layer_infer_smem(a);
     static bool attr_set = false;
@@ -957,17 +968,17 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
         attr_set = true;
     }
     if (smem > 160 * 1024) return hipErrorInvalidValue;
-    const dim3 grid(a.num_graphs);
+    const dim3 grid(a.num_graphs, count);
 #ifndef TRX_WIDE_GRAPHS
 #define TRX_WIDE_GRAPHS 2048
 #endif
-    const bool wide = a.num_graphs < TRX_WIDE_GRAPHS;
+    const bool wide = a.num_graphs * count < TRX_WIDE_GRAPHS;
 #define TRX_LAYER_CASE(HCV, INV, XFV)                                                                          \
     if (HC == HCV && a.in_dim == INV && (a.exact != 0) == XFV) {                                               \
         if (wide)                                                                                              \
-            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 512, XFV>), grid, dim3(512), smem, stream, a); \
+            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 512, XFV>), grid, dim3(512), smem, stream, l); \
         else                                                                                                   \
-            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 256, XFV>), grid, dim3(256), smem, stream, a); \
+            hipLaunchKernelGGL((gat_layer_infer_kernel<HCV, INV, 256, XFV>), grid, dim3(256), smem, stream, l); \
         return hipGetLastError();                                                                              \
     }
     TRX_LAYER_CASE(1024, 0, false)
@@ -1009,10 +1020,16 @@ hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t strea
 constexpr int kEhbThreads = 1024, kEhbParts = kEhbThreads / 256;
 
 template <bool XF>  // exact mode: p and grad_p float
-__global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(trx_edge_head_args a, const float* grad_logits,
-                                                                    void* grad_p_, float* grad_c,
-                                                                    uint16_t* grad_z, float* grad_w2_part,
-                                                                    float* grad_we_part, float* grad_ea) {
+__global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(const NetList<EdgeHeadBwdItem> nets) {
+    const trx_edge_head_args& a = nets.a[blockIdx.y].a;
+    const trx_edge_head_bwd_io& io = nets.a[blockIdx.y].io;
+    const float* const grad_logits = io.grad_logits;
+    void* const grad_p_ = io.grad_p;
+    float* const grad_c = io.grad_c;
+    uint16_t* const grad_z = static_cast<uint16_t*>(io.grad_z);
+    float* const grad_w2_part = io.grad_w2_part;
+    float* const grad_we_part = io.grad_we_part;
+    float* const grad_ea = io.grad_ea;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename XElem<XF>::T XE;
     constexpr int EV = 16 / sizeof(XE);
@@ -1170,9 +1187,9 @@ size_t edge_head_bwd_smem(const trx_edge_head_args& a) {
            256 * kEdgeED * 4 + 2 * (n + 1) * 4;
 }
 
-hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
-                                void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea,
-                                hipStream_t stream) {
+hipError_t launch_edge_head_bwd(const EdgeHeadBwdItem* items, int count, hipStream_t stream) {
+    const trx_edge_head_args& a = items[0].a;
+    const NetList<EdgeHeadBwdItem> l = net_list(items, count);
     const size_t smem = edge_head_bwd_smem(a);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     const void* fn = a.exact ? reinterpret_cast<const void*>(edge_head_bwd_kernel<true>)
@@ -1182,41 +1199,40 @@ hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_l
         if (e != hipSuccess) return e;
     }
     if (a.exact)
-        hipLaunchKernelGGL(edge_head_bwd_kernel<true>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a,
-                           grad_logits, grad_p, grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part, grad_we_part,
-                           grad_ea);
+        hipLaunchKernelGGL(edge_head_bwd_kernel<true>, dim3(a.num_graphs, count), dim3(kEhbThreads), smem, stream, l);
     else
-        hipLaunchKernelGGL(edge_head_bwd_kernel<false>, dim3(a.num_graphs), dim3(kEhbThreads), smem, stream, a,
-                           grad_logits, grad_p, grad_c, static_cast<uint16_t*>(grad_z), grad_w2_part, grad_we_part,
-                           grad_ea);
+        hipLaunchKernelGGL(edge_head_bwd_kernel<false>, dim3(a.num_graphs, count), dim3(kEhbThreads), smem, stream, l);
     return hipGetLastError();
 }
 
 template <int MQ, int DK, bool XF>
-static hipError_t launch_edge_head_infer_t(const trx_edge_head_args& a, size_t smem, hipStream_t stream) {
+static hipError_t launch_edge_head_infer_t(const trx_edge_head_args* al, int count, size_t smem,
+                                           hipStream_t stream) {
     if (smem > 64 * 1024) {  // opt in to more than 64 KB of dynamic LDS
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(edge_head_infer_kernel<MQ, DK, XF>),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((edge_head_infer_kernel<MQ, DK, XF>), dim3(a.num_graphs), dim3(kInferThreads), smem, stream, a);
+    hipLaunchKernelGGL((edge_head_infer_kernel<MQ, DK, XF>), dim3(al[0].num_graphs, count), dim3(kInferThreads), smem,
+                       stream, net_list(al, count));
     return hipGetLastError();
 }
 
-hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream) {
+hipError_t launch_edge_head_infer(const trx_edge_head_args* al, int count, hipStream_t stream) {
+    const trx_edge_head_args& a = al[0];
     const size_t smem = edge_head_infer_smem(a);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
     const bool d6 = a.edge_dim == 6;  // the networks' link features (repair_env.py:800-808)
     if (a.exact) {
         if (a.hidden > 256) return hipErrorInvalidValue;
-        return d6 ? launch_edge_head_infer_t<1, 6, true>(a, smem, stream)
-                  : launch_edge_head_infer_t<1, 0, true>(a, smem, stream);
+        return d6 ? launch_edge_head_infer_t<1, 6, true>(al, count, smem, stream)
+                  : launch_edge_head_infer_t<1, 0, true>(al, count, smem, stream);
     }
     if (a.hidden <= 256)
-        return d6 ? launch_edge_head_infer_t<1, 6, false>(a, smem, stream)
-                  : launch_edge_head_infer_t<1, 0, false>(a, smem, stream);
-    return d6 ? launch_edge_head_infer_t<2, 6, false>(a, smem, stream)
-              : launch_edge_head_infer_t<2, 0, false>(a, smem, stream);
+        return d6 ? launch_edge_head_infer_t<1, 6, false>(al, count, smem, stream)
+                  : launch_edge_head_infer_t<1, 0, false>(al, count, smem, stream);
+    return d6 ? launch_edge_head_infer_t<2, 6, false>(al, count, smem, stream)
+              : launch_edge_head_infer_t<2, 0, false>(al, count, smem, stream);
 }
 
 }  // namespace trx

@@ -98,7 +98,8 @@ __device__ __forceinline__ float4 st4x(typename XE_<XF>::T* p, float a, float b,
 // bias, [3F,4F) att_src, [4F,5F) att_dst; layer 0 adds [5F,9F) lin.weight (F x 4,
 // row-major), [9F,13F) input_proj.weight, [13F,14F) input_proj.bias.  F = heads*channels.
 template <int HC, int IN, int NT, bool XF>
-__global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(trx_gat_layer_bwd_args a) {
+__global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(const NetList<trx_gat_layer_bwd_args> nets) {
+    const trx_gat_layer_bwd_args& a = nets.a[blockIdx.y];  // network blockIdx.y (*_multi launches)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename XE_<XF>::T XE;
     constexpr int EV = 16 / sizeof(XE);
@@ -529,7 +530,9 @@ static void set_bwd_lds_attr() {
 // One workgroup per graph and ~144 KB of LDS for HC 1024: one workgroup per
 // CU, so the waves per workgroup are the occupancy -- 8 (two per SIMD) where
 // the registers allow it (HC 1024: up to 218 VGPRs), 16 for the narrower layers.
-hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t stream) {
+hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args* al, int count, hipStream_t stream) {
+    const trx_gat_layer_bwd_args& a = al[0];
+    const NetList<trx_gat_layer_bwd_args> l = net_list(al, count);
     static bool attr_set = false;
     if (!attr_set) {
         set_bwd_lds_attr<1024, 0, 512>();
@@ -549,10 +552,10 @@ hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t str
     const int HC = a.heads * a.channels;
     const size_t smem = gat_layer_bwd_smem(a);
     if (smem > 160 * 1024) return hipErrorInvalidValue;
-    const dim3 grid(a.num_graphs);
+    const dim3 grid(a.num_graphs, count);
 #define TRX_BWD_CASE(HCV, INV, NTV, XFV)                                                                 \
     if (HC == HCV && a.in_dim == INV && (a.exact != 0) == XFV) {                                         \
-        hipLaunchKernelGGL((gat_layer_bwd_kernel<HCV, INV, NTV, XFV>), grid, dim3(NTV), smem, stream, a); \
+        hipLaunchKernelGGL((gat_layer_bwd_kernel<HCV, INV, NTV, XFV>), grid, dim3(NTV), smem, stream, l); \
         return hipGetLastError();                                                                        \
     }
     TRX_BWD_CASE(1024, 0, 512, false)
@@ -709,7 +712,8 @@ __device__ __forceinline__ void ln_fwd_row(float (&x)[kPD], int d, const float* 
 
 constexpr int kPBT = 256;  // prologue backward: threads per graph
 
-__global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(trx_gat_prologue_bwd_args a) {
+__global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<trx_gat_prologue_bwd_args> nets) {
+    const trx_gat_prologue_bwd_args& a = nets.a[blockIdx.y];
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MD = kPD, NW = kPBT / kW;
     const int g = blockIdx.x, tid = threadIdx.x, lane = tid & (kW - 1), wave = tid / kW;
@@ -855,8 +859,9 @@ size_t gat_prologue_bwd_smem(const trx_gat_prologue_bwd_args& a) {
             a.nodes_per_graph + a.edges_per_graph) * 4;
 }
 
-hipError_t launch_gat_prologue_bwd(const trx_gat_prologue_bwd_args& a, hipStream_t stream) {
-    hipLaunchKernelGGL(gat_prologue_bwd_kernel, dim3(a.num_graphs), dim3(kPBT), gat_prologue_bwd_smem(a), stream, a);
+hipError_t launch_gat_prologue_bwd(const trx_gat_prologue_bwd_args* a, int count, hipStream_t stream) {
+    hipLaunchKernelGGL(gat_prologue_bwd_kernel, dim3(a[0].num_graphs, count), dim3(kPBT), gat_prologue_bwd_smem(a[0]),
+                       stream, net_list(a, count));
     return hipGetLastError();
 }
 

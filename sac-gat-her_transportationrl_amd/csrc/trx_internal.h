@@ -167,8 +167,24 @@ hipError_t launch_gat_backward(int Nt, int H, int C, const int32_t* rowptr, cons
                                hipStream_t stream);
 
 size_t gat_layer_infer_smem(const trx_gat_layer_args& a);
-hipError_t launch_gat_layer_infer(const trx_gat_layer_args& a, hipStream_t stream);
-hipError_t launch_edge_head_infer(const trx_edge_head_args& a, hipStream_t stream);
+// several networks' passes in one launch (blockIdx.y = network): the argument
+// blocks travel by value in the kernel arguments, indexed by blockIdx.y
+template <class A>
+struct NetList {
+    A a[TRX_MAX_NETS];
+};
+template <class A>
+inline NetList<A> net_list(const A* a, int count) {
+    NetList<A> l{};
+    for (int k = 0; k < count; ++k) l.a[k] = a[k];
+    return l;
+}
+struct EdgeHeadBwdItem {
+    trx_edge_head_args a;
+    trx_edge_head_bwd_io io;
+};
+hipError_t launch_gat_layer_infer(const trx_gat_layer_args* a, int count, hipStream_t stream);
+hipError_t launch_edge_head_infer(const trx_edge_head_args* a, int count, hipStream_t stream);
 size_t gat_layer0_smem(const trx_gat_layer0_args& a);
 hipError_t launch_gat_layer0(const trx_gat_layer0_args& a, hipStream_t stream);
 size_t gat_mid_smem(const trx_gat_mid_args& a);
@@ -180,9 +196,7 @@ size_t gat_tail_smem(const trx_gat_tail_args& a);
 int gat_tail_mtiles(int nodes_per_graph);
 hipError_t launch_gat_tail_infer(const trx_gat_tail_args& a, hipStream_t stream);
 size_t edge_head_bwd_smem(const trx_edge_head_args& a);
-hipError_t launch_edge_head_bwd(const trx_edge_head_args& a, const float* grad_logits, void* grad_p, float* grad_c,
-                                void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea,
-                                hipStream_t stream);
+hipError_t launch_edge_head_bwd(const EdgeHeadBwdItem* items, int count, hipStream_t stream);
 int layer_tail_blocks(int N);
 int att_dots_blocks(int N);
 int small_ln_blocks(int N);
@@ -211,17 +225,17 @@ hipError_t launch_layer_tail_fwd(int N, int F, int act, int res_bf16, const floa
 hipError_t launch_layer_tail_bwd(int N, int F, int act, int res_bf16, const float* gy, const float* out,
                                  const float* bias, const float* w, const float* y, const float* stats, float* gout,
                                  void* gres, float* part, float* grads, hipStream_t stream);
-hipError_t launch_gat_prologue(const trx_gat_prologue_args& a, hipStream_t stream);
+hipError_t launch_gat_prologue(const trx_gat_prologue_args* a, int count, hipStream_t stream);
 size_t gat_prologue_smem(const trx_gat_prologue_args& a);
 hipError_t patch_graph_memsets(hipGraph_t graph, int* n_patched);
 size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a);
-hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args& a, hipStream_t stream);
+hipError_t launch_gat_layer_bwd(const trx_gat_layer_bwd_args* a, int count, hipStream_t stream);
 hipError_t launch_partial_sum(const float* part, int rows, int width, int64_t stride, float* out, hipStream_t stream);
 hipError_t launch_partial_sum_multi(const trx_psum_list& l, hipStream_t stream);
 hipError_t launch_edge_att_weights_bwd(const trx_gat_prologue_args& a, const float* gm, int gm_stride, float* out,
                                        hipStream_t stream);
 size_t gat_prologue_bwd_smem(const trx_gat_prologue_bwd_args& a);
-hipError_t launch_gat_prologue_bwd(const trx_gat_prologue_bwd_args& a, hipStream_t stream);
+hipError_t launch_gat_prologue_bwd(const trx_gat_prologue_bwd_args* a, int count, hipStream_t stream);
 hipError_t launch_sac_loss(const trx_sac_loss_args& a, hipStream_t stream);
 hipError_t launch_sac_adam(const trx_adam_args& a, hipStream_t stream);
 hipError_t launch_per_update(double* tree, int64_t capacity, const int64_t* idx, const double* pri, int n,

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("TRX_LIB") or os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 10
+ABI_VERSION = 11
 SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 
@@ -35,7 +35,10 @@ EXPORTS = (
     "trx_gat_prologue_backward",
     "trx_sac_loss", "trx_sac_adam", "trx_gat_tail_infer", "trx_edge_att_weights_backward",
     "trx_gat_layer0_infer", "trx_gat_layer0_prepare", "trx_gat_mid_infer",
+    "trx_gat_layer_infer_multi", "trx_edge_head_infer_multi", "trx_edge_head_backward_multi",
+    "trx_gat_prologue_infer_multi", "trx_gat_layer_backward_multi", "trx_gat_prologue_backward_multi",
 )
+MAX_NETS = 6   # TRX_MAX_NETS: networks per *_multi launch (ABI 11)
 
 
 class TrxParams(ctypes.Structure):
@@ -213,7 +216,7 @@ class TrxAdamArgs(ctypes.Structure):
     ]
 
 
-MAX_ROUND = 16
+MAX_ROUND = 48
 
 
 class TrxRoundList(ctypes.Structure):
@@ -223,6 +226,11 @@ class TrxRoundList(ctypes.Structure):
         ("cols", ctypes.c_int64 * MAX_ROUND), ("src_stride", ctypes.c_int64 * MAX_ROUND),
         ("src", _vp * MAX_ROUND), ("dst", _vp * MAX_ROUND), ("dst_stride", ctypes.c_int64 * MAX_ROUND),
     ]
+
+
+class TrxEdgeHeadBwdIO(ctypes.Structure):   # trx_edge_head_bwd_io (ABI 11)
+    _fields_ = [(n, _vp) for n in ("grad_logits", "grad_p", "grad_c", "grad_z", "grad_w2_part", "grad_we_part",
+                                   "grad_ea")]
 
 
 MAX_PSUM = 32
@@ -331,6 +339,13 @@ def load():
     L.trx_edge_att_weights_backward.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp, _i32, _vp, _vp]
     L.trx_gat_prologue_infer.argtypes = [ctypes.POINTER(TrxGatPrologueArgs), _vp]
     L.trx_edge_head_backward.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    for name, st in (("trx_gat_layer_infer_multi", TrxGatLayerArgs), ("trx_edge_head_infer_multi", TrxEdgeHeadArgs),
+                     ("trx_gat_prologue_infer_multi", TrxGatPrologueArgs),
+                     ("trx_gat_layer_backward_multi", TrxGatLayerBwdArgs),
+                     ("trx_gat_prologue_backward_multi", TrxGatPrologueBwdArgs)):
+        getattr(L, name).argtypes = [ctypes.POINTER(st), _i32, _vp]
+    L.trx_edge_head_backward_multi.argtypes = [ctypes.POINTER(TrxEdgeHeadArgs), ctypes.POINTER(TrxEdgeHeadBwdIO),
+                                               _i32, _vp]
     L.trx_graph_pool_forward.argtypes = [_i32, _i32, _i32, _vp, _vp, _vp, _vp]
     L.trx_bf16_round.argtypes = [ctypes.POINTER(TrxRoundList), _vp]
     L.trx_multi_copy.argtypes = [ctypes.POINTER(TrxCopyList), _vp]
@@ -386,6 +401,11 @@ def check(rc: int, what: str):
     if rc == TRX_EINVAL:
         raise ValueError(f"{what}: {msg}")
     raise TrafficRLError(f"{what} failed ({rc}): {msg}")
+
+
+def multi(struct_type, items):
+    """A ctypes array of argument blocks for a *_multi entry point."""
+    return (struct_type * len(items))(*items)
 
 
 def ptr(t) -> ctypes.c_void_p:

@@ -131,10 +131,16 @@ _STATIC = [False]
 
 
 def _round_into(pairs):
-    """One trx_bf16_round launch: for each (src float32 2-D/1-D view with unit
-    column stride, dst contiguous float32 or bfloat16 tensor of the same
-    shape[, exact]) write bf16(src) (as bf16 bits, or rounded float32), or with
-    exact=True the float32 value itself (a strided copy)."""
+    """trx_bf16_round launches (one per _lib.MAX_ROUND blocks): for each (src
+    float32 2-D/1-D view with unit column stride, dst contiguous float32 or
+    bfloat16 tensor of the same shape[, exact]) write bf16(src) (as bf16 bits,
+    or rounded float32), or with exact=True the float32 value itself (a
+    strided copy)."""
+    for b0 in range(0, len(pairs), _lib.MAX_ROUND):
+        _round_list(pairs[b0:b0 + _lib.MAX_ROUND])
+
+
+def _round_list(pairs):
     L = _lib.load()
     lst = _lib.TrxRoundList()
     lst.count = len(pairs)
@@ -426,7 +432,20 @@ def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topolog
     wave per graph for the rest).  Returns (x0, ea, a_all), or with keep_m
     ((x0, ea, a_all, M rows), None, None) for the training backward.
     exact: no bf16 rounding of the M rows / link features / edge logits."""
+    a, (x0, ea, a_all, m_work), keep = prologue_args(model, node_x, edge_attr, topo, exact)
     L = _lib.load()
+    _lib.check(L.trx_gat_prologue_infer(a, _lib.stream_ptr(node_x.device)), "trx_gat_prologue_infer")
+    del keep
+    if keep_m:
+        return (x0, ea, a_all, m_work), None, None
+    return x0, ea, a_all
+
+
+def prologue_args(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topology, exact: bool = False):
+    """The trx_gat_prologue_args block of `prologue` with its freshly
+    allocated outputs (x0, ea, a_all, M rows) and the temporaries it points at
+    (`keep`: alive until the launch is enqueued) -- one block per network of a
+    trx_gat_prologue_infer_multi launch."""
     layers = list(model.encoder.layers)
     dev = node_x.device
     nx, ex = node_x.float().contiguous(), edge_attr.float().contiguous()
@@ -436,7 +455,7 @@ def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topolog
     ea = torch.empty(ex.shape[0], ed, device=dev)
     a_all = torch.empty(topo.g.col.numel(), A, device=dev)
     m_work = torch.empty(A, ed, device=dev)
-    keep = [m_work]
+    keep = [m_work, nx, ex]
     a = _lib.TrxGatPrologueArgs()
     a.num_graphs, a.nodes_per_graph, a.edges_per_graph, a.node_dim, a.edge_dim = topo.B, topo.n, topo.e, nd, ed
     a.node_x, a.edge_x = nx.data_ptr(), ex.data_ptr()
@@ -457,11 +476,7 @@ def prologue(model, node_x: torch.Tensor, edge_attr: torch.Tensor, topo: Topolog
         a.lin_edge_w[i], a.att_edge[i] = w.data_ptr(), at.data_ptr()
     a.m_work, a.x0, a.ea, a.a_edge = m_work.data_ptr(), x0.data_ptr(), ea.data_ptr(), a_all.data_ptr()
     a.exact = int(exact)
-    _lib.check(L.trx_gat_prologue_infer(a, _lib.stream_ptr(dev)), "trx_gat_prologue_infer")
-    del keep
-    if keep_m:
-        return (x0, ea, a_all, m_work), None, None
-    return x0, ea, a_all
+    return a, (x0, ea, a_all, m_work), keep
 
 
 def prologue_supported(model) -> bool:

@@ -21,6 +21,7 @@ it against the autograd path and the fp32 restatement.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -78,6 +79,20 @@ class NetCtx:
     p: torch.Tensor
     c: torch.Tensor
     head_w: tuple
+    grp: Optional["NetGroup"] = None   # net_forward_multi: the stacked tensors of the group
+    j: int = 0                         # this network's index in the group
+
+
+@dataclass
+class NetGroup:
+    """The stacked ([k, ...], network-major) tensors of one net_forward_multi
+    call that the GEMMs of net_backward_multi read."""
+    x_in: List[torch.Tensor]   # per layer >= 1: its GEMM input [k, N, in] bf16
+    W: List[torch.Tensor]      # per layer >= 1: its lin weights [k, out, in] bf16
+    emb: torch.Tensor          # [k, N, embed] bf16
+    ctx: torch.Tensor          # [k, B, 2 embed] float32
+    WN: torch.Tensor           # [k, 2 hidden, embed] bf16 edge-MLP node blocks
+    WC: torch.Tensor           # [k, hidden, 2 embed] bf16 edge-MLP context block
 
 
 _MM32 = [None]   # torch.mm(..., out_dtype=torch.float32) available on this build (probe_mm32)
@@ -302,6 +317,372 @@ def net_forward(net, node_x: torch.Tensor, edge_x: torch.Tensor, topo: Topology,
     if not save:
         return logits, None
     return logits, NetCtx(x0, ea, a_all, m_work, node_x, edge_x, recs, emb, ctx, p, c, head_w)
+
+
+# grouped launches in the update: 0 = six branches, one network each (the default: the
+# fastest replay, 2.01 ms per update); 1 = the five bf16 passes in one group beside the
+# float32 actor (two branches, 2.21 ms); 2 = the critics' training passes and the three
+# next-state passes as two groups (three branches, 2.13 ms).  Bit-identical results
+# (tests/test_fused_update.py test_grouped_update_bit_identical); DESIGN §5
+MULTI = int(os.environ.get("TRX_UPD_MULTI", "0"))
+
+
+def _stack_weights(nets):
+    """Every network's weight blocks for the bf16 (non-exact) passes, stacked
+    network-major: layer 0's w0 / wp / bp bf16-rounded float32 [k, ...], the
+    lin weights of layers >= 1 as bf16 [k, out, in], the edge MLP's node and
+    context blocks as bf16 WN [k, 2H, d] / WC [k, H, 2d], its link-feature
+    block, output weight and bias float32 (models/fused.py _encoder_weights
+    and _head_weights, for k networks in trx_bf16_round launches of 48)."""
+    k, dev = len(nets), nets[0].edge_mlp[0].weight.device
+    enc0, head0 = nets[0].encoder, nets[0]
+    l0 = list(enc0.layers)
+    W1 = head0.edge_mlp[0].weight
+    d, K, hid = head0.embed, head0.edge_in, W1.shape[0]
+    bf = torch.bfloat16
+    w0 = torch.empty((k,) + tuple(l0[0].lin.weight.shape), device=dev)
+    wp = torch.empty((k,) + tuple(enc0.input_proj.weight.shape), device=dev)
+    bp = torch.empty((k,) + tuple(enc0.input_proj.bias.shape), device=dev)
+    W = [torch.empty((k,) + tuple(l.lin.weight.shape), device=dev, dtype=bf) for l in l0[1:]]
+    WN = torch.empty(k, 2 * hid, d, device=dev, dtype=bf)
+    WC = torch.empty(k, hid, W1.shape[1] - 2 * d - K, device=dev, dtype=bf)
+    WE = torch.empty(k, hid, K, device=dev)
+    W2 = torch.empty(k, hid, device=dev)
+    B2 = torch.empty(k, 1, device=dev)
+    pairs = []
+    for j, net in enumerate(nets):
+        enc = net.encoder
+        ls = list(enc.layers)
+        pairs += [(ls[0].lin.weight, w0[j]), (enc.input_proj.weight, wp[j]), (enc.input_proj.bias, bp[j])]
+        pairs += [(l.lin.weight, Wl[j]) for l, Wl in zip(ls[1:], W)]
+        W1 = net.edge_mlp[0].weight
+        pairs += [(W1[:, :d], WN[j, :hid]), (W1[:, d:2 * d], WN[j, hid:]), (W1[:, 2 * d + K:], WC[j]),
+                  (W1[:, 2 * d:2 * d + K], WE[j], True), (net.edge_mlp[2].weight.reshape(-1), W2[j], True),
+                  (net.edge_mlp[2].bias.reshape(-1), B2[j], True)]
+    fused._round_into(pairs)
+    return w0, wp, bp, W, WN, WC, WE, W2, B2
+
+
+def multi_supported(nets) -> bool:
+    """Networks whose passes can share launches: identical layer / head shapes."""
+    def sig(net):
+        return ([(l.heads, l.out_channels, l.concat, tuple(l.lin.weight.shape)) for l in net.encoder.layers],
+                tuple(net.edge_mlp[0].weight.shape), net.embed, net.edge_in)
+    return len(nets) <= _lib.MAX_NETS and all(sig(n) == sig(nets[0]) for n in nets)
+
+
+def net_forward_multi(specs, topo: Topology):
+    """net_forward (bf16 mode) for several networks of the same shapes in
+    shared launches: specs = [(net, node_x, edge_x, save, mask)], each with its
+    own inputs, weights and outputs.  One trx_*_multi launch per kernel (the
+    network index in blockIdx.y), the lin / edge-head GEMMs per network as
+    net_forward issues them, the edge scorer once per softmax kind.  Same kernels,
+    arithmetic and rounding points per network as net_forward; returns
+    [(logits, NetCtx | None)] in spec order (the contexts share one NetGroup)."""
+    L = _lib.load()
+    k = len(specs)
+    nets = [sp[0] for sp in specs]
+    dev = specs[0][1].device
+    stream = _lib.stream_ptr(dev)
+    layers = list(nets[0].encoder.layers)
+    B, n, e = topo.B, topo.n, topo.e
+    N = B * n
+    pro = [fused.prologue_args(net, nx, ex, topo) for net, nx, ex, _, _ in specs]
+    _lib.check(L.trx_gat_prologue_infer_multi(_lib.multi(_lib.TrxGatPrologueArgs, [p[0] for p in pro]), k, stream),
+               "trx_gat_prologue_infer_multi")
+    keep = [p[2] for p in pro]
+    x0s, eas, a_alls, m_works = zip(*[p[1] for p in pro])
+    stride = a_alls[0].shape[1]
+    w0, wp, bp, W, WN, WC, WE, W2, B2 = _stack_weights(nets)
+    recs = [[] for _ in range(k)]
+    prev_f32 = [None] * k
+    prev_b = None
+    x_in = []
+    ctx = None
+    off = 0
+    for i, l in enumerate(layers):
+        last = i == len(layers) - 1
+        HC = l.heads * l.out_channels
+        xh = None
+        if i > 0:
+            # per network, the single pass's GEMM (a batched bf16 GEMM over the networks faulted
+            # in hipBLASLt on this image at [5, 6144, 1024] x [5, 1024, 1024]^T)
+            xh = [F.linear(prev_b[j], W[i - 1][j]) for j in range(k)]   # [N, HC] bf16 each
+            x_in.append(prev_b)
+        out_b = torch.empty(k, N, HC, device=dev, dtype=torch.bfloat16)
+        if last:
+            ctx = torch.empty(k, B, 2 * HC, device=dev)
+        arglist = []
+        for j, (net, _, _, save, _) in enumerate(specs):
+            enc = net.encoder
+            lj, norm = enc.layers[i], enc.norms[i]
+            args = _layer_args(lj, norm, topo, a_alls[j], off, stride, i, last)
+            args.exact = 0
+            rec = {"off": off, "heads": lj.heads, "channels": lj.out_channels}
+            if i == 0:
+                args.in_dim, args.x0, args.w0 = x0s[j].shape[1], x0s[j].data_ptr(), w0[j].data_ptr()
+                args.residual, args.wp, args.bp = 2, wp[j].data_ptr(), bp[j].data_ptr()
+                rec.update(w0=w0[j], wp=wp[j])
+            else:
+                args.in_dim, args.xh = 0, xh[j].data_ptr()
+                rec.update(xh=xh[j], x_in=prev_b[j], w=W[i - 1][j])
+                if last:
+                    args.residual = 0
+                else:
+                    args.residual, args.res = 1, prev_f32[j].data_ptr()
+            att_s, att_d = lj.att_src.detach().reshape(-1), lj.att_dst.detach().reshape(-1)
+            args.att_src, args.att_dst, args.bias = att_s.data_ptr(), att_d.data_ptr(), lj.bias.detach().data_ptr()
+            args.ln_weight, args.ln_bias = norm.weight.detach().data_ptr(), norm.bias.detach().data_ptr()
+            args.out_bf16 = out_b[j].data_ptr()
+            out_f32 = None
+            if save or (i + 1 < len(layers) - 1):
+                out_f32 = torch.empty(N, HC, device=dev)
+                args.out_f32 = out_f32.data_ptr()
+            if last:
+                args.pool = ctx[j].data_ptr()
+            if save:
+                Et = topo.g.col.numel()
+                rec.update(alpha=torch.empty(Et, lj.heads, device=dev), asd=torch.empty(N, 2 * lj.heads, device=dev),
+                           v=torch.empty(N, HC, device=dev), stats=torch.empty(N, 2, device=dev), y=out_f32)
+                args.save_alpha, args.save_asd = rec["alpha"].data_ptr(), rec["asd"].data_ptr()
+                args.save_v, args.save_stats = rec["v"].data_ptr(), rec["stats"].data_ptr()
+            arglist.append(args)
+            recs[j].append(rec)
+            prev_f32[j] = out_f32
+        _lib.check(L.trx_gat_layer_infer_multi(_lib.multi(_lib.TrxGatLayerArgs, arglist), k, stream),
+                   "trx_gat_layer_infer_multi")
+        prev_b = out_b
+        off += l.heads
+    emb = prev_b                                                        # [k, N, d] bf16
+    p = [F.linear(emb[j], WN[j]) for j in range(k)]                     # bf16 [N, 2H] per-node projections
+    ctx_b = ctx.to(torch.bfloat16)
+    c = [_mm32(ctx_b[j], WC[j].t(), net.edge_mlp[0].bias.detach())      # bf16 operands, fp32 product + bias
+         for j, net in enumerate(nets)]
+    grp = NetGroup(x_in, W, emb, ctx, WN, WC)
+    logits = [torch.empty(B * e, device=dev) for _ in range(k)]
+    heads = {0: [], 1: []}
+    for j, (net, _, _, _, mask) in enumerate(specs):
+        a = fused._edge_args(p[j], c[j], eas[j], WE[j], W2[j], B2[j], topo.src32, topo.dst32, B, n, e)
+        a.exact = 0
+        a.out = logits[j].data_ptr()
+        if mask is not None:
+            m = mask.float().contiguous()
+            keep.append(m)
+            a.mask, a.softmax = m.data_ptr(), 1
+        heads[a.softmax].append(a)
+    for grp_args in heads.values():
+        if grp_args:
+            _lib.check(L.trx_edge_head_infer_multi(_lib.multi(_lib.TrxEdgeHeadArgs, grp_args), len(grp_args), stream),
+                       "trx_edge_head_infer_multi")
+    del keep
+    out = []
+    for j, (net, nx, ex, save, _) in enumerate(specs):
+        if not save:
+            out.append((logits[j], None))
+            continue
+        head_w = (WN[j], WC[j].t(), WE[j], W2[j], B2[j])
+        out.append((logits[j], NetCtx(x0s[j], eas[j], a_alls[j], m_works[j], nx, ex, recs[j], emb[j], ctx[j], p[j],
+                                      c[j], head_w, grp, j)))
+    return out
+
+
+def net_backward_multi(nets, cxs: List[NetCtx], g_logits: List[torch.Tensor], topo: Topology,
+                       sinks: List["GradFlat"], sums: "PartialSums"):
+    """net_backward (bf16 mode) for networks of one net_forward_multi group in
+    shared launches: the edge-scorer, layer and prologue backward kernels once
+    per kind (trx_*_backward_multi), the weight-gradient and input-gradient
+    GEMMs per network as net_backward issues them.  Each network's gradients go into its own
+    sink in net_backward's order; the column sums are left to `sums`."""
+    L = _lib.load()
+    k = len(nets)
+    grp = cxs[0].grp
+    assert grp is not None and all(cx.grp is grp for cx in cxs) and [cx.j for cx in cxs] == list(range(k))
+    dev = g_logits[0].device
+    stream = _lib.stream_ptr(dev)
+    layers = list(nets[0].encoder.layers)
+    B, n, e = topo.B, topo.n, topo.e
+    N = B * n
+    WN, WC = grp.WN[:k], grp.WC[:k]   # the group's first k networks (the trained ones)
+    Hd = WN.shape[1] // 2
+    K = cxs[0].head_w[2].shape[1]
+    # ---- edge scorer
+    g_p = torch.empty(k, N, 2 * Hd, device=dev, dtype=torch.bfloat16)
+    g_c = torch.empty(k, B, Hd, device=dev)
+    gw2p = torch.empty(k, B, Hd, device=dev)
+    gwep = torch.empty(k, B, Hd * K, device=dev)
+    g_ea_head = torch.empty(k, B * e, K, device=dev)
+    gl = [g.contiguous() for g in g_logits]
+    args, ios = [], []
+    for j, cx in enumerate(cxs):
+        wn, wc, we, w2, b2 = cx.head_w[:5]
+        a = fused._edge_args(cx.p, cx.c, cx.ea, we, w2, b2, topo.src32, topo.dst32, B, n, e)
+        a.exact = 0
+        args.append(a)
+        ios.append(_lib.TrxEdgeHeadBwdIO(gl[j].data_ptr(), g_p[j].data_ptr(), g_c[j].data_ptr(), None,
+                                         gw2p[j].data_ptr(), gwep[j].data_ptr(), g_ea_head[j].data_ptr()))
+    _lib.check(L.trx_edge_head_backward_multi(_lib.multi(_lib.TrxEdgeHeadArgs, args),
+                                              _lib.multi(_lib.TrxEdgeHeadBwdIO, ios), k, stream),
+               "trx_edge_head_backward_multi")
+    g_we = torch.empty(k, Hd, K, device=dev)
+    for j in range(k):
+        sums.add(gwep[j], Hd * K, Hd * K, g_we[j])
+    # the GEMMs per network, as net_backward issues them
+    g_wn = [_splitk_wgrad(g_p[j], grp.emb[j]) for j in range(k)]              # [2H, embed] fp32
+    g_emb = [_mm32(g_p[j], WN[j]) for j in range(k)]                           # [N, embed] fp32
+    g_cb = g_c.to(torch.bfloat16)
+    ctx_b = grp.ctx[:k].to(torch.bfloat16)
+    g_wc = [_mm32(g_cb[j].t(), ctx_b[j]) for j in range(k)]                    # [H, 2 embed]
+    g_ctx = [_mm32(g_cb[j], WC[j]) for j in range(k)]                          # [B, 2 embed]
+    for j, net in enumerate(nets):
+        W1 = net.edge_mlp[0].weight
+        gW1 = sinks[j].take(W1.numel()).view_as(W1)
+        sums.after.append(lambda j=j, gW1=gW1: torch.cat([g_wn[j][:Hd], g_wn[j][Hd:], g_we[j], g_wc[j]], 1, out=gW1))
+        sums.used += [gW1]
+        _grad(W1, gW1)
+        for prm, src in ((net.edge_mlp[0].bias, g_c[j]), (net.edge_mlp[2].weight, gw2p[j])):
+            dst = sinks[j].take(prm.numel())
+            sums.add(src, Hd, Hd, dst)
+            _grad(prm, dst)
+        gb2 = sinks[j].take(1)
+        torch.sum(gl[j], 0, keepdim=True, out=gb2)
+        _grad(net.edge_mlp[2].bias, gb2)
+    sums.used += g_wn + g_wc + [g_we]
+    # ---- GAT layers, last to first
+    g_a_all = [torch.empty_like(cx.a_all) for cx in cxs]
+    g_x0 = [torch.empty_like(cx.x0) for cx in cxs]
+    gy, g_pool = g_emb, g_ctx
+    for i in range(len(layers) - 1, -1, -1):
+        l = layers[i]
+        last = i == len(layers) - 1
+        HC = l.heads * l.out_channels
+        g_xh = torch.empty(k, N, HC, device=dev, dtype=torch.bfloat16)
+        g_res = torch.empty(k, N, HC, device=dev)
+        PW = int(L.trx_gat_layer_backward_part_floats(l.heads, l.out_channels, 4 if i == 0 else 0))
+        part = torch.empty(k, B, PW, device=dev)
+        bargs = []
+        for j, (net, cx) in enumerate(zip(nets, cxs)):
+            lj, norm, rec = net.encoder.layers[i], net.encoder.norms[i], cx.layers[i]
+            ba = _lib.TrxGatLayerBwdArgs()
+            ba.num_graphs, ba.nodes_per_graph, ba.heads, ba.channels = B, n, lj.heads, lj.out_channels
+            ba.max_graph_edges, ba.in_dim = topo.max_graph_edges, 4 if i == 0 else 0
+            g = topo.g
+            ba.rowptr, ba.col, ba.sptr, ba.spos = g.rowptr.data_ptr(), g.col.data_ptr(), g.sptr.data_ptr(), g.spos.data_ptr()
+            ba.att_src = lj.att_src.detach().reshape(-1).data_ptr()
+            ba.att_dst = lj.att_dst.detach().reshape(-1).data_ptr()
+            ba.ln_weight = norm.weight.detach().data_ptr()
+            ba.a_edge, ba.a_edge_stride, ba.a_edge_offset = cx.a_all.data_ptr(), cx.a_all.shape[1], rec["off"]
+            ba.negative_slope = float(lj.negative_slope)
+            ba.exact = 0
+            ba.activation = 1 if last else 0
+            ba.residual = 0 if last else (2 if i == 0 else 1)
+            if i == 0:
+                ba.x0, ba.w0, ba.wp, ba.g_x0 = (cx.x0.data_ptr(), rec["w0"].data_ptr(), rec["wp"].data_ptr(),
+                                                g_x0[j].data_ptr())
+            else:
+                ba.xh = rec["xh"].data_ptr()
+            ba.alpha, ba.asd, ba.v, ba.stats, ba.y = (rec["alpha"].data_ptr(), rec["asd"].data_ptr(),
+                                                       rec["v"].data_ptr(), rec["stats"].data_ptr(), rec["y"].data_ptr())
+            ba.gy = gy[j].data_ptr()
+            ba.g_pool = 0 if g_pool is None else g_pool[j].data_ptr()
+            ba.g_xh, ba.g_res, ba.g_a_edge, ba.part = (g_xh[j].data_ptr(), g_res[j].data_ptr(), g_a_all[j].data_ptr(),
+                                                       part[j].data_ptr())
+            bargs.append(ba)
+        _lib.check(L.trx_gat_layer_backward_multi(_lib.multi(_lib.TrxGatLayerBwdArgs, bargs), k, stream),
+                   "trx_gat_layer_backward_multi")
+        for j, net in enumerate(nets):
+            lj, norm = net.encoder.layers[i], net.encoder.norms[i]
+            pg = sinks[j].take(PW)
+            sums.add(part[j], PW, PW, pg)
+            _grad(lj.bias, pg[:HC])
+            _grad(norm.weight, pg[HC:2 * HC])
+            _grad(norm.bias, pg[2 * HC:3 * HC])
+            _grad(lj.att_src, pg[3 * HC:4 * HC])
+            _grad(lj.att_dst, pg[4 * HC:5 * HC])
+            if i == 0:
+                _grad(lj.lin.weight, pg[5 * HC:9 * HC])
+                _grad(net.encoder.input_proj.weight, pg[9 * HC:13 * HC])
+                _grad(net.encoder.input_proj.bias, pg[13 * HC:14 * HC])
+        sums.used += [part]
+        if i > 0:
+            # lin: xh = x_in @ w^T (bf16): split-K fp32 weight gradients, then the previous layer's output gradient (bf16 through lin + fp32 residual)
+            x_in = grp.x_in[i - 1]
+            S = 4 if N % 4 == 0 else 1
+            gy = []
+            for j, net in enumerate(nets):
+                lw = net.encoder.layers[i].lin.weight
+                gw = sinks[j].take(lw.numel()).view_as(lw)
+                part_w = torch.bmm(g_xh[j].view(S, N // S, -1).transpose(1, 2), x_in[j].view(S, N // S, -1))
+                torch.sum(part_w, 0, dtype=torch.float32, out=gw)
+                _grad(lw, gw)
+                # a middle layer's input also reaches it as the float32 residual
+                gy.append(_mm32(g_xh[j], grp.W[i - 1][j], None if last else g_res[j]))
+            g_pool = None
+    # ---- prologue (input LayerNorms, loop attrs, edge-logit projections)
+    A = cxs[0].a_all.shape[1]
+    PP = 8 * A + 32
+    ppart = torch.empty(k, B, PP, device=dev)
+    pargs = []
+    for j, (net, cx) in enumerate(zip(nets, cxs)):
+        pa = _lib.TrxGatPrologueBwdArgs()
+        pa.num_graphs, pa.nodes_per_graph, pa.edges_per_graph = B, n, e
+        pa.node_dim, pa.edge_dim, pa.A = cx.node_x.shape[1], cx.edge_x.shape[1], A
+        pa.node_x, pa.edge_x = cx.node_x.data_ptr(), cx.edge_x.data_ptr()
+        nw, nb = net.node_norm.weight.detach(), net.node_norm.bias.detach()
+        ew, eb = net.edge_norm.weight.detach(), net.edge_norm.bias.detach()
+        pa.node_ln_w, pa.node_ln_b, pa.node_ln_eps = nw.data_ptr(), nb.data_ptr(), float(net.node_norm.eps)
+        pa.edge_ln_w, pa.edge_ln_b, pa.edge_ln_eps = ew.data_ptr(), eb.data_ptr(), float(net.edge_norm.eps)
+        pa.src, pa.dst, pa.rowptr, pa.pos_src = (topo.src32.data_ptr(), topo.dst32.data_ptr(),
+                                                 topo.g.rowptr.data_ptr(), topo.pos_src.data_ptr())
+        pa.m_work, pa.g_a_edge, pa.g_x0, pa.g_ea_head = (cx.m_work.data_ptr(), g_a_all[j].data_ptr(),
+                                                         g_x0[j].data_ptr(), g_ea_head[j].data_ptr())
+        pa.part = ppart[j].data_ptr()
+        pa.exact = 0
+        pargs.append(pa)
+    _lib.check(L.trx_gat_prologue_backward_multi(_lib.multi(_lib.TrxGatPrologueBwdArgs, pargs), k, stream),
+               "trx_gat_prologue_backward_multi")
+    sums.used += [ppart] + g_a_all + g_x0 + [g_ea_head]
+    for j, (net, cx) in enumerate(zip(nets, cxs)):
+        _prologue_grads(net, cx, ppart[j], sinks[j], sums, PP, A, dev)
+
+
+def _prologue_grads(net, cx: NetCtx, ppart: torch.Tensor, sink: "GradFlat", sums: "PartialSums", PP: int, A: int,
+                    dev):
+    """The prologue's parameter gradients from its per-graph partials: the
+    input LayerNorms (column sums) and every layer's lin_edge / att_edge
+    (trx_edge_att_weights_backward after the sums), into `sink`."""
+    L = _lib.load()
+    layers = list(net.encoder.layers)
+    pp = sink.take(PP)
+    sums.add(ppart, PP, PP, pp)
+    ed, nd = cx.edge_x.shape[1], cx.node_x.shape[1]
+    _grad(net.edge_norm.weight, pp[8 * A:8 * A + ed])
+    _grad(net.edge_norm.bias, pp[8 * A + 8:8 * A + 8 + ed])
+    _grad(net.node_norm.weight, pp[8 * A + 16:8 * A + 16 + nd])
+    _grad(net.node_norm.bias, pp[8 * A + 24:8 * A + 24 + nd])
+    # M[h, j] = sum_c W[h*C + c, j] * att[h, c] (fp32, then bf16-rounded in the forward):
+    # every layer's lin_edge / att_edge gradient from the summed M-row gradients, one launch
+    ea_args = _lib.TrxGatPrologueArgs()
+    ea_args.num_layers, ea_args.edge_dim = len(layers), ed
+    keep = []
+    for i, l in enumerate(layers):
+        w, at = l.lin_edge.weight.detach().contiguous(), l.att_edge.detach().contiguous()
+        keep += [w, at]
+        ea_args.heads[i], ea_args.channels[i] = l.heads, l.out_channels
+        ea_args.lin_edge_w[i], ea_args.att_edge[i] = w.data_ptr(), at.data_ptr()
+    tot = sum(l.heads * l.out_channels * (ed + 1) for l in layers)
+    gout = sink.take(tot)
+
+    def att_weights():   # needs the summed prologue partials (pp)
+        _lib.check(L.trx_edge_att_weights_backward(ea_args, _lib.ptr(pp), 8, _lib.ptr(gout),
+                                                   _lib.stream_ptr(dev)), "trx_edge_att_weights_backward")
+    sums.after.append(att_weights)
+    sums.used += [gout] + keep
+    off = 0
+    for l in layers:
+        HC = l.heads * l.out_channels
+        _grad(l.lin_edge.weight, gout[off:off + HC * ed].view(HC, ed))
+        _grad(l.att_edge, gout[off + HC * ed:off + HC * (ed + 1)])
+        off += HC * (ed + 1)
 
 
 class GradFlat:
@@ -570,17 +951,37 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     # forward + backward is the update's longest chain, and a replayed graph
     # starts its branches in issue order, ~0.2 ms apart
     xa, xc = (exact_nets(agent)[k] for k in ("actor", "critic"))
+    # grouped (MULTI 1 / 2): the five bf16 passes -- the critics' training forwards and
+    # the next-state actor / target passes -- share their launches (net_forward_multi),
+    # beside the actor's float32 training pass: two or three branches instead of six
+    grouped = MULTI in (1, 2) and not xc and multi_supported([agent.critic1, agent.critic2, agent.actor, agent.target1,
+                                                     agent.target2])
     with torch.no_grad():
-        outs = agent._concurrent(
-            [lambda net=net, x=x: net_forward(net, nx, ex, topo, save=True, exact=x)
-             for net, x in ((agent.actor, xa), (agent.critic1, xc), (agent.critic2, xc))] + [
-                # the next-state probabilities only enter the critics' target: the
-                # critics' precision (bf16 unless the agent trains in float32)
-                lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask, exact=xc)[0],
-                lambda: net_forward(agent.target1, nnx, nex, topo, save=False, exact=xc)[0],
-                lambda: net_forward(agent.target2, nnx, nex, topo, save=False, exact=xc)[0]])
-    (lg, ca), (q1, c1), (q2, c2) = outs[:3]
-    nprobs, qt1, qt2 = outs[3:]
+        if grouped:
+            specs = [(agent.critic1, nx, ex, True, None), (agent.critic2, nx, ex, True, None),
+                     (agent.actor, nnx, nex, False, next_action_mask), (agent.target1, nnx, nex, False, None),
+                     (agent.target2, nnx, nex, False, None)]
+            if MULTI == 2:
+                (lg, ca), crit, nxt = agent._concurrent(
+                    [lambda: net_forward(agent.actor, nx, ex, topo, save=True, exact=xa),
+                     lambda: net_forward_multi(specs[:2], topo), lambda: net_forward_multi(specs[2:], topo)])
+                group = crit + nxt
+            else:
+                (lg, ca), group = agent._concurrent(
+                    [lambda: net_forward(agent.actor, nx, ex, topo, save=True, exact=xa),
+                     lambda: net_forward_multi(specs, topo)])
+            (q1, c1), (q2, c2), (nprobs, _), (qt1, _), (qt2, _) = group
+        else:
+            outs = agent._concurrent(
+                [lambda net=net, x=x: net_forward(net, nx, ex, topo, save=True, exact=x)
+                 for net, x in ((agent.actor, xa), (agent.critic1, xc), (agent.critic2, xc))] + [
+                    # the next-state probabilities only enter the critics' target: the
+                    # critics' precision (bf16 unless the agent trains in float32)
+                    lambda: net_forward(agent.actor, nnx, nex, topo, save=False, mask=next_action_mask, exact=xc)[0],
+                    lambda: net_forward(agent.target1, nnx, nex, topo, save=False, exact=xc)[0],
+                    lambda: net_forward(agent.target2, nnx, nex, topo, save=False, exact=xc)[0]])
+            (lg, ca), (q1, c1), (q2, c2) = outs[:3]
+            nprobs, qt1, qt2 = outs[3:]
     L = _lib.load()
     la = agent.log_alpha.detach().reshape(1)
     act_local = action % E      # the batch tuple carries graph offsets (arange(B) * E + action)
@@ -629,9 +1030,14 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     # each network's backward on the stream its training forward ran on: the
     # saved tensors are read on the stream that allocated them
     sums = PartialSums(B)
-    agent._concurrent([lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
-                       lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc, sums=sums),
-                       lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc, sums=sums)])
+    if grouped:
+        agent._concurrent([lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
+                           lambda: net_backward_multi([agent.critic1, agent.critic2], [c1, c2], [g_q1, g_q2], topo,
+                                                      sinks[:2], sums)])
+    else:
+        agent._concurrent([lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
+                           lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc, sums=sums),
+                           lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc, sums=sums)])
     sums.flush(_lib.stream_ptr(dev))   # every network's column sums in one launch, on the joined stream
     agent.log_alpha.grad = g_la.view_as(agent.log_alpha)
     agent.grad_flat = flat        # every gradient of this update is a view of it (GradAllReduce)

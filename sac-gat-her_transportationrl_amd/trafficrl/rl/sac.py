@@ -593,10 +593,13 @@ class DiscreteSAC:
                 outs.append(fn())
         for st in {id(s): s for s in used}.values():
             main.wait_stream(st)
-        for o in outs:   # consumed (and freed) on the main stream from here on
-            for t in (o if isinstance(o, (tuple, list)) else (o,)):
-                if isinstance(t, torch.Tensor):
-                    t.record_stream(main)
+        def record(o):   # consumed (and freed) on the main stream from here on
+            if isinstance(o, torch.Tensor):
+                o.record_stream(main)
+            elif isinstance(o, (tuple, list)):
+                for t in o:
+                    record(t)
+        record(outs)
         return outs
 
     def _flat_opt(self):

@@ -35,7 +35,7 @@ def test_exports_every_declared_symbol():
     assert set(syms) == set(_lib.EXPORTS)
     for s in syms:
         assert hasattr(L, s), s
-    assert L.trx_abi_version() == _lib.ABI_VERSION == 10
+    assert L.trx_abi_version() == _lib.ABI_VERSION == 11
 
 
 def test_struct_layout_matches_header(tmp_path):
@@ -165,7 +165,8 @@ def test_batch_damage_sampler_matches_numpy_generator(net):
 
 def test_fused_args_layout_matches_header(tmp_path):
     """Every field offset of the fused kernels' argument structs (incl. ABI
-    10's exact fields, the round list's dst_stride and trx_psum_list) as the C
+    10's exact fields, the round list's dst_stride, trx_psum_list and ABI 11's
+    trx_edge_head_bwd_io) as the C
     compiler lays them out equals the ctypes mirror in trafficrl/_lib.py."""
     from trafficrl import _lib
     lines = []
@@ -173,7 +174,7 @@ def test_fused_args_layout_matches_header(tmp_path):
                ("trx_gat_prologue_args", _lib.TrxGatPrologueArgs), ("trx_gat_layer0_args", _lib.TrxGatLayer0Args),
                ("trx_gat_mid_args", _lib.TrxGatMidArgs), ("trx_gat_layer_bwd_args", _lib.TrxGatLayerBwdArgs),
                ("trx_gat_prologue_bwd_args", _lib.TrxGatPrologueBwdArgs), ("trx_round_list", _lib.TrxRoundList),
-               ("trx_psum_list", _lib.TrxPsumList))
+               ("trx_psum_list", _lib.TrxPsumList), ("trx_edge_head_bwd_io", _lib.TrxEdgeHeadBwdIO))
     for cname, cls in structs:
         lines.append(f'printf("%zu\\n", sizeof({cname}));')
         for f, _ in cls._fields_:
@@ -299,3 +300,32 @@ def test_integration_snippet_matches_abi():
         assert C.sizeof(mine) == C.sizeof(ref), name
         assert [(f[0], getattr(mine, f[0]).offset) for f in mine._fields_ if not f[0].startswith("_")] == \
                [(f[0], getattr(ref, f[0]).offset) for f in ref._fields_ if not f[0].startswith("_")], name
+
+
+def test_multi_launches_validated_without_gpu():
+    """The *_multi entry points (ABI 11) refuse a network count outside
+    1..TRX_MAX_NETS and networks whose shapes differ, before any HIP call."""
+    from trafficrl import _lib
+    L = _lib.load()
+    a = _lib.TrxGatLayerArgs()
+    assert L.trx_gat_layer_infer_multi(_lib.multi(_lib.TrxGatLayerArgs, [a]), 0, None) == _lib.TRX_EINVAL
+    assert L.trx_gat_layer_infer_multi(_lib.multi(_lib.TrxGatLayerArgs, [a] * 7), 7, None) == _lib.TRX_EINVAL
+    # two otherwise valid blocks that differ in heads: refused as a pair
+    keep = []
+    def block(heads):
+        b = _lib.TrxGatLayerArgs()
+        b.num_graphs, b.nodes_per_graph, b.heads, b.channels, b.concat, b.max_graph_edges = 0, 24, heads, 256 // heads, 1, 100
+        b.in_dim, b.residual, b.activation = 0, 0, 0
+        buf = (ctypes.c_float * 16)()
+        keep.append(buf)
+        p = ctypes.addressof(buf)
+        b.xh = b.rowptr = b.col = b.a_edge = b.att_src = b.att_dst = b.bias = b.ln_weight = b.ln_bias = p
+        b.out_bf16 = p
+        b.a_edge_stride, b.a_edge_offset = 8, 0
+        return b
+    assert L.trx_gat_layer_infer_multi(_lib.multi(_lib.TrxGatLayerArgs, [block(4), block(4)]), 2, None) == 0
+    rc = L.trx_gat_layer_infer_multi(_lib.multi(_lib.TrxGatLayerArgs, [block(4), block(2)]), 2, None)
+    assert rc == _lib.TRX_EINVAL and b"differs" in L.trx_last_error()
+    io = _lib.TrxEdgeHeadBwdIO()
+    assert L.trx_edge_head_backward_multi(_lib.multi(_lib.TrxEdgeHeadArgs, [_lib.TrxEdgeHeadArgs()]),
+                                          _lib.multi(_lib.TrxEdgeHeadBwdIO, [io]), 0, None) == _lib.TRX_EINVAL

@@ -138,6 +138,34 @@ def test_fused_update_fp32_mode_vs_restatement():
         assert abs(float(out[k]) - r) <= 1e-4 * max(1e-3, abs(r)), (k, float(out[k]), r)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_grouped_update_bit_identical(mode):
+    """The grouped update (rl/fused_update.py MULTI 1 / 2: the bf16 passes in
+    shared trx_*_multi launches, network index in blockIdx.y) computes the
+    same gradients and metrics, bit for bit, as the six-branch default: the
+    same kernels per network, the same GEMM calls, the same sums.  Two eager
+    updates each: the second runs its branches on the concurrent side streams."""
+    from trafficrl.rl import fused_update as FU
+    B = 256
+    batch = _update_batch(B)
+    w = torch.rand(B, device="cuda") * 0.5 + 0.5
+    res = {}
+    old = FU.MULTI
+    try:
+        for m in (0, mode):
+            FU.MULTI = m
+            agent = make_agent(hidden=256, embed=256)
+            outs = [agent.compute_gradients(batch, weights=w) for _ in range(2)]
+            assert agent.last_update_path == "fused"
+            torch.cuda.synchronize()
+            res[m] = (agent.grad_flat.clone(), {k: v.clone() for k, v in outs[-1].items()})
+    finally:
+        FU.MULTI = old
+    assert torch.equal(res[0][0], res[mode][0])
+    for k, v in res[0][1].items():
+        assert torch.equal(v, res[mode][1][k]), k
+
+
 def test_fused_update_vs_autograd_path():
     """The bf16 rounding points of autocast (fp32_actor off), different
     summation orders and layer-0 arithmetic: critics per tensor within 3e-2,

@@ -107,9 +107,20 @@ for s in "$@"; do
                TRX_PER_OVERLAP=0 step bench_pov0b 400 python bench.py --steps 44 --warmup 22 --no-cpu && step bench_pov1b 400 python bench.py --steps 44 --warmup 22 --no-cpu ;;
         updtl) step updtl 300 rocprofv3 --kernel-trace -d gpurun_out/updtl -o run --output-format csv -- python3 tools/upd_timeline.py run &&
                python tools/upd_timeline.py report $(ls gpurun_out/updtl/*/run_kernel_trace.csv gpurun_out/updtl/run_kernel_trace.csv 2>/dev/null | head -1) > gpurun_out/updtl_report.txt 2>&1 ;;
+        multi2) for m in 0 1 2; do TRX_UPD_MULTI=$m step upd_time_m$m 300 python tools/upd_time.py || exit 1; done &&
+                for m in 1 2; do TRX_UPD_MULTI=$m step updtl_m$m 300 rocprofv3 --kernel-trace -d gpurun_out/updtl_m$m -o run --output-format csv -- python3 tools/upd_timeline.py run || exit 1
+                    python tools/upd_timeline.py report $(ls gpurun_out/updtl_m$m/*/run_kernel_trace.csv gpurun_out/updtl_m$m/run_kernel_trace.csv 2>/dev/null | head -1) > gpurun_out/updtl_m${m}_report.txt 2>&1; done ;;
         disttests) step dist_tests 600 python -u -m pytest tests/test_dist_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         dist2) step bench_dist2 600 env TRX_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 44 --warmup 22 --no-cpu ;;
         branchprobe) step branch_probe3 300 python tools/branch_probe.py 3 && step branch_probe6 300 python tools/branch_probe.py 6 ;;
+        fu1) step fu1 150 env AMD_SERIALIZE_KERNEL=3 python -u -m pytest tests/test_fused_update.py -m gpu -x -v -s --timeout 60 --timeout-method thread -k vs_fp32_restatement ;;
+        mprobe) step multi_probe 150 python -u tools/multi_probe.py 5 && PROBE_STAGES=1 step multi_stages 150 python -u tools/multi_probe.py 5 ;;
+        multi) step multi_tests 900 python -u -m pytest tests/test_fused_update.py tests/test_concurrent_update.py tests/test_sac_e2e.py tests/test_gat_infer.py tests/test_flat_adam.py -m gpu -x -v -s --timeout 300 --timeout-method thread &&
+               TRX_UPD_MULTI=0 step upd_time_m0 300 python tools/upd_time.py && TRX_UPD_MULTI=1 step upd_time_m1 300 python tools/upd_time.py &&
+               TRX_UPD_MULTI=0 step upd_time_m0b 300 python tools/upd_time.py && TRX_UPD_MULTI=1 step upd_time_m1b 300 python tools/upd_time.py ;;
+        resab) step gat_e2e 600 python -u -m pytest tests/test_gat_infer.py tests/test_sac_e2e.py tests/test_gat_tail.py tests/test_capi_cpu.py -m gpu -v -s --timeout 300 --timeout-method thread &&
+               TRX_RES_BF16=0 step act_res0 300 python tools/agent_profile.py 4096 act && TRX_RES_BF16=1 step act_res1 300 python tools/agent_profile.py 4096 act &&
+               TRX_RES_BF16=0 step act_res0b 300 python tools/agent_profile.py 4096 act && TRX_RES_BF16=1 step act_res1b 300 python tools/agent_profile.py 4096 act ;;
         updt) step upd_time 300 python tools/upd_time.py ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
         uprof) step uprof 300 python tools/update_profile.py 70 ;;
