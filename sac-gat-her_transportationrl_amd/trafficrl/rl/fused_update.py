@@ -933,9 +933,11 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
         sums.flush(stream)
 
 
-def compute_gradients_fused(agent, batch, weights, topo: Topology):
+def compute_gradients_fused(agent, batch, weights, topo: Topology, on_td=None):
     """DiscreteSAC.compute_gradients (sac.py:157-243) on the fused path: the
-    same returned metrics (device tensors), every gradient set."""
+    same returned metrics (device tensors), every gradient set.  on_td(td):
+    work that needs only the TD errors (the trainer's priority write-back),
+    run as one more branch beside the backwards."""
     (node_x, edge_index, edge_attr, action_mask, batch_vec, action, reward, next_node_x, next_edge_attr,
      next_action_mask, next_batch_vec, done) = batch
     B = reward.shape[0]
@@ -1031,13 +1033,18 @@ def compute_gradients_fused(agent, batch, weights, topo: Topology):
     # saved tensors are read on the stream that allocated them
     sums = PartialSums(B)
     if grouped:
-        agent._concurrent([lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
-                           lambda: net_backward_multi([agent.critic1, agent.critic2], [c1, c2], [g_q1, g_q2], topo,
-                                                      sinks[:2], sums)])
+        fns = [lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
+               lambda: net_backward_multi([agent.critic1, agent.critic2], [c1, c2], [g_q1, g_q2], topo, sinks[:2],
+                                          sums)]
     else:
-        agent._concurrent([lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
-                           lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc, sums=sums),
-                           lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc, sums=sums)])
+        fns = [lambda: net_backward(agent.actor, ca, g_lg, topo, sinks[2], exact=xa, sums=sums),
+               lambda: net_backward(agent.critic1, c1, g_q1, topo, sinks[0], exact=xc, sums=sums),
+               lambda: net_backward(agent.critic2, c2, g_q2, topo, sinks[1], exact=xc, sums=sums)]
+    streams = list(range(len(fns)))
+    if on_td is not None:   # behind the last critic backward: off the actor's (longest) chain
+        fns.append(lambda: on_td(td))
+        streams.append(streams[-1])
+    agent._concurrent(fns, streams)
     sums.flush(_lib.stream_ptr(dev))   # every network's column sums in one launch, on the joined stream
     agent.log_alpha.grad = g_la.view_as(agent.log_alpha)
     agent.grad_flat = flat        # every gradient of this update is a view of it (GradAllReduce)

@@ -449,11 +449,14 @@ class DiscreteSAC:
     def gradients(self):
         return [p.grad for p in self._all_params() if p.grad is not None]
 
-    def compute_gradients(self, batch, weights=None):
+    def compute_gradients(self, batch, weights=None, on_td=None):
         """Losses and the three backward passes of sac.py:157-243.  None of
         critic, actor and alpha backward depends on another's optimizer step,
         so all gradients exist before any step: one synchronisation point for
-        data parallelism.  No host synchronisation (HIP-graph capturable)."""
+        data parallelism.  No host synchronisation (HIP-graph capturable).
+        on_td(td_errors): work that needs only the TD errors (the trainer's
+        priority write-back, src/train.py:1017-1019), run beside the backward
+        passes on the fused path, after them otherwise."""
         if isinstance(batch, list) and len(batch) == 1:
             batch = batch[0]
         (node_x, edge_index, edge_attr, action_mask, batch_vec, action, reward, next_node_x, next_edge_attr,
@@ -464,7 +467,7 @@ class DiscreteSAC:
             topo = fused.topology(edge_index, batch_vec, B)
             if fused_update.supported(self, topo):
                 self.last_update_path = "fused"
-                return fused_update.compute_gradients_fused(self, batch, weights, topo)
+                return fused_update.compute_gradients_fused(self, batch, weights, topo, on_td=on_td)
         self.last_update_path = "autograd"
         self.grad_flat = None
         if weights is None:
@@ -554,6 +557,8 @@ class DiscreteSAC:
         critic_loss.backward()
         actor_loss.backward()
         alpha_loss.backward()
+        if on_td is not None:
+            on_td(td_error)
         self._warm = True
         return {
             "critic_loss": critic_loss.detach(),

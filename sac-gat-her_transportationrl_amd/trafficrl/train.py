@@ -479,12 +479,14 @@ class Trainer:
         batch = (s.node_x.reshape(bs * N, -1), self.upd_ei, s.edge_x.reshape(bs * E, -1), s.mask.reshape(-1),
                  self.upd_batch, action, s.reward, s.next_node_x.reshape(bs * N, -1), s.next_edge_x.reshape(bs * E, -1),
                  s.next_mask.reshape(-1), self.upd_batch, s.done)
-        out = self.agent.compute_gradients(batch, weights=s.weights)
+        # the priority write-back (src/train.py:1017-1019) reads only the TD errors and
+        # touches only the replay tree: it runs beside the backward passes
+        out = self.agent.compute_gradients(batch, weights=s.weights,
+                                           on_td=lambda td: self.replay.update_priorities(s.idx, td))
         return s, out
 
     def _update_apply(self, s, out):
         self.agent.apply_gradients(self.cfg.get("alpha_max"))
-        self.replay.update_priorities(s.idx, out["td_errors"])
 
     def updates_due(self, it: int) -> int:
         """SAC updates to run after iteration `it` (its B transitions added).
