@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "trx_internal.h"
 
@@ -38,8 +39,10 @@ __global__ void __launch_bounds__(kAT) adam_norm_kernel(trx_adam_args a) {
     const int b = blockIdx.x, tid = threadIdx.x;
     const trx_adam_block blk = a.blocks[b];
     const trx_adam_seg sg = a.segs[blk.seg];
-    const float* g = a.g_base + sg.goff;
+    const float* __restrict__ g = a.g_base + sg.goff;
     float s = 0.0f;
+    // unrolled: the loads of eight strided elements in flight, the sum in element order
+#pragma unroll 8
     for (int i = blk.begin + tid; i < blk.end; i += kAT) {
         const float v = g[i];
         s += v * v;
@@ -84,24 +87,54 @@ __global__ void __launch_bounds__(kAT) adam_apply_kernel(trx_adam_args a) {
     const float coef = a.scal[4 * grp], step_size = a.scal[4 * grp + 1], bc2s = a.scal[4 * grp + 2];
     const float b1 = a.beta1, b2 = a.beta2, eps = a.eps;
     const float omb1 = 1.0f - b1, omb2 = 1.0f - b2, tau = a.tau, omt = 1.0f - a.tau;
+    // four strided elements per round: every load of the round issued before its
+    // arithmetic and stores (the element's own expression order is unchanged).
+    // Out-of-range slots load a valid element (clamped index) and store nothing:
+    // no per-element branch around a load.
     const float* g = a.g_base + sg.goff;
     float* m = a.m + sg.moff;
     float* v = a.v + sg.moff;
-    for (int i = blk.begin + tid; i < blk.end; i += kAT) {
-        const float gi = g[i] * coef;
-        const float mi = b1 * m[i] + omb1 * gi;
-        const float vi = b2 * v[i] + omb2 * gi * gi;
-        const float denom = sqrtf(vi) / bc2s + eps;
-        float p = sg.p[i] - step_size * mi / denom;
-        if (grp == 2) {  // log_alpha clamps (sac.py:241-246)
-            p = p < a.log_alpha_max ? p : a.log_alpha_max;
-            p = p > a.log_alpha_min ? p : a.log_alpha_min;
+    float* pp = sg.p;
+    float* tt = sg.t;
+    constexpr int U = 4;
+    auto rounds = [&](auto has_t) {
+        constexpr bool HT = decltype(has_t)::value;
+        for (int i0 = blk.begin + tid; i0 < blk.end; i0 += U * kAT) {
+            float gv[U], mv[U], vv[U], pv[U], tv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * kAT < blk.end ? i0 + u * kAT : i0;
+                gv[u] = g[i];
+                mv[u] = m[i];
+                vv[u] = v[i];
+                pv[u] = pp[i];
+                if constexpr (HT) tv[u] = tt[i];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * kAT;
+                const float gi = gv[u] * coef;
+                const float mi = b1 * mv[u] + omb1 * gi;
+                const float vi = b2 * vv[u] + omb2 * gi * gi;
+                const float denom = sqrtf(vi) / bc2s + eps;
+                float p = pv[u] - step_size * mi / denom;
+                if (grp == 2) {  // log_alpha clamps (sac.py:241-246)
+                    p = p < a.log_alpha_max ? p : a.log_alpha_max;
+                    p = p > a.log_alpha_min ? p : a.log_alpha_min;
+                }
+                if (i < blk.end) {
+                    m[i] = mi;
+                    v[i] = vi;
+                    pp[i] = p;
+                    if constexpr (HT) tt[i] = tv[u] * omt + p * tau;  // Polyak (288-291)
+                }
+            }
         }
-        m[i] = mi;
-        v[i] = vi;
-        sg.p[i] = p;
-        if (sg.t) sg.t[i] = sg.t[i] * omt + p * tau;  // Polyak (288-291)
-    }
+    };
+    if (tt)
+        rounds(std::true_type{});
+    else
+        rounds(std::false_type{});
 }
 
 }  // namespace
