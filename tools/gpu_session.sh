@@ -44,8 +44,6 @@ for s in "$@"; do
         benchfw) step bench_fw 400 python bench.py --method fw --steps 44 --warmup 22 --cpu-seconds 5 ;;
         benchana) step bench_ana 600 python bench.py --network anaheim --steps 10 --warmup 3 --cpu-seconds 5 ;;
         benchrand) step bench_rand 400 python bench.py --workload env --damage random --steps 66 --warmup 22 --no-cpu ;;
-        wgrad) step wgrad 200 python tools/wgrad_probe.py ;;
-        opprobe) step op_probe 300 python tools/op_probe.py ;;
         envtests) step env_tests 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_sparse.py tests/test_gpu_fallback.py tests/test_torch_sp.py tests/test_rewards.py tests/test_replay_train.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
         obstests) step obs_tests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_oracle_observe.py tests/test_gpu_gp.py tests/test_rewards.py tests/test_torch_sp.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
         largetests) step large_tests 400 python -u -m pytest tests/test_gpu_large.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
@@ -74,7 +72,6 @@ for s in "$@"; do
                     step stamps_rand 300 env TRX_DAMAGE=random python tools/phase_stamps.py 4096 &&
                     step stamps_rand_reset 300 env TRX_DAMAGE=random TRX_STAMP_RESET=1 python tools/phase_stamps.py 4096 ;;
         epw) for e in 1 2 3 4; do step bench_epw$e 300 env TRX_EPW=$e python bench.py --workload env --steps 44 --warmup 22 --no-cpu; done ;;
-        detprobe) step det_probe 1000 bash tools/det_probe.sh ;;
         dettests) step det_tests 600 python -u -m pytest tests/test_determinism.py -m gpu -v -s --timeout 500 --timeout-method thread ;;
         gattests) step gat_tests 400 python -u -m pytest tests/test_gat_infer.py tests/test_gat.py tests/test_sac.py tests/test_gat_tail.py -m gpu -v --timeout 120 --timeout-method thread ;;
         actmid) TRX_MID=0 step act_mid0 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_mid0 -o run --output-format csv -- python3 tools/agent_profile.py 4096 act &&
@@ -129,8 +126,6 @@ for s in "$@"; do
                TRX_RES_BF16=0 step act_res0b 300 python tools/agent_profile.py 4096 act && TRX_RES_BF16=1 step act_res1b 300 python tools/agent_profile.py 4096 act ;;
         updt) step upd_time 300 python tools/upd_time.py ;;
         walls) step walls_act 300 python tools/agent_profile.py 4096 act && step walls_upd 300 python tools/agent_profile.py 4096 update ;;
-        uprof) step uprof 300 python tools/update_profile.py 70 ;;
-        copies) step copies 300 python tools/update_profile.py 60 copies ;;
         istamps) step istamps 300 python tools/infer_stamps.py 4096 ;;
         abact) TRX_LIB=${TRX_LIB_A:-} step act_a 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_a -o run --output-format csv -- python3 tools/agent_profile.py 4096 act
                TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/libtrafficrl_old.so step act_b 300 rocprofv3 --kernel-trace --stats -d gpurun_out/act_b -o run --output-format csv -- python3 tools/agent_profile.py 4096 act ;;
