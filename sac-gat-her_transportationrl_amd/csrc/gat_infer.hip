@@ -442,18 +442,37 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(const NetList<trx_g
         float4 acc[KC];
 #pragma unroll
         for (int k = 0; k < KC; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int p = rp[i]; p < rp[i + 1]; ++p) {
-            const XE* row = xs + cl[p] * XS;
-            const float* alr = al + p * H;
+        if (KC == 4 && C == 256) {
+            // chunk k is head k: the edge's four weights in one 16-byte LDS read
+            // (al rows are 16-byte aligned: H == 4 floats per edge)
+            for (int p = rp[i]; p < rp[i + 1]; ++p) {
+                const XE* row = xs + cl[p] * XS;
+                const float4 w4 = *reinterpret_cast<const float4*>(al + p * 4);
+                const float wk[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-            for (int k = 0; k < KC; ++k) {
-                const int q = lane + kWave * k;
-                const float w = alr[(4 * q) / C];
-                const float4 x4 = xld4<XF>(row + 4 * q);
-                acc[k].x += w * x4.x;
-                acc[k].y += w * x4.y;
-                acc[k].z += w * x4.z;
-                acc[k].w += w * x4.w;
+                for (int k = 0; k < KC; ++k) {
+                    const float w = wk[k & 3];
+                    const float4 x4 = xld4<XF>(row + 4 * (lane + kWave * k));
+                    acc[k].x += w * x4.x;
+                    acc[k].y += w * x4.y;
+                    acc[k].z += w * x4.z;
+                    acc[k].w += w * x4.w;
+                }
+            }
+        } else {
+            for (int p = rp[i]; p < rp[i + 1]; ++p) {
+                const XE* row = xs + cl[p] * XS;
+                const float* alr = al + p * H;
+#pragma unroll
+                for (int k = 0; k < KC; ++k) {
+                    const int q = lane + kWave * k;
+                    const float w = alr[(4 * q) / C];
+                    const float4 x4 = xld4<XF>(row + 4 * q);
+                    acc[k].x += w * x4.x;
+                    acc[k].y += w * x4.y;
+                    acc[k].z += w * x4.z;
+                    acc[k].w += w * x4.w;
+                }
             }
         }
         float v[KC][4];
