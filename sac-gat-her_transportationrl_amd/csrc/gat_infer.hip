@@ -720,15 +720,20 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(const Ne
                     const trx_f2 pdv[2] = {{d4.x, d4.y}, {d4.z, d4.w}};
 #pragma unroll
                     for (int rp = 0; rp < 2; ++rp) {
-                        trx_f2 ew = {0.0f, 0.0f};
+                        // the link-feature term and the 256 -> 1 product as fused multiply-adds
+                        // (one rounding per term; edge_head_bwd_kernel recomputes z the same way)
+                        float ewx = 0.0f, ewy = 0.0f;
 #pragma unroll
                         for (int j = 0; j < DC; ++j)
-                            if (DK > 0 || j < D) ew += (trx_f2){ear[j], ear[j]} * we2[m][rp][j];
+                            if (DK > 0 || j < D) {
+                                ewx = __builtin_fmaf(ear[j], we2[m][rp][j].x, ewx);
+                                ewy = __builtin_fmaf(ear[j], we2[m][rp][j].y, ewy);
+                            }
                         // fp32 from the bf16 GEMM outputs on: the link's hidden units and
                         // their shares of the 256 -> 1 product (units in order)
-                        const trx_f2 z = ((psv[rp] + pdv[rp]) + ew) + c2[m][rp];
-                        part[u] += fmaxf(z.x, 0.0f) * w2_r[m][2 * rp];
-                        part[u] += fmaxf(z.y, 0.0f) * w2_r[m][2 * rp + 1];
+                        const trx_f2 z = ((psv[rp] + pdv[rp]) + (trx_f2){ewx, ewy}) + c2[m][rp];
+                        part[u] = __builtin_fmaf(fmaxf(z.x, 0.0f), w2_r[m][2 * rp], part[u]);
+                        part[u] = __builtin_fmaf(fmaxf(z.y, 0.0f), w2_r[m][2 * rp + 1], part[u]);
                     }
                 }
             }
@@ -1133,10 +1138,10 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(const NetLis
     if (on) {  // (1) per link
         for (int e = part; e < E; e += P) {
             const int s = sl[e], d = dl[e];
-            float ew = 0.0f;
+            float ew = 0.0f;  // edge_head_infer_kernel's fused multiply-adds, same order
 #pragma unroll
             for (int j = 0; j < ED; ++j)
-                if (j < D) ew += eal[e * ED + j] * we[j];
+                if (j < D) ew = __builtin_fmaf(eal[e * ED + j], we[j], ew);
             const float z = ((xv(prow[s * 2 * Hd + k]) + xv(prow[d * 2 * Hd + Hd + k])) + ew) + ck;
             const float gb = gl[e];
             gw2 += gb * fmaxf(z, 0.0f);

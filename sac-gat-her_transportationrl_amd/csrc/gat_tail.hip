@@ -623,12 +623,12 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
                 float part = 0.0f;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    float ew = 0.0f;
+                    float ew = 0.0f;  // edge_head_infer_kernel's fused multiply-adds, same order
 #pragma unroll
                     for (int j = 0; j < kTED; ++j)
-                        if (j < D) ew += ear[j] * we_r[r][j];
+                        if (j < D) ew = __builtin_fmaf(ear[j], we_r[r][j], ew);
                     const float z = ((psv[r] + pdv[r]) + ew) + c_r[r];   // fp32 after the p GEMM
-                    part += fmaxf(z, 0.0f) * w2_r[r];
+                    part = __builtin_fmaf(fmaxf(z, 0.0f), w2_r[r], part);
                 }
                 part = t_row_sum16(part);
                 if (sl == 0 && e < E) tsum[4 * v + b] = part;
