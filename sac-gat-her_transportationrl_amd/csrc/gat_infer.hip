@@ -401,7 +401,9 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(const NetList<trx_g
     TRX_ISTAMP(4);
 
     // 4. aggregation + epilogue, one wave per node; lane owns chunks q = lane + 64k.
-    //    Per-column constants live in registers across the wave's nodes.
+    //    Per-column constants live in registers across the wave's nodes.  The
+    //    weighted sums and the LayerNorm affine are fused multiply-adds (one
+    //    rounding each; the backward reads the saved pre-LN rows, not a recompute).
     float bias_r[KC][4], lnw_r[KC][4], lnb_r[KC][4];
     float wp_r[KC][4][IN > 0 ? IN : 1], bp_r[KC][4];
 #pragma unroll
@@ -453,10 +455,10 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(const NetList<trx_g
                 for (int k = 0; k < KC; ++k) {
                     const float w = wk[k & 3];
                     const float4 x4 = xld4<XF>(row + 4 * (lane + kWave * k));
-                    acc[k].x += w * x4.x;
-                    acc[k].y += w * x4.y;
-                    acc[k].z += w * x4.z;
-                    acc[k].w += w * x4.w;
+                    acc[k].x = __builtin_fmaf(w, x4.x, acc[k].x);
+                    acc[k].y = __builtin_fmaf(w, x4.y, acc[k].y);
+                    acc[k].z = __builtin_fmaf(w, x4.z, acc[k].z);
+                    acc[k].w = __builtin_fmaf(w, x4.w, acc[k].w);
                 }
             }
         } else {
@@ -468,10 +470,10 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(const NetList<trx_g
                     const int q = lane + kWave * k;
                     const float w = alr[(4 * q) / C];
                     const float4 x4 = xld4<XF>(row + 4 * q);
-                    acc[k].x += w * x4.x;
-                    acc[k].y += w * x4.y;
-                    acc[k].z += w * x4.z;
-                    acc[k].w += w * x4.w;
+                    acc[k].x = __builtin_fmaf(w, x4.x, acc[k].x);
+                    acc[k].y = __builtin_fmaf(w, x4.y, acc[k].y);
+                    acc[k].z = __builtin_fmaf(w, x4.z, acc[k].z);
+                    acc[k].w = __builtin_fmaf(w, x4.w, acc[k].w);
                 }
             }
         }
@@ -515,7 +517,7 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(const NetList<trx_g
             float y4[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                float y = lnw_r[k][r] * (rstd * (v[k][r] - mean)) + lnb_r[k][r];
+                float y = __builtin_fmaf(lnw_r[k][r], rstd * (v[k][r] - mean), lnb_r[k][r]);
                 if (IN > 0 && a.residual == 2) {
                     float t = 0.0f;
 #pragma unroll

@@ -440,10 +440,10 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
         }
         float acc4[4] = {0.f, 0.f, 0.f, 0.f};
         auto fma_row = [&](uint2 u, float w) {
-            acc4[0] += w * lo_bf(u.x);
-            acc4[1] += w * hi_bf(u.x);
-            acc4[2] += w * lo_bf(u.y);
-            acc4[3] += w * hi_bf(u.y);
+            acc4[0] = __builtin_fmaf(w, lo_bf(u.x), acc4[0]);  // the layer kernel's fused multiply-adds
+            acc4[1] = __builtin_fmaf(w, hi_bf(u.x), acc4[1]);
+            acc4[2] = __builtin_fmaf(w, lo_bf(u.y), acc4[2]);
+            acc4[3] = __builtin_fmaf(w, hi_bf(u.y), acc4[3]);
         };
         int e = 0;
         for (; e + 4 <= deg; e += 4) {  // four rows in flight, summed in CSR order
@@ -478,7 +478,7 @@ __global__ void __launch_bounds__(kTThreads) gat_tail_kernel(trx_gat_tail_args a
         const float rstd = rsqrtf(t_wave_sum(s2) / (float)kTC + a.ln_eps);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            float y = lnw_r[r] * (rstd * (v[r] - mean)) + lnb_r[r];
+            float y = __builtin_fmaf(lnw_r[r], rstd * (v[r] - mean), lnb_r[r]);
             y = y <= 0.0f ? (expf(y) - 1.0f) : y;
             ysv[j][r] = y;
             if (!par) {
