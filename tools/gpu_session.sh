@@ -61,6 +61,9 @@ for s in "$@"; do
         pmcenv) pmc4 pmcenv python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu &&
                 python tools/pmc_summary.py r05_sf "pmcenv_p*" env_kernel > gpurun_out/pmcenv_summary.log 2>&1
                 cp profiles/r05_sf_pmc.json gpurun_out/; rm -rf gpurun_out/pmcenv_p* ;;
+        pmcana) pmc4 pmcana python3 bench.py --network anaheim --steps 6 --warmup 2 --no-cpu &&
+                python tools/pmc_summary.py r05_ana "pmcana_p*" env_kernel_big > gpurun_out/pmcana_summary.log 2>&1
+                cp profiles/r05_ana_pmc.json gpurun_out/; rm -rf gpurun_out/pmcana_p* ;;
         pmcact) pmc4 pmcact python3 tools/agent_profile.py 4096 act &&
                 python tools/pmc_summary.py r05_act "pmcact_p*" gat_layer gat_mid edge_head gat_prologue Cijk > gpurun_out/pmcact_summary.log 2>&1
                 cp profiles/r05_act_pmc.json gpurun_out/; rm -rf gpurun_out/pmcact_p* ;;
