@@ -500,8 +500,11 @@ __global__ void __launch_bounds__(NT) gat_layer_infer_kernel(const NetList<trx_g
         if (a.save_v) {
 #pragma unroll
             for (int k = 0; k < KC; ++k)
-                *reinterpret_cast<float4*>(a.save_v + (size_t)node * HC + 4 * (lane + kWave * k)) =
-                    make_float4(v[k][0], v[k][1], v[k][2], v[k][3]);
+            {  // read back only by the backward, much later: non-temporal, past the caches
+                typedef float trx_f4v __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store((trx_f4v){v[k][0], v[k][1], v[k][2], v[k][3]},
+                                            reinterpret_cast<trx_f4v*>(a.save_v + (size_t)node * HC + 4 * (lane + kWave * k)));
+            }
         }
         if (a.save_stats && lane == 0) {
             a.save_stats[2 * (size_t)node] = mean;
