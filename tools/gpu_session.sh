@@ -119,6 +119,9 @@ for s in "$@"; do
         fmatests) step fma_tests 900 python -u -m pytest tests/test_gat_infer.py tests/test_gat_tail.py tests/test_sac_e2e.py tests/test_fused_update.py tests/test_gat.py tests/test_sac.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         wsplit) step wsplit 300 python tools/wgrad3_split.py ;;
         updab) for r in 1 2; do for L in libtrafficrl libtrafficrl_${VAR:-x}; do TRX_LIB=sac-gat-her_transportationrl_amd/trafficrl/$L.so step upd_ab_${L}_$r 300 python tools/upd_time.py || exit 1; echo "$L $(tail -1 gpurun_out/upd_ab_${L}_$r.log)" >> gpurun_out/updab_summary.txt; done; done ;;
+        actab) T=sac-gat-her_transportationrl_amd/trafficrl
+               for r in 1 2; do for L in libtrafficrl libtrafficrl_${VAR:-x}; do
+                   TRX_LIB=$T/$L.so step actab_${L}_$r 300 rocprofv3 --kernel-trace --stats -d gpurun_out/actab_${L}_$r -o run --output-format csv -- python3 tools/agent_profile.py 4096 act || exit 1; done; done ;;
         disttests) step dist_tests 600 python -u -m pytest tests/test_dist_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
         dist2) step bench_dist2 600 env TRX_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 44 --warmup 22 --no-cpu ;;
         branchprobe) step branch_probe3 300 python tools/branch_probe.py 3 && step branch_probe6 300 python tools/branch_probe.py 6 ;;
