@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define TRX_ABI_VERSION 11  /* 11: *_multi entry points (several networks' passes per launch);
+#define TRX_ABI_VERSION 12  /* 12: trx_bf16_round modes 16..23 (a three-piece split from one read);
+                                 11: *_multi entry points (several networks' passes per launch);
                                  10: `exact` (float32) mode of the fused forward/backward kernels;
                                   9: fp32 edge scorer after its p GEMM; trx_gat_layer0_* */
 
@@ -804,7 +805,12 @@ int trx_graph_pool_backward(int32_t B, int32_t n, int32_t F, const float* x, con
  * (src rows x cols float32 with row stride src_stride; dst rows dst_stride apart;
  * out_bf16[k] = 1: bf16 bits, 0: the bf16-rounded value as float32, 2: the
  * float32 value unrounded -- a plain strided copy, 3 (ABI 10): bf16 bits of
- * the remainder x - bf16(x), the low half of a two-term split x ~ hi + lo).
+ * the remainder x - bf16(x), the low half of a two-term split x ~ hi + lo),
+ * 16 + b (ABI 12): the three bf16 pieces of a split GEMM operand from one read
+ * of x -- piece p is the remainder when bit p of b is set, else bf16(x); the
+ * pieces lie cols elements apart when dst_stride > 0 (side by side in each
+ * row; dst_stride >= 3 cols) and rows x cols elements apart when it is 0
+ * (stacked blocks).
  * Used to prepare the small weight blocks of the fused inference passes and
  * the split operands of the update's three-product float32 GEMMs.          */
 #define TRX_MAX_ROUND 48  /* ABI 11: 48 (was 16): every weight block of five networks in one launch */

@@ -1079,7 +1079,8 @@ int trx_bf16_round(const trx_round_list* l, void* stream) {
     if (!l || l->count < 0 || l->count > TRX_MAX_ROUND) return fail(TRX_EINVAL, "bf16_round: count must be 0..%d", TRX_MAX_ROUND);
     for (int k = 0; k < l->count; ++k)
         if (!l->src[k] || !l->dst[k] || l->rows[k] < 0 || l->cols[k] < 0 || l->src_stride[k] < l->cols[k] ||
-            l->out_bf16[k] < 0 || l->out_bf16[k] > 3 || (l->dst_stride[k] != 0 && l->dst_stride[k] < l->cols[k]))
+            l->out_bf16[k] < 0 || (l->out_bf16[k] > 3 && (l->out_bf16[k] < 16 || l->out_bf16[k] > 23)) ||
+            (l->dst_stride[k] != 0 && l->dst_stride[k] < (l->out_bf16[k] >= 16 ? 3 : 1) * l->cols[k]))
             return fail(TRX_EINVAL, "bf16_round: bad entry %d", k);
     if (l->count == 0) return TRX_OK;
     hipError_t e = trx::launch_bf16_round(*l, static_cast<hipStream_t>(stream));

@@ -80,11 +80,45 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
     const int64_t ss = l.src_stride[k];
     const uint32_t ds = l.dst_stride[k] > 0 ? (uint32_t)l.dst_stride[k] : cols;  // dst row stride (elements)
     // 0 bf16-rounded float32, 1 bf16 bits, 2 exact float32 copy, 3 bf16 bits of the
-    // remainder x - bf16(x) (the low half of a two-term bf16 split)
+    // remainder x - bf16(x) (the low half of a two-term bf16 split); 16 + bits: the
+    // three pieces of a split operand from one read of x (piece p = the remainder
+    // when bit p is set, else bf16(x)), pieces `poff` elements apart
     const int mode = l.out_bf16[k];
     const bool bf = mode == 1 || mode == 3;
     auto lo = [](float x, __bf16 h) -> __bf16 { return (__bf16)(x - (float)h); };
     const uint32_t step = gridDim.x * 256u;
+    auto pk = [](__bf16 a, __bf16 b) -> uint32_t {
+        return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+    };
+    if (mode >= 16) {
+        const uint32_t poff = l.dst_stride[k] > 0 ? cols : n;
+        uint16_t* dst = static_cast<uint16_t*>(l.dst[k]);
+        if ((cols & 3u) == 0 && (ss & 3) == 0 && (ds & 3u) == 0 && (poff & 3u) == 0 && ((uintptr_t)src & 15) == 0 &&
+            ((uintptr_t)dst & 7) == 0) {
+            for (uint32_t q = blockIdx.x * 256u + threadIdx.x; 4 * q < n; q += step) {
+                const uint32_t i0 = 4 * q, r = i0 / cols, c = i0 - r * cols, i = r * ds + c;
+                const float4 v = *reinterpret_cast<const float4*>(src + r * ss + c);
+                const __bf16 h0 = (__bf16)v.x, h1 = (__bf16)v.y, h2 = (__bf16)v.z, h3 = (__bf16)v.w;
+                uint2 uh, ul;
+                uh.x = pk(h0, h1);
+                uh.y = pk(h2, h3);
+                ul.x = pk(lo(v.x, h0), lo(v.y, h1));
+                ul.y = pk(lo(v.z, h2), lo(v.w, h3));
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    *reinterpret_cast<uint2*>(dst + i + p * poff) = (mode >> p) & 1 ? ul : uh;
+            }
+            return;
+        }
+        for (uint32_t i0 = blockIdx.x * 256u + threadIdx.x; i0 < n; i0 += step) {
+            const uint32_t r = i0 / cols, c = i0 - r * cols, i = r * ds + c;
+            const float x = src[r * ss + c];
+            const __bf16 h = (__bf16)x, w = lo(x, h);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) dst[i + p * poff] = __builtin_bit_cast(uint16_t, (mode >> p) & 1 ? w : h);
+        }
+        return;
+    }
     if ((cols & 3u) == 0 && (ss & 3) == 0 && (ds & 3u) == 0 && ((uintptr_t)src & 15) == 0 &&
         ((uintptr_t)l.dst[k] & 15) == 0) {
         for (uint32_t q = blockIdx.x * 256u + threadIdx.x; 4 * q < n; q += step) {
@@ -100,8 +134,8 @@ __global__ void __launch_bounds__(256) bf16_round_kernel(trx_round_list l) {
             }
             if (bf) {
                 uint2 u;
-                u.x = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-                u.y = (uint32_t)__builtin_bit_cast(uint16_t, h2) | ((uint32_t)__builtin_bit_cast(uint16_t, h3) << 16);
+                u.x = pk(h0, h1);
+                u.y = pk(h2, h3);
                 *reinterpret_cast<uint2*>(static_cast<uint16_t*>(l.dst[k]) + i) = u;
             } else if (mode == 2) {
                 *reinterpret_cast<float4*>(static_cast<float*>(l.dst[k]) + i) = v;
@@ -128,7 +162,7 @@ hipError_t launch_bf16_round(const trx_round_list& l, hipStream_t stream) {
     int64_t mx = 1;
     for (int k = 0; k < l.count; ++k) {
         const int64_t n = l.rows[k] * l.cols[k];
-        if (n >= ((int64_t)1 << 31) || l.rows[k] * l.src_stride[k] >= ((int64_t)1 << 31) ||
+        if ((l.out_bf16[k] >= 16 ? 3 * n : n) >= ((int64_t)1 << 31) || l.rows[k] * l.src_stride[k] >= ((int64_t)1 << 31) ||
             l.rows[k] * l.dst_stride[k] >= ((int64_t)1 << 31))
             return hipErrorInvalidValue;
         mx = n > mx ? n : mx;

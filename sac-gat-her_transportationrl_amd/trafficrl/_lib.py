@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("TRX_LIB") or os.path.join(_HERE, "libtrafficrl.so")
 
 TRX_OK, TRX_EINVAL, TRX_EHIP, TRX_EUNSUP = 0, -1, -2, -3
 METHODS = {"msa": 0, "fw": 1, "cfw": 2, "gp": 3}
-ABI_VERSION = 11
+ABI_VERSION = 12
 SP_SCIPY, SP_TORCH = 0, 1   # TRX_SP_* (include/trafficrl.h)
 REWARD_MODES = {"delta": 0, "log_delta": 1, "neg_tstt": 2, "minimize_tstt": 3, "rel_improve": 4}
 

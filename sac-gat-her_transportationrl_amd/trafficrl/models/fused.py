@@ -168,30 +168,30 @@ def split3(specs):
     specs: [(x, layout, order)] with x float32 [R, C] (unit column stride),
     layout "cols" -> [R, 3C] (pieces side by side: contraction over columns)
     or "rows" -> [3R, C] (stacked: contraction over rows), order a 3-letter
-    string of h / l.  One trx_bf16_round launch per 5 specs."""
+    string of h / l.  One trx_bf16_round entry per spec (mode 16 + the
+    order's remainder bits: x is read once for its three pieces), up to
+    _lib.MAX_ROUND specs per launch."""
     L = _lib.load()
     outs = []
-    for b0 in range(0, len(specs), 5):
+    for b0 in range(0, len(specs), _lib.MAX_ROUND):
         lst = _lib.TrxRoundList()
-        e = 0
         dev = None
-        for x, layout, order in specs[b0:b0 + 5]:
+        chunk = specs[b0:b0 + _lib.MAX_ROUND]
+        for e, (x, layout, order) in enumerate(chunk):
             x = x.detach()
             assert x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1 and len(order) == 3
+            assert set(order) <= {"h", "l"}
             R, C = x.shape
             cols = layout == "cols"
             out = torch.empty((R, 3 * C) if cols else (3 * R, C), device=x.device, dtype=torch.bfloat16)
-            for k, ch in enumerate(order):
-                lst.out_bf16[e] = 1 if ch == "h" else 3
-                lst.rows[e], lst.cols[e] = R, C
-                lst.src_stride[e] = x.stride(0)
-                lst.src[e] = x.data_ptr()
-                lst.dst[e] = out.data_ptr() + 2 * (k * C if cols else k * R * C)
-                lst.dst_stride[e] = 3 * C if cols else 0
-                e += 1
+            lst.out_bf16[e] = 16 + sum(1 << p for p, ch in enumerate(order) if ch == "l")
+            lst.rows[e], lst.cols[e] = R, C
+            lst.src_stride[e] = x.stride(0)
+            lst.src[e], lst.dst[e] = x.data_ptr(), out.data_ptr()
+            lst.dst_stride[e] = 3 * C if cols else 0
             outs.append(out)
             dev = x.device
-        lst.count = e
+        lst.count = len(chunk)
         _lib.check(L.trx_bf16_round(lst, _lib.stream_ptr(dev)), "trx_bf16_round")
     return outs
 

@@ -35,7 +35,7 @@ def test_exports_every_declared_symbol():
     assert set(syms) == set(_lib.EXPORTS)
     for s in syms:
         assert hasattr(L, s), s
-    assert L.trx_abi_version() == _lib.ABI_VERSION == 11
+    assert L.trx_abi_version() == _lib.ABI_VERSION == 12
 
 
 def test_struct_layout_matches_header(tmp_path):

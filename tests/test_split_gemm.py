@@ -23,6 +23,25 @@ def test_split3_pieces_exact():
     assert rel < 2 ** -15
 
 
+@pytest.mark.parametrize("cols", [64, 63])
+def test_split3_every_order_and_layout(cols):
+    """Mode 16 + bits (ABI 12): every piece order, both layouts, the vector
+    path (cols % 4 == 0) and the scalar one, from a row-strided view."""
+    from trafficrl.models import fused
+    torch.manual_seed(3)
+    base = torch.randn(50, 80, device="cuda") * 7.0
+    x = base[:, 3:3 + cols] if cols % 4 else base[:, 8:8 + cols]
+    hi = x.bfloat16()
+    lo = (x - hi.float()).bfloat16()
+    orders = ["hhh", "hhl", "hlh", "lhh", "llh", "lhl", "hll", "lll"]
+    specs = [(x, lay, o) for o in orders for lay in ("cols", "rows")]
+    outs = fused.split3(specs)
+    for (_, lay, o), out in zip(specs, outs):
+        for p, ch in enumerate(o):
+            piece = out[:, p * cols:(p + 1) * cols] if lay == "cols" else out[p * 50:(p + 1) * 50]
+            assert torch.equal(piece, lo if ch == "l" else hi), (lay, o, p)
+
+
 def test_tripled_contraction_gemm_and_split_k():
     from trafficrl.models import fused
     from trafficrl.rl import fused_update as FU

@@ -39,7 +39,7 @@ def run(n=12):
 
 
 def short(name):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
     if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
         mt = [p for p in name.split("_") if p.startswith("MT")]
         return "GEMM " + (mt[0] if mt else "")
