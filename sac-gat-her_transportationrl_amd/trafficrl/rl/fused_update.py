@@ -615,7 +615,8 @@ def net_backward_multi(nets, cxs: List[NetCtx], g_logits: List[torch.Tensor], to
                 torch.sum(part_w, 0, dtype=torch.float32, out=gw)
                 _grad(lw, gw)
                 # a middle layer's input also reaches it as the float32 residual
-                gy.append(_mm32(g_xh[j], grp.W[i - 1][j], None if last else g_res[j]))
+                gy.append(_mm32(g_xh[j], grp.W[i - 1][j]) if last else
+                          _mm3(g_xh[j], grp.W[i - 1][j], g_res[j], out=g_res[j]))   # in place: no addend copy
             g_pool = None
     # ---- prologue (input LayerNorms, loop attrs, edge-logit projections)
     A = cxs[0].a_all.shape[1]
@@ -872,10 +873,10 @@ def net_backward(net, cx: NetCtx, g_logits: torch.Tensor, topo: Topology, sink: 
             _grad(l.lin.weight, gw)
             # the previous layer's output reaches this layer twice: bf16 through lin,
             # fp32 as the residual of a middle layer (gat_encoder.py:44-46)
-            if exact:
-                gy_f32 = _mm3(gx_c, rec["w"], g_res if ba.residual == 1 else None)   # g_xh W (+ residual)
-            else:
-                gy_f32 = _mm32(g_xh, rec["w"], g_res if ba.residual == 1 else None)
+            # (+ residual): accumulated in place into g_res -- addmm into a fresh
+            # output first copies the [N, HC] float32 addend (a 25 MB device copy)
+            a3 = gx_c if exact else g_xh
+            gy_f32 = _mm3(a3, rec["w"], g_res, out=g_res) if ba.residual == 1 else _mm3(a3, rec["w"])   # g_xh W
             gy_b16 = None
             g_pool = None
     # ---- prologue: input LayerNorms, loop attrs, edge-logit projections

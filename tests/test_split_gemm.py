@@ -61,6 +61,22 @@ def test_tripled_contraction_gemm_and_split_k():
     assert float((out.double() - ref).abs().max() / ref.abs().max()) < 2e-5
 
 
+def test_inplace_residual_addmm_bit_identical():
+    """The backward's g_xh W + g_res accumulated in place (out = the addend)
+    equals the copying addmm bit for bit, at the update's actor shapes."""
+    from trafficrl.rl import fused_update as FU
+    torch.manual_seed(4)
+    FU.probe_mm32(torch.device("cuda"))
+    for (n, k, m) in ((6144, 3072, 1024), (6144, 1024, 1024), (500, 96, 40)):
+        a = torch.randn(n, k, device="cuda").bfloat16()
+        b = torch.randn(k, m, device="cuda").bfloat16()
+        add = torch.randn(n, m, device="cuda")
+        ref = FU._mm32(a, b, add)
+        acc = add.clone()
+        got = FU._mm3(a, b, acc, out=acc)
+        assert got.data_ptr() == acc.data_ptr() and torch.equal(acc, ref), (n, k, m)
+
+
 def test_partial_sum_multi_matches_single():
     from trafficrl import _lib
     from trafficrl.rl.fused_update import PartialSums
