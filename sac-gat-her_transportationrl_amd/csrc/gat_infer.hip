@@ -1077,7 +1077,7 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(const NetLis
     float* eal = dzs + (size_t)E * Hd;                                  // [E][ED] link features
     float* gl = eal + (size_t)E * ED;                                   // [E] grad logit
     float* red = gl + E;                                                // [P][2 + ED][256] per-part sums
-    float* wes = red + P * (2 + ED) * 256;                              // [256][ED] link-feature weights
+    float* wes = red + P * (2 + ED) * 256;                              // [ED][256] link-feature weights
     int* sl = reinterpret_cast<int*>(wes + 256 * ED);                   // [E]
     int* dl = sl + E;                                                   // [E]
     int* lo = dl + E;                                                   // [E] links by source node, link order
@@ -1110,7 +1110,7 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(const NetLis
     for (int j = 0; j < ED; ++j) we[j] = (on && j < D) ? a.we[k * D + j] : 0.0f;
     if (part == 0)
 #pragma unroll
-        for (int j = 0; j < ED; ++j) wes[k * ED + j] = we[j];
+        for (int j = 0; j < ED; ++j) wes[j * 256 + k] = we[j];   // unit-major per feature: (3) reads it conflict-free
     const float w2 = on ? a.w2[k] : 0.0f, ck = on ? a.c[(int64_t)g * Hd + k] : 0.0f;
     __syncthreads();
     if (tid < n) {  // per-node link lists (link order); counts first
@@ -1186,7 +1186,7 @@ __global__ void __launch_bounds__(kEhbThreads) edge_head_bwd_kernel(const NetLis
             for (int kk = ln; kk < Hd; kk += 64) {
                 const float dz = dzs[e * Hd + kk];
 #pragma unroll
-                for (int j = 0; j < ED; ++j) s[j] += dz * wes[kk * ED + j];
+                for (int j = 0; j < ED; ++j) s[j] += dz * wes[j * 256 + kk];
             }
 #pragma unroll
             for (int j = 0; j < ED; ++j) {
