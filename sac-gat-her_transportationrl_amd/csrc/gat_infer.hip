@@ -814,7 +814,8 @@ __global__ void __launch_bounds__(kWave) edge_att_weights_kernel(const NetList<t
     if (lane == 0) a.m_work[(row0 + h) * D + j] = s;
 }
 
-constexpr int kProMD = 8;  // node_dim, edge_dim <= 8; LDS rows padded to 8 floats
+constexpr int kProMD = 8;  // node_dim, edge_dim <= 8 (register rows)
+constexpr int kProLS = 9;  // LDS row stride of the per-link / per-node rows: odd, so a wave's rows hit distinct banks
 
 // x[0..d) -> LayerNorm (biased variance, like torch); compile-time bounded loops
 __device__ __forceinline__ void layer_norm_row(float (&x)[kProMD], int d, const float* w, const float* b, float eps) {
@@ -849,9 +850,10 @@ __global__ void __launch_bounds__(NT) gat_prologue_kernel(const NetList<trx_gat_
     constexpr int MD = kProMD;
     const int g = blockIdx.x, tid = threadIdx.x;
     const int n = a.nodes_per_graph, E = a.edges_per_graph, ND = a.node_dim, D = a.edge_dim;
-    float* ean = reinterpret_cast<float*>(smem);  // [E][8] normalised link features
-    float* lp = ean + E * MD;                     // [n][8] self-loop attrs
-    float* Ml = lp + n * MD;                      // [A][8] bf16-rounded M rows
+    constexpr int LS = kProLS;
+    float* ean = reinterpret_cast<float*>(smem);  // [E][LS] normalised link features
+    float* lp = ean + E * LS;                     // [n][LS] self-loop attrs
+    float* Ml = lp + n * LS;                      // [A][8] bf16-rounded M rows (broadcast reads)
     const int64_t node0 = (int64_t)g * n, link0 = (int64_t)g * E;
     const int p0 = a.rowptr[node0], p1 = a.rowptr[node0 + n];
     for (int v = tid; v < A * D; v += NT) {
@@ -866,7 +868,7 @@ __global__ void __launch_bounds__(NT) gat_prologue_kernel(const NetList<trx_gat_
 #pragma unroll
         for (int j = 0; j < MD; ++j)
             if (j < D) {
-                ean[l * MD + j] = x[j];
+                ean[l * LS + j] = x[j];
                 a.ea[(link0 + l) * D + j] = x[j];
             }
     }
@@ -892,19 +894,19 @@ __global__ void __launch_bounds__(NT) gat_prologue_kernel(const NetList<trx_gat_
             ++cnt;
 #pragma unroll
             for (int j = 0; j < MD; ++j)
-                if (j < D) s[j] += ean[li * MD + j];
+                if (j < D) s[j] += ean[li * LS + j];
         }
         const float deg = cnt > 0 ? (float)cnt : 1.0f;
 #pragma unroll
         for (int j = 0; j < MD; ++j)
-            if (j < D) lp[i * MD + j] = s[j] / deg;
+            if (j < D) lp[i * LS + j] = s[j] / deg;
     }
     __syncthreads();
     for (int p = p0 + tid; p < p1; p += NT) {
         const int code = a.pos_src[p];
         const int64_t li = (int64_t)code - link0, ni = -(int64_t)code - 1 - node0;
         const bool ok = code >= 0 ? (li >= 0 && li < E) : (ni >= 0 && ni < n);
-        const float* fr = code >= 0 ? ean + (ok ? li : 0) * MD : lp + (ok ? ni : 0) * MD;
+        const float* fr = code >= 0 ? ean + (ok ? li : 0) * LS : lp + (ok ? ni : 0) * LS;
         float f[MD];
 #pragma unroll
         for (int j = 0; j < MD; ++j) f[j] = j < D ? (a.exact ? fr[j] : bf16r(fr[j])) : 0.0f;
@@ -921,7 +923,7 @@ __global__ void __launch_bounds__(NT) gat_prologue_kernel(const NetList<trx_gat_
 size_t gat_prologue_smem(const trx_gat_prologue_args& a) {
     int A = 0;
     for (int l = 0; l < a.num_layers; ++l) A += a.heads[l];
-    return ((size_t)a.edges_per_graph * kProMD + (size_t)a.nodes_per_graph * kProMD + (size_t)A * kProMD +
+    return ((size_t)a.edges_per_graph * kProLS + (size_t)a.nodes_per_graph * kProLS + (size_t)A * kProMD +
             a.edges_per_graph) * 4;
 }
 

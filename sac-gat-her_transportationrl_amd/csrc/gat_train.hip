@@ -687,6 +687,7 @@ hipError_t launch_edge_att_weights_bwd(const trx_gat_prologue_args& a, const flo
 // width 8A + 32): [0, 8A) dL/dMl (rows of 8), then edge LN weight / bias,
 // node LN weight / bias (8 each).
 constexpr int kPD = 8;
+constexpr int kPLS = 9;  // LDS row stride of the per-link / per-node rows
 
 __device__ __forceinline__ void ln_fwd_row(float (&x)[kPD], int d, const float* w, const float* b, float eps,
                                            float (&xhat)[kPD]) {
@@ -718,12 +719,13 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<tr
     constexpr int MD = kPD, NW = kPBT / kW;
     const int g = blockIdx.x, tid = threadIdx.x, lane = tid & (kW - 1), wave = tid / kW;
     const int n = a.nodes_per_graph, E = a.edges_per_graph, ND = a.node_dim, D = a.edge_dim, A = a.A;
-    float* ean = reinterpret_cast<float*>(smem);  // [E][8] normalised link features
-    float* exh = ean + E * MD;                    // [E][8] their xhat
-    float* gea = exh + E * MD;                    // [E][8] dL/dea
-    float* lp = gea + E * MD;                     // [n][8] loop attrs
-    float* glp = lp + n * MD;                     // [n][8] dL/dloop
-    float* Ml = glp + n * MD;                     // [A][8]
+    constexpr int LS = kPLS;                      // odd LDS row stride: a wave's rows on distinct banks
+    float* ean = reinterpret_cast<float*>(smem);  // [E][LS] normalised link features
+    float* exh = ean + E * LS;                    // [E][LS] their xhat
+    float* gea = exh + E * LS;                    // [E][LS] dL/dea
+    float* lp = gea + E * LS;                     // [n][LS] loop attrs
+    float* glp = lp + n * LS;                     // [n][LS] dL/dloop
+    float* Ml = glp + n * LS;                     // [A][8] (broadcast reads)
     float* dg = Ml + A * MD;                      // [n] kept in-degree
     int* ld = reinterpret_cast<int*>(dg + n);     // [E] local dst of kept links, else -1
     const int64_t node0 = (int64_t)g * n, link0 = (int64_t)g * E;
@@ -741,9 +743,9 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<tr
         const int64_t s = a.src[link0 + l] - node0, d = a.dst[link0 + l] - node0;
 #pragma unroll
         for (int j = 0; j < MD; ++j) {
-            ean[l * MD + j] = x[j];
-            exh[l * MD + j] = xh[j];
-            gea[l * MD + j] = (a.g_ea_head && j < D) ? a.g_ea_head[(link0 + l) * D + j] : 0.0f;
+            ean[l * LS + j] = x[j];
+            exh[l * LS + j] = xh[j];
+            gea[l * LS + j] = (a.g_ea_head && j < D) ? a.g_ea_head[(link0 + l) * D + j] : 0.0f;
         }
         ld[l] = (s == d || d < 0 || d >= n) ? -1 : (int)d;
     }
@@ -760,14 +762,14 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<tr
             if (code < 0 || li < 0 || li >= E) continue;
             ++cnt;
 #pragma unroll
-            for (int j = 0; j < MD; ++j) s[j] += ean[li * MD + j];
+            for (int j = 0; j < MD; ++j) s[j] += ean[li * LS + j];
         }
         const float deg = cnt > 0 ? (float)cnt : 1.0f;
         dg[i] = deg;
 #pragma unroll
         for (int j = 0; j < MD; ++j) {
-            lp[i * MD + j] = j < D ? s[j] / deg : 0.0f;
-            glp[i * MD + j] = 0.0f;
+            lp[i * LS + j] = j < D ? s[j] / deg : 0.0f;
+            glp[i * LS + j] = 0.0f;
         }
     }
     __syncthreads();
@@ -784,7 +786,7 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<tr
 #pragma unroll
             for (int j = 0; j < MD; ++j) gf[j] += gk * Ml[k * MD + j];
         }
-        float* dstg = code >= 0 ? gea + li * MD : glp + ni * MD;
+        float* dstg = code >= 0 ? gea + li * LS : glp + ni * LS;
 #pragma unroll
         for (int j = 0; j < MD; ++j) dstg[j] += gf[j];
     }
@@ -795,7 +797,7 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<tr
         for (int j = 0; j < MD; ++j) gm[j] = 0.0f;
         for (int p = p0 + lane; p < p1; p += kW) {
             const int code = a.pos_src[p];
-            const float* fr = code >= 0 ? ean + ((int64_t)code - link0) * MD : lp + (-(int64_t)code - 1 - node0) * MD;
+            const float* fr = code >= 0 ? ean + ((int64_t)code - link0) * LS : lp + (-(int64_t)code - 1 - node0) * LS;
             const float gk = a.g_a_edge[(size_t)p * A + k];
 #pragma unroll
             for (int j = 0; j < MD; ++j) gm[j] += gk * (j < D ? (a.exact ? fr[j] : rbf(fr[j])) : 0.0f);
@@ -815,9 +817,9 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<tr
             const int d = ld[l];
 #pragma unroll
             for (int j = 0; j < MD; ++j) {
-                float gj = gea[l * MD + j];
-                if (d >= 0) gj += glp[d * MD + j] / dg[d];
-                pw[j] += gj * exh[l * MD + j];
+                float gj = gea[l * LS + j];
+                if (d >= 0) gj += glp[d * LS + j] / dg[d];
+                pw[j] += gj * exh[l * LS + j];
                 pb[j] += gj;
             }
         }
@@ -855,7 +857,7 @@ __global__ void __launch_bounds__(kPBT) gat_prologue_bwd_kernel(const NetList<tr
 }
 
 size_t gat_prologue_bwd_smem(const trx_gat_prologue_bwd_args& a) {
-    return ((size_t)a.edges_per_graph * kPD * 3 + (size_t)a.nodes_per_graph * kPD * 2 + (size_t)a.A * kPD +
+    return ((size_t)a.edges_per_graph * kPLS * 3 + (size_t)a.nodes_per_graph * kPLS * 2 + (size_t)a.A * kPD +
             a.nodes_per_graph + a.edges_per_graph) * 4;
 }
 
