@@ -32,7 +32,10 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     const int tid = threadIdx.x;
     const int env0 = blockIdx.x * EPW;
     // LDS (sized so that 8 blocks of a 24-node graph share one CU):
-    //   delta[N][L] f64, sigma[N][L] u16, dist[N][L] u8 (0xff = unreached), queue[N][L] u8,
+    //   delta[N][L] f64, bfs[N][L] u32 packing a lane's dist (byte 0, 0xff = unreached),
+    //   queue entry (byte 1) and sigma (bytes 2-3) -- one dword per (row, lane), so the
+    //   byte / half-word accesses of a wave never share a bank (separate u8 / u16
+    //   arrays put four / two lanes' entries in one dword: 1.1 conflicts per access),
     //   odst[EPW][E] i8 (head of CSR out-slot k, -1 when that link is damaged),
     //   isrc[EPW][E] i8 (tail of CSR in-slot k, -1 when damaged), insub[EPW][N] u8, nsub[16] i32,
     //   out_ptr / in_ptr [N+1] and nx_order [N] as int16.
@@ -43,10 +46,13 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     // sum(level sizes) <= N-2, i.e. <= 3^10 = 59049 for N <= 32 -- exact in u16 and,
     // converted, the same float64 value networkx's float sigma holds.
     double* delta = reinterpret_cast<double*>(smem_raw);
-    uint16_t* sigma = reinterpret_cast<uint16_t*>(delta + (size_t)N * L);
-    uint8_t* dist = reinterpret_cast<uint8_t*>(sigma + (size_t)N * L);
-    uint8_t* queue = dist + (size_t)N * L;
-    int8_t* odst = reinterpret_cast<int8_t*>(queue + (size_t)N * L);
+    uint32_t* bfs = reinterpret_cast<uint32_t*>(delta + (size_t)N * L);
+    uint8_t* const bfs8 = reinterpret_cast<uint8_t*>(bfs);
+    uint16_t* const bfs16 = reinterpret_cast<uint16_t*>(bfs);
+    auto dist = [&](int v, int ln) -> uint8_t& { return bfs8[4 * (v * L + ln)]; };
+    auto queue = [&](int q) -> uint8_t& { return bfs8[4 * (q * L + tid) + 1]; };
+    auto sigma = [&](int v) -> uint16_t& { return bfs16[2 * (v * L + tid) + 1]; };
+    int8_t* odst = reinterpret_cast<int8_t*>(bfs + (size_t)N * L);
     int8_t* isrc = odst + (size_t)EPW * E;
     uint8_t* insub = reinterpret_cast<uint8_t*>(isrc + (size_t)EPW * E);
     int* nsub = reinterpret_cast<int*>(smem_raw + (((size_t)N * L * 12 + 2 * (size_t)EPW * E + EPW * N + 15) & ~size_t(15)));
@@ -87,43 +93,42 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
     const bool active_src = on && insub[lenv * N + src];
     if (on) {
         for (int v = 0; v < N; ++v) {
-            sigma[v * L + tid] = 0;
+            bfs[v * L + tid] = 0xffu;   // dist unreached, sigma 0
             delta[v * L + tid] = 0.0;
-            dist[v * L + tid] = 0xff;
         }
     }
     if (active_src) {
         const int8_t* od = odst + lenv * E;
         const int8_t* is = isrc + lenv * E;
-        sigma[src * L + tid] = 1;
-        dist[src * L + tid] = 0;
+        sigma(src) = 1;
+        dist(src, tid) = 0;
         int qh = 0, qt = 0;
-        queue[qt++ * L + tid] = (uint8_t)src;
+        queue(qt++) = (uint8_t)src;
         while (qh < qt) {
-            int v = queue[qh++ * L + tid];
-            int dv1 = dist[v * L + tid] + 1;
-            uint16_t sv = sigma[v * L + tid];
+            int v = queue(qh++);
+            int dv1 = dist(v, tid) + 1;
+            uint16_t sv = sigma(v);
             for (int k = gop[v], ke = gop[v + 1]; k < ke; ++k) {
                 int w = od[k];
                 if (w < 0) continue;  // only active links are in the subgraph
-                int dw = dist[w * L + tid];
+                int dw = dist(w, tid);
                 if (dw == 0xff) {
-                    queue[qt++ * L + tid] = (uint8_t)w;
-                    dist[w * L + tid] = (uint8_t)dv1;
+                    queue(qt++) = (uint8_t)w;
+                    dist(w, tid) = (uint8_t)dv1;
                     dw = dv1;
                 }
-                if (dw == dv1) sigma[w * L + tid] += sv;
+                if (dw == dv1) sigma(w) += sv;
             }
         }
         // _accumulate_basic: pop in reverse BFS order
         for (int q = qt - 1; q >= 0; --q) {
-            int w = queue[q * L + tid];
-            double coeff = (1.0 + delta[w * L + tid]) / (double)sigma[w * L + tid];
-            int dw1 = dist[w * L + tid] - 1;
+            int w = queue(q);
+            double coeff = (1.0 + delta[w * L + tid]) / (double)sigma(w);
+            int dw1 = dist(w, tid) - 1;
             for (int k = gip[w], ke = gip[w + 1]; k < ke; ++k) {
                 int v = is[k];
                 if (v < 0) continue;
-                if (dist[v * L + tid] == dw1) delta[v * L + tid] += (double)sigma[v * L + tid] * coeff;
+                if (dist(v, tid) == dw1) delta[v * L + tid] += (double)sigma(v) * coeff;
             }
         }
     }
@@ -131,7 +136,7 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
 
     // ---------------- per (env, node): betweenness, then per-env features
     // betweenness[w] = sum over sources s (nx order, s != w, w reached) of delta_s[w]
-    float* bwv = reinterpret_cast<float*>(sigma);  // reuse after the barrier below
+    float* bwv = reinterpret_cast<float*>(bfs);  // reuse after the barrier below
     float bw0 = 0.f, bw1 = 0.f;  // this thread's (at most 2) nodes, kept out of scratch
     int nloc = 0;
     for (int i = tid; i < EPW * N; i += L) {
@@ -142,7 +147,7 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
                 int s_ = gnx[jj];
                 int lane = el * N + jj;
                 if (s_ == w || !insub[el * N + s_]) continue;
-                if (dist[w * L + lane] == 0xff) continue;
+                if (dist(w, lane) == 0xff) continue;
                 bc += delta[w * L + lane];
             }
             int n = nsub[el];
@@ -253,7 +258,7 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
 static size_t observe_smem(const DevGraph& g, int epw) {
     size_t b = (((size_t)g.N * kObsThreads * 12 + 2 * (size_t)epw * g.E + (size_t)epw * g.N + 15) & ~size_t(15));
     b += 16 * 4 + ((size_t)3 * g.N + 2) * 2;
-    // bwv reuses sigma (epw*N floats <= N*L u16) and the feature scratch reuses
+    // bwv reuses the packed BFS words (epw*N floats <= N*L u32) and the feature scratch reuses
     // delta (epw*(E+8) floats <= N*L doubles), both checked at launch
     return b;
 }
