@@ -64,12 +64,19 @@ __global__ void __launch_bounds__(kObsThreads) observe_kernel(const DevGraph g, 
         gip[i] = (int16_t)g.in_ptr[i];
     }
     for (int i = tid; i < N; i += L) gnx[i] = (int16_t)g.nx_order[i];
+    // the envs' damaged flags staged first (coalesced, in link order), then the CSR slot
+    // tables from LDS: no slot -> link -> flag chain of dependent global loads.  delta is
+    // free until the Brandes initialisation below.
+    uint8_t* dmg = reinterpret_cast<uint8_t*>(delta);  // [EPW][E], 1 = damaged or no env
     for (int i = tid; i < EPW * E; i += L) {
-        int el = i / E, k = i - el * E, gb = env0 + el;
-        const float* dm = s.damaged + (size_t)(gb < B ? gb : 0) * E;
-        bool ok = gb < B;
-        odst[i] = ok && dm[g.out_eid[k]] == 0.0f ? (int8_t)g.out_dst[k] : (int8_t)-1;
-        isrc[i] = ok && dm[g.in_eid[k]] == 0.0f ? (int8_t)g.in_src[k] : (int8_t)-1;
+        const int el = i / E, k = i - el * E, gb = env0 + el;
+        dmg[i] = gb < B ? (uint8_t)(s.damaged[(size_t)gb * E + k] != 0.0f) : (uint8_t)1;
+    }
+    __syncthreads();
+    for (int i = tid; i < EPW * E; i += L) {
+        const int el = i / E, k = i - el * E;
+        odst[i] = dmg[el * E + g.out_eid[k]] ? (int8_t)-1 : (int8_t)g.out_dst[k];
+        isrc[i] = dmg[el * E + g.in_eid[k]] ? (int8_t)-1 : (int8_t)g.in_src[k];
     }
     __syncthreads();
     for (int i = tid; i < EPW * N; i += L) {
