@@ -158,3 +158,4 @@ for s in "$@"; do
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
+
