@@ -235,6 +235,8 @@ def env_kernel_name(env, big):
     """The env kernel trx_step launches for this workload (trx_env_kernel_name),
     with the template arguments of the Sioux Falls instantiation."""
     k = env.kernel_name
+    if k == "env_kernel_pair" and env.num_nodes == 24:
+        return "trx::env_kernel_pair<24, 3, true>"   # pair-per-tree Dijkstra (SF: max out-degree 5, every node reachable)
     if k == "env_kernel_s" and env.num_nodes == 24:
         return "trx::env_kernel_s<24, 2>"   # sparse-relaxation Dijkstra (SF: max out-degree 5)
     if k in ("env_kernel_t", "env_kernel_q") and env.num_nodes == 24:

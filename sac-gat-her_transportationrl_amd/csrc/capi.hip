@@ -92,16 +92,18 @@ int check_state(const trx_state* s, bool need_initial) {
 }
 
 // The env kernel a (graph, params) pair runs.  TRX_KERNEL=quad forces the
-// general quad kernel for both rules (A/B runs).
-enum EnvKernel { kEnvNone = 0, kEnvSparse, kEnvQuad, kEnvTorch, kEnvBig, kEnvGp };
+// general quad kernel for both rules, TRX_KERNEL=sparse the quad-per-tree
+// sparse kernel instead of the pair kernel (A/B runs, fallback tests).
+enum EnvKernel { kEnvNone = 0, kEnvSparse, kEnvQuad, kEnvTorch, kEnvBig, kEnvGp, kEnvPair };
 
-bool force_quad() {
-    static const bool q = [] {
+const std::string& kernel_override() {
+    static const std::string k = [] {
         const char* e = getenv("TRX_KERNEL");
-        return e && std::string(e) == "quad";
+        return std::string(e ? e : "");
     }();
-    return q;
+    return k;
 }
+bool force_quad() { return kernel_override() == "quad"; }
 
 EnvKernel select_env_kernel(const trx::DevGraph& g, const trx_params& p) {
     const bool small = g.N <= trx::kSmallMaxNodes;
@@ -109,6 +111,7 @@ EnvKernel select_env_kernel(const trx::DevGraph& g, const trx_params& p) {
     if (!small) return p.sp_rule == TRX_SP_SCIPY ? kEnvBig : kEnvNone;  // torch rule: N <= 32 only
     if (!force_quad()) {
         if (p.sp_rule == TRX_SP_TORCH && trx::torch_kernel_ok(g)) return kEnvTorch;
+        if (p.sp_rule == TRX_SP_SCIPY && kernel_override() != "sparse" && trx::pair_ok(g, p)) return kEnvPair;
         if (p.sp_rule == TRX_SP_SCIPY && trx::sparse_ok(g, p)) return kEnvSparse;
     }
     return trx::quad_ok(g, p.sp_rule) ? kEnvQuad : kEnvNone;
@@ -116,6 +119,7 @@ EnvKernel select_env_kernel(const trx::DevGraph& g, const trx_params& p) {
 
 const char* env_kernel_label(EnvKernel k) {
     switch (k) {
+        case kEnvPair: return "env_kernel_pair";
         case kEnvSparse: return "env_kernel_s";
         case kEnvQuad: return "env_kernel_q";
         case kEnvTorch: return "env_kernel_t";
@@ -147,6 +151,9 @@ int run(const trx_graph* g, const trx_params* p, int32_t B, trx_state* s, int mo
             break;
         case kEnvSparse:
             e = trx::launch_env_kernel_sparse(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, ws, st);
+            break;
+        case kEnvPair:
+            e = trx::launch_env_kernel_pair(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, st);
             break;
         case kEnvQuad:
             e = trx::launch_env_kernel_quad(g->dg, *p, *s, B, mode, action, reward, done, valid, env_mask, st);
@@ -423,6 +430,25 @@ int trx_graph_create(int32_t N, int32_t E, const int32_t* src, const int32_t* ds
     for (int u = 0; u < N; ++u) {
         d.max_out_deg = std::max(d.max_out_deg, out_ptr[u + 1] - out_ptr[u]);
         d.max_in_deg = std::max(d.max_in_deg, in_ptr[u + 1] - in_ptr[u]);
+    }
+    // every origin reaches every node: link costs stay finite (a damaged link costs
+    // 1e6, repair_env.py:677), so this is a property of the graph, and the pair
+    // kernel's trees then scan exactly N nodes (assign_pair.hip FULL)
+    d.reach_all = 0;
+    if (small) {
+        d.reach_all = 1;
+        for (int z = 0; z < Z && d.reach_all; ++z) {
+            std::vector<char> vis(N, 0);
+            std::vector<int> q{origins[z]};
+            vis[origins[z]] = 1;
+            for (size_t h = 0; h < q.size(); ++h)
+                for (int a = out_ptr[q[h]]; a < out_ptr[q[h] + 1]; ++a)
+                    if (!vis[out_dst[a]]) {
+                        vis[out_dst[a]] = 1;
+                        q.push_back(out_dst[a]);
+                    }
+            if ((int)q.size() != N) d.reach_all = 0;
+        }
     }
     int rc = TRX_OK;
     std::vector<int32_t> vsrc(src, src + E), vdst(dst, dst + E);

@@ -61,6 +61,7 @@ struct DevGraph {
     float max_t0, max_cap;      // RepairEnv.max_t0 / max_capacity
     float min_t0;               // smallest free-flow time (exact-label headroom, assign_sparse.hip)
     int max_out_deg, max_in_deg;  // largest out-/in-degree (sparse-relaxation kernel tables)
+    int reach_all;              // every origin reaches every node (N <= kSmallMaxNodes; env_kernel_pair FULL)
 };
 
 // Per-lane Fibonacci-heap state for the exact (scipy-order) SSSP fallback.
@@ -120,7 +121,8 @@ struct LaunchCfg {
 
 // Small-graph (N <= kSmallMaxNodes) env kernels, selected per graph and
 // parameters by capi.hip select_env_kernel():
-//   scipy rule: env_kernel_s (assign_sparse.hip) when sparse_ok(), else
+//   scipy rule: env_kernel_pair (assign_pair.hip) when pair_ok(), else
+//               env_kernel_s (assign_sparse.hip) when sparse_ok(), else
 //               env_kernel_q (assign_quad.hip, no exact-label / degree limits);
 //   torch rule: env_kernel_t (assign_torch.hip) when torch_kernel_ok(), else
 //               env_kernel_q's torch-rule instantiation.
@@ -133,6 +135,11 @@ hipError_t launch_env_kernel_sparse(const DevGraph& g, const trx_params& p, cons
                                     int mode, const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                     const uint8_t* env_mask, void* workspace, hipStream_t stream);
 size_t sparse_workspace_bytes(const DevGraph& g, int num_envs);  // exact-heap scratch, one FibLane per tree
+bool pair_ok(const DevGraph& g, const trx_params& p);
+LaunchCfg pair_launch_cfg(const DevGraph& g, int num_envs, int method);
+hipError_t launch_env_kernel_pair(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
+                                  const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
+                                  const uint8_t* env_mask, hipStream_t stream);
 hipError_t launch_env_kernel_quad(const DevGraph& g, const trx_params& p, const trx_state& s, int num_envs, int mode,
                                   const int32_t* action, double* reward, uint8_t* done, uint8_t* valid,
                                   const uint8_t* env_mask, hipStream_t stream);

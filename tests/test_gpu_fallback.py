@@ -107,7 +107,7 @@ def test_kernel_selection():
     from trafficrl.data import sioux_falls
     from trafficrl.env import VecRepairEnv
     sf = sioux_falls()
-    assert VecRepairEnv(sf, 2, device="cuda", reset=False, sp_backend="scipy").kernel_name == "env_kernel_s"
+    assert VecRepairEnv(sf, 2, device="cuda", reset=False, sp_backend="scipy").kernel_name == "env_kernel_pair"
     assert VecRepairEnv(sf, 2, device="cuda", reset=False, sp_backend="torch").kernel_name == "env_kernel_t"
     assert VecRepairEnv(sf, 2, device="cuda", reset=False, assignment_method="gp").kernel_name == "gp_kernel"
     for _, build, rules in CASES:
