@@ -52,6 +52,15 @@ __device__ unsigned long long trx_phase_cycles_w[8];
             stamp_prev_ = now_;                                             \
         }                                                                   \
     } while (0)
+// per-workgroup wall cycles (thread 0, kernel start -> end) of the last launch
+__device__ unsigned long long trx_wg_cycles_w[1 << 16];
+extern "C" int trx_debug_wg_cycles_w(unsigned long long* out, int n) {
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (n > (1 << 16)) n = 1 << 16;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_wg_cycles_w), sizeof(unsigned long long) * n) != hipSuccess)
+        return -2;
+    return 0;
+}
 extern "C" int trx_debug_phase_cycles_w(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -2;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(trx_phase_cycles_w), sizeof(unsigned long long) * 8) != hipSuccess)
@@ -260,8 +269,11 @@ static int pair_rounds(const DevGraph& g) {  // out-slots per lane: ceil(max out
     return r < 1 ? 1 : r;
 }
 
+// 4 waves/SIMD of register budget (<= 128 VGPRs): the 3 waves of each of a CU's 4
+// workgroups (Sioux Falls: 4 envs, 39.4 KB of LDS each) must find room on whichever
+// SIMDs they are dealt to, so that B = 4096 runs in one round on 256 CUs
 template <int NP, int RS, bool FULL>  // RS = out-slots per lane (2 RS per node); FULL: N == NP, every origin reaches every node
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, int EPW, int mode,
                 const int32_t* __restrict__ action, double* __restrict__ reward_out, uint8_t* __restrict__ done_out,
                 uint8_t* __restrict__ valid_out, const uint8_t* __restrict__ env_mask) {
@@ -299,6 +311,7 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
     constexpr int ENV_SLOTS = NP * DSP;
 #ifdef TRX_PHASE_STAMPS
     unsigned long long stamp_prev_ = __builtin_amdgcn_s_memtime();
+    const unsigned long long wg_start_ = stamp_prev_;
 #endif
 
     // ------------------------------------------------ per-env activation
@@ -392,6 +405,7 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
     for (int it = 0; it < p.iters; ++it) {
         int amb = 0;
         int nscan = 0;
+        uint32_t ow[NQ];  // the tree's scan order, four nodes per word (pair-uniform)
         // ---------------- shortest-path tree per lane pair (Dijkstra, sparse relaxation)
         if (tree_on) {
 #pragma unroll
@@ -409,7 +423,9 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
                     pl[4 * q + 2 * j + 1] = kNoPred;
                 }
             }
-            ol[0] = (uint8_t)origin;
+            ow[0] = (uint32_t)origin;
+#pragma unroll
+            for (int q = 1; q < NQ; ++q) ow[q] = 0u;
             wave_sync_w();
             uint64_t m[KL];
             // relax u's out-slots of lane j from label bl (FIRST: the origin, label 0:
@@ -438,7 +454,9 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
                     // scipy's strict improvement: u becomes v's predecessor.  An equal key:
                     // v holds this label from the tail pl[v] already; the tails' labels
                     // are equal (heap order decides: exact replay) iff the costs are
+#ifndef TRX_PAIR_NOPRED  // diagnostic variant: predecessor stores left out (wrong results; timing only)
                     if (nk[r] < was[r]) pl[hv[r]] = (uint8_t)u;
+#endif
                     if (nk[r] == was[r]) {
                         const int tail = pl[hv[r]];
                         const float ct = stl[seid[(tail << 5) + (int)hv[r]]];
@@ -468,8 +486,10 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
                     if (FULL || alive) {
                         const uint64_t best = dbits_w(bd);
                         const uint32_t u = (uint32_t)best & 31u;
-                        kt[u] = kScannedW;  // both lanes of the pair store the same words
-                        ol[k] = (uint8_t)u;
+                        // scanned: the key's high word becomes 0xFFF80000 (a quiet NaN, negative);
+                        // both lanes of the pair store the same word
+                        reinterpret_cast<uint32_t*>(kt + u)[1] = (uint32_t)(kScannedW >> 32);
+                        ow[k >> 2] |= u << (8 * (k & 3));
                         nscan = k + 1;
                         // FULL: the last step's heads are all scanned -- nothing to relax
                         if (FULL ? k + 1 < NP : true) relax(u, bitsd_w(best & ~31ull), false, FULL ? k + 1 < NP : k + 1 < N);
@@ -483,7 +503,15 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
         // the wave takes part: the heap lives in the wave's registers)
         amb |= (int)wdpp<0xB1>((uint32_t)amb);
         const uint64_t need = __ballot(amb != 0 && j == 0);
-        if (need) {  // wave-uniform
+#ifdef TRX_PHASE_STAMPS
+        if (tid == 0) atomicAdd(&trx_phase_cycles_w[7], (unsigned long long)__popcll(need));  // replayed trees (wave 0)
+#endif
+        if (need) {  // wave-uniform: the scan orders go through LDS, where the replays rewrite theirs
+            if (tree_on && j == 0) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) reinterpret_cast<uint32_t*>(ol)[q] = ow[q];
+            }
+            wave_sync_w();
             uint64_t pend = need;
             while (pend) {
                 const int bit = __builtin_ctzll(pend);
@@ -493,6 +521,10 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
                 replay_tree_pair<RS>(N, soc + le * ENV_SLOTS, g.origins[zt], sord + t * NP, spred + t * NP);
             }
             wave_sync_w();
+            if (tree_on) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) ow[q] = reinterpret_cast<const uint32_t*>(ol)[q];
+            }
         }
         TRX_WSTAMP(2);
         // ---------------- all-or-nothing (repair_env.py:490-502, 707-722): subtree demand
@@ -501,7 +533,11 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
         // demands: exact in any order).  The pair takes the scan slots two at a time:
         // lane 0 slot 2g + 1, lane 1 slot 2g; lane 0's S is final when read, lane 1 adds
         // it over a DPP broadcast when lane 0's node is its child.
+#ifdef TRX_PAIR_NOSUB  // diagnostic variant: no subtree pass (wrong results; timing only)
+        if (false) {
+#else
         if (tree_on) {
+#endif
             const float* dm = gdem + zi * N;
             uint32_t* const sa = reinterpret_cast<uint32_t*>(kt);  // the key row is dead
             float un = 0.0f;
@@ -520,9 +556,6 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
             }
             unassigned_lane = un;
             const int ns = FULL ? NP : nscan;
-            uint32_t ow[NQ];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) ow[q] = reinterpret_cast<const uint32_t*>(ol)[q];
             wave_sync_w();
             uint32_t* const ll = sload + lenv * E;
             const uint32_t sh0 = 8u * (1u - (uint32_t)j);  // my byte of a slot pair: slot 2g + 1 - j
@@ -642,6 +675,9 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
         }
     }
     TRX_WSTAMP(5);
+#ifdef TRX_PHASE_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) trx_wg_cycles_w[blockIdx.x] = __builtin_amdgcn_s_memtime() - wg_start_;
+#endif
 }
 
 LaunchCfg pair_launch_cfg(const DevGraph& g, int num_envs, int method) {

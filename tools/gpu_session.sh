@@ -57,19 +57,19 @@ for s in "$@"; do
              step pmc4 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc4 -o run --output-format csv -- python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu ;;
         profrand) step profrand 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profrand -o run --output-format csv -- python3 bench.py --workload env --damage random --steps 44 --warmup 22 --no-cpu ;;
         # raw counter CSVs stay on the box (gpurun copies back <= 64 MiB): summarised there
-        # into profiles/r05_<name>_pmc.json (tools/pmc_summary.py, same library)
+        # into profiles/r06_<name>_pmc.json (tools/pmc_summary.py, same library)
         pmcenv) pmc4 pmcenv python3 bench.py --workload env --steps 22 --warmup 0 --no-cpu &&
-                python tools/pmc_summary.py r05_sf "pmcenv_p*" env_kernel > gpurun_out/pmcenv_summary.log 2>&1
-                cp profiles/r05_sf_pmc.json gpurun_out/; rm -rf gpurun_out/pmcenv_p* ;;
+                python tools/pmc_summary.py r06_sf "pmcenv_p*" env_kernel > gpurun_out/pmcenv_summary.log 2>&1
+                cp profiles/r06_sf_pmc.json gpurun_out/; rm -rf gpurun_out/pmcenv_p* ;;
         pmcana) pmc4 pmcana python3 bench.py --network anaheim --steps 6 --warmup 2 --no-cpu &&
-                python tools/pmc_summary.py r05_ana "pmcana_p*" env_kernel_big > gpurun_out/pmcana_summary.log 2>&1
-                cp profiles/r05_ana_pmc.json gpurun_out/; rm -rf gpurun_out/pmcana_p* ;;
+                python tools/pmc_summary.py r06_ana "pmcana_p*" env_kernel_big > gpurun_out/pmcana_summary.log 2>&1
+                cp profiles/r06_ana_pmc.json gpurun_out/; rm -rf gpurun_out/pmcana_p* ;;
         pmcact) pmc4 pmcact python3 tools/agent_profile.py 4096 act &&
-                python tools/pmc_summary.py r05_act "pmcact_p*" gat_layer gat_mid edge_head gat_prologue Cijk > gpurun_out/pmcact_summary.log 2>&1
-                cp profiles/r05_act_pmc.json gpurun_out/; rm -rf gpurun_out/pmcact_p* ;;
+                python tools/pmc_summary.py r06_act "pmcact_p*" gat_layer gat_mid edge_head gat_prologue Cijk > gpurun_out/pmcact_summary.log 2>&1
+                cp profiles/r06_act_pmc.json gpurun_out/; rm -rf gpurun_out/pmcact_p* ;;
         pmcupd) pmc4 pmcupd python3 tools/agent_profile.py 4096 update &&
-                python tools/pmc_summary.py r05_upd "pmcupd_p*" trx:: Cijk > gpurun_out/pmcupd_summary.log 2>&1
-                cp profiles/r05_upd_pmc.json gpurun_out/; rm -rf gpurun_out/pmcupd_p* ;;
+                python tools/pmc_summary.py r06_upd "pmcupd_p*" trx:: Cijk > gpurun_out/pmcupd_summary.log 2>&1
+                cp profiles/r06_upd_pmc.json gpurun_out/; rm -rf gpurun_out/pmcupd_p* ;;
         stamps) step stamps 300 python tools/phase_stamps.py 4096 ;;
         stampsrand)
                     step stamps_rand 300 env TRX_DAMAGE=random python tools/phase_stamps.py 4096 &&

@@ -15,10 +15,15 @@ from trafficrl import _lib  # noqa: E402
 
 _lib.LIB_PATH = os.path.join(ROOT, "sac-gat-her_transportationrl_amd", "trafficrl", "libtrafficrl_stamps.so")
 L = _lib.load()
-# each small-graph kernel has its own counters: sparse (default), packed, quad
-KIND = os.environ.get("TRX_KERNEL", "sparse")
-PACKED = KIND != "quad"
-if KIND == "packed":
+# each small-graph kernel has its own counters: pair (default), sparse, packed, quad
+KIND = os.environ.get("TRX_KERNEL", "pair")
+PACKED = KIND not in ("quad", "pair")
+EPW = 4 if KIND == "pair" else 2   # Sioux Falls envs per workgroup
+if KIND == "pair":
+    os.environ.pop("TRX_KERNEL", None)   # the pair kernel is the default selection
+    L.trx_debug_phase_cycles = L.trx_debug_phase_cycles_w
+    L.trx_debug_wg_cycles_s = L.trx_debug_wg_cycles_w
+elif KIND == "packed":
     L.trx_debug_phase_cycles = L.trx_debug_phase_cycles_p
 elif KIND == "sparse":
     L.trx_debug_phase_cycles = L.trx_debug_phase_cycles_s
@@ -44,25 +49,28 @@ for _ in range(5):
     a = (torch.rand(B, 76, device="cuda", generator=gen) * env.damaged).argmax(1).to(torch.int32)
     env.step(a, observe=False)
 L.trx_debug_phase_cycles(buf, 1)
-names = (["load", "dijkstra", "pred pass", "replay+subtree", "barrier wait", "gather+update+bpr", "tstt+store"]
+names = (["load", "dijkstra", "replay", "subtree+barrier", "update+bpr+barrier", "tstt+store", "-"]
+         if KIND == "pair" else
+         ["load", "dijkstra", "pred pass", "replay+subtree", "barrier wait", "gather+update+bpr", "tstt+store"]
          if KIND == "sparse" else
          ["load", "dijkstra", "tie check+replay", "aon walk", "barrier wait", "update+bpr", "tie candidates"]
          if PACKED else ["load", "cost build", "dijkstra", "tie check+replay", "aon", "update+bpr", "tstt+store"])
 tot = sum(buf[i] for i in range(7))
-if KIND == "sparse":
-    print(f"replayed trees (wave 0 of each workgroup): {buf[7]} over 5 steps x {B // 2} workgroups x 30 iterations "
-          f"x 16 trees = {buf[7] / (5 * (B // 2) * 30 * 16) * 100:.3f} %")
+if KIND in ("sparse", "pair"):
+    tpw = 32 if KIND == "pair" else 16
+    print(f"replayed trees (wave 0 of each workgroup): {buf[7]} over 5 steps x {B // EPW} workgroups x 30 iterations "
+          f"x {tpw} trees = {buf[7] / (5 * (B // EPW) * 30 * tpw) * 100:.3f} %")
 for i, n in enumerate(names):
-    print(f"{n:>14}: {buf[i] / tot * 100:6.2f} %  ({buf[i] / 5 / (B / 4) / 30:.0f} cycles/WG/iter)")
+    print(f"{n:>18}: {buf[i] / tot * 100:6.2f} %  ({buf[i] / 5 / (B / EPW) / 30:.0f} cycles/WG/iter)")
 
 # per-workgroup wall cycles of the last step launch: the launch lasts as long as its slowest workgroup
 import numpy as np  # noqa: E402
 L.trx_debug_wg_cycles_s.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-nb = B // 2
+nb = B // EPW
 wg = (ctypes.c_ulonglong * nb)()
 L.trx_debug_wg_cycles_s(wg, nb)
 w = np.array(wg[:nb], dtype=np.float64)
 print("per-WG cycles of the last launch: mean %.0f  p50 %.0f  p90 %.0f  p99 %.0f  max %.0f" %
       (w.mean(), np.percentile(w, 50), np.percentile(w, 90), np.percentile(w, 99), w.max()))
 slow = np.argsort(w)[-8:]
-print("slowest workgroups (envs 2k, 2k+1):", [(int(i), int(w[i])) for i in slow])
+print(f"slowest workgroups (envs {EPW}k..):", [(int(i), int(w[i])) for i in slow])
