@@ -200,7 +200,7 @@ def lib_sha16():
         return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
-PMC_SUMMARIES = {"sf": "r05_sf_pmc.json", "anaheim": "r04_ana_pmc.json"}
+PMC_SUMMARIES = {"sf": "r06_sf_pmc.json", "anaheim": "r05_ana_pmc.json"}
 
 
 def measured_traffic(network, kname):

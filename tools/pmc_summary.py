@@ -57,9 +57,11 @@ def mangled_key(short):
     key = f"{len(name)}{name}"
     if targs is not None:
         args = [a.strip() for a in targs.split(",")]
-        if not all(re.fullmatch(r"-?\d+", a) for a in args):
+        if not all(re.fullmatch(r"-?\d+|true|false", a) for a in args):
             return None
-        key += "I" + "".join(f"Li{a}E" if not a.startswith("-") else f"Lin{a[1:]}E" for a in args) + "E"
+        enc = {"true": "Lb1E", "false": "Lb0E"}
+        key += "I" + "".join(enc.get(a) or (f"Li{a}E" if not a.startswith("-") else f"Lin{a[1:]}E")
+                             for a in args) + "E"
     return key
 
 
