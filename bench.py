@@ -410,7 +410,7 @@ def main():
     reset_ev = []      # env_kernel reset launches (whole-batch cold resets, once per episode)
     phase_ev = {}      # per-phase events (train workload)
     phase_on = [False]  # recording them (the instrumented steps after the timed loop)
-    PHASE_STEPS = 16    # instrumented steps: four updates at update_every 4
+    PHASE_STEPS = 64    # instrumented steps: sixteen updates at update_every 4
 
     def timed(fn, bucket):
         s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -516,6 +516,7 @@ def main():
     for v in phase_ev.values():
         v.clear()
     torch.cuda.synchronize()
+    upd0 = tr.updates_done if args.workload == "train" else 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         one_step()
@@ -524,6 +525,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    upd_in_loop = (tr.updates_done - upd0) if args.workload == "train" else 0
     step_ms = [s.elapsed_time(e) for s, e in ev_pairs]
     reset_ms = [s.elapsed_time(e) for s, e in reset_ev]
     if args.workload == "train":   # the per-phase breakdown, from instrumented steps after the timed loop
@@ -576,9 +578,12 @@ def main():
         # update per 4 transitions, src/train.py:954-955) instead of the bench's 1/(4B)
         upd_ms = [s_.elapsed_time(e_) for s_, e_ in phase_ev["update"]]
         ms_upd = float(np.mean(upd_ms))
-        ms_rest = elapsed / args.steps * 1e3 - float(np.sum(upd_ms)) / PHASE_STEPS   # one iteration without updates
+        # one iteration without its updates: the timed loop's own update count times the
+        # instrumented mean update time (update_unit "transitions" runs a varying number)
+        ms_rest = elapsed / args.steps * 1e3 - upd_in_loop * ms_upd / args.steps
         flops = sac_update_flops(int(cfg["batch_size"]), N, E)
         upd_stats = {"ms_per_update": ms_upd, "updates_per_s": 1e3 / ms_upd, "updates_timed": len(upd_ms),
+                     "updates_in_timed_loop": upd_in_loop,
                      "flops_per_update": flops, "mfma_frac": flops / (ms_upd / 1e3) / MFMA_PEAK_BF16,
                      "env_steps_per_s_at_reference_utd": 1e3 / (ms_rest / B + ms_upd / 4.0),
                      "note": "mfma_frac: GEMM FLOPs of 3 no-grad + 3 training forwards and 3 backwards "
@@ -639,7 +644,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "breakdown_note": (f"act / update: HIP events over {PHASE_STEPS} instrumented steps after the timed "
-                               "loop; env_*: events around every env launch of the timed loop")
+                               f"loop ({len(phase_ev.get('update', []))} updates); env_*: events around every env "
+                               "launch of the timed loop")
             if args.workload == "train" else None,
             "breakdown_ms_per_step": dict(breakdown, env_kernel=float(np.sum(kern_ms)) / args.steps,
                                           env_step_kernel=float(np.sum(step_ms)) / args.steps,

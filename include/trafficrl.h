@@ -427,7 +427,10 @@ int trx_gat_tail_infer(const trx_gat_tail_args* a, void* stream);
 int trx_edge_head_backward(const trx_edge_head_args* a, const float* grad_logits, void* grad_p, float* grad_c,
                            void* grad_z, float* grad_w2_part, float* grad_we_part, float* grad_ea, void* stream);
 /* ABI 11: trx_edge_head_backward for `count` networks in one launch; io[k]
- * holds network k's gradient buffers (the arguments of the single call). */
+ * holds network k's gradient buffers (the arguments of the single call).  The
+ * networks must agree on num_graphs, edges_per_graph, nodes_per_graph, hidden,
+ * edge_dim, exact, softmax, the presence of u and the presence of grad_z
+ * (TRX_EINVAL otherwise). */
 typedef struct trx_edge_head_bwd_io {
     const float* grad_logits;
     void* grad_p;

@@ -897,6 +897,14 @@ static int check_edge_head_backward(const trx_edge_head_args* a, const trx_edge_
     return TRX_OK;
 }
 
+// the fields every network of one backward launch must share (the kernel reads
+// network 0's for the launch shape; each block's buffers are its own): those of
+// the forward's same_shape plus the presence of grad_z
+static bool same_shape_bwd(const trx_edge_head_args& x, const trx_edge_head_bwd_io& xio, const trx_edge_head_args& y,
+                           const trx_edge_head_bwd_io& yio) {
+    return same_shape(x, y) && (xio.grad_z != nullptr) == (yio.grad_z != nullptr);
+}
+
 int trx_edge_head_backward_multi(const trx_edge_head_args* a, const trx_edge_head_bwd_io* io, int32_t count,
                                  void* stream) {
     if (!a || !io || count < 1 || count > TRX_MAX_NETS)
@@ -905,10 +913,7 @@ int trx_edge_head_backward_multi(const trx_edge_head_args* a, const trx_edge_hea
     for (int k = 0; k < count; ++k) {
         const int rc = check_edge_head_backward(a + k, io + k);
         if (rc != TRX_OK) return rc;
-        const trx_edge_head_args& b = a[k];
-        if (!(b.num_graphs == a->num_graphs && b.edges_per_graph == a->edges_per_graph &&
-              b.nodes_per_graph == a->nodes_per_graph && b.hidden == a->hidden && b.edge_dim == a->edge_dim &&
-              b.exact == a->exact))
+        if (!same_shape_bwd(a[k], io[k], *a, *io))
             return fail(TRX_EINVAL, "edge_head_backward_multi: network %d differs from network 0 in shape or mode", k);
         items[k].a = a[k];
         items[k].io = io[k];

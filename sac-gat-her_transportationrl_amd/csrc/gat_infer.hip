@@ -648,9 +648,10 @@ __global__ void __launch_bounds__(kInferThreads) edge_head_infer_kernel(const Ne
         eal[v] = j < D ? a.ea[((int64_t)g * E + e) * D + j] : 0.0f;
     }
     constexpr int DC = DK > 0 ? DK : ED;
-    // a lane's four hidden units as two pairs: the per-unit arithmetic below runs on
-    // packed float32 pairs (v_pk_mul_f32 / v_pk_add_f32), the same IEEE operations
-    // in the same order per unit as scalar code (bit-identical), half the VALU issue
+    // a lane's four hidden units as two pairs: the per-unit arithmetic below is written on
+    // float32 pairs (for v_pk_mul_f32 / v_pk_add_f32); under -packed-fp32-ops (Makefile:
+    // the gfx950 packed -> DPP hazard) each pair compiles to scalar ops, the
+    // same IEEE operations in the same order per unit (bit-identical)
     trx_f2 we2[MQ][2][DC], c2[MQ][2];
     float w2_r[MQ][4];
 #pragma unroll

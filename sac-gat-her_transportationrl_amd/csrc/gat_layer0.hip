@@ -368,8 +368,9 @@ __global__ void __launch_bounds__(HC / 4) gat_mid_gen_kernel(trx_gat_mid_args a)
     }
     __syncthreads();
     // aggregation + bias + LayerNorm + regenerated residual + ReLU, NB nodes per round.
-    // The four channels as two packed pairs (v_pk_mul_f32 / v_pk_add_f32: each lane of a
-    // pair is the scalar operation, so the regenerated residual keeps layer 0's values)
+    // The four channels as two float pairs (written for v_pk_mul_f32 / v_pk_add_f32; the
+    // library is built with -packed-fp32-ops, so each pair compiles to two scalar ops:
+    // the same IEEE operations, and the regenerated residual keeps layer 0's values)
     typedef float f2 __attribute__((ext_vector_type(2)));
     f2 w0p[4][2], wpp[4][2], b0p[2], g0p[2], e0p[2], bpp[2], b1p[2], g1p[2], e1p[2];
 #pragma unroll

@@ -1,6 +1,7 @@
 """Autograd helpers for the GAT-SAC update's odd-shaped products.
 
-Profiling one SAC update (tools/update_profile.py) showed two kinds of ops
+Profiling one SAC update (round 2; DESIGN.md §6, profiles/r02_update_kernel_stats.csv)
+showed two kinds of ops
 costing far more than their FLOPs:
 
 * weight gradients of "skinny" products -- a 4-, 6- or 1-wide side against a
@@ -72,8 +73,8 @@ class _SplitKLinear(torch.autograd.Function):
     gradient is `splits` bf16 partial products over K/splits batch rows summed
     in float32 and returned as the float32 master weight's gradient: no
     bf16 -> float32 cast of dW, and hipBLASLt's single-tile walk over K = 6144
-    (~11 % of the MFMA peak) becomes a batched product (tools/wgrad_probe.py:
-    44 -> 29 us for 6144 x 1024 x 1024)."""
+    (~11 % of the MFMA peak) becomes a batched product (44 -> 29 us for
+    6144 x 1024 x 1024 in round 2's probe)."""
 
     @staticmethod
     def forward(ctx, x, w, splits: int):

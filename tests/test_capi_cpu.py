@@ -329,3 +329,21 @@ def test_multi_launches_validated_without_gpu():
     io = _lib.TrxEdgeHeadBwdIO()
     assert L.trx_edge_head_backward_multi(_lib.multi(_lib.TrxEdgeHeadArgs, [_lib.TrxEdgeHeadArgs()]),
                                           _lib.multi(_lib.TrxEdgeHeadBwdIO, [io]), 0, None) == _lib.TRX_EINVAL
+    # the backward's networks must agree like the forward's, and on the presence of grad_z
+    def eh(softmax, gz):
+        b = _lib.TrxEdgeHeadArgs()
+        b.num_graphs, b.edges_per_graph, b.nodes_per_graph, b.hidden, b.edge_dim, b.softmax = 0, 76, 24, 256, 6, softmax
+        buf = (ctypes.c_float * 16)()
+        keep.append(buf)
+        p = ctypes.addressof(buf)
+        b.src = b.dst = b.p = b.c = b.ea = b.we = b.w2 = p
+        o = _lib.TrxEdgeHeadBwdIO()
+        o.grad_logits = o.grad_p = o.grad_c = o.grad_w2_part = o.grad_we_part = o.grad_ea = p
+        o.grad_z = p if gz else None
+        return b, o
+    def bwd(*nets):
+        return L.trx_edge_head_backward_multi(_lib.multi(_lib.TrxEdgeHeadArgs, [n[0] for n in nets]),
+                                              _lib.multi(_lib.TrxEdgeHeadBwdIO, [n[1] for n in nets]), len(nets), None)
+    assert bwd(eh(0, False), eh(0, False)) == 0
+    assert bwd(eh(0, False), eh(1, False)) == _lib.TRX_EINVAL
+    assert bwd(eh(0, True), eh(0, False)) == _lib.TRX_EINVAL and b"differs" in L.trx_last_error()
