@@ -86,6 +86,12 @@ constexpr uint64_t kUnreachedW = 0x7FF8000000000000ull;  // | id: quiet NaN, lar
 constexpr uint64_t kScannedW = 0xFFF8000000000000ull;    // quiet NaN, negative integer
 constexpr int kPairMaxDeg = 8;                           // out-slots per node: 2 lanes x RS rounds
 constexpr uint32_t kEidBytes = 32 * 32;                  // (u, v) -> link id table at LDS offset 0
+#ifndef TRX_PAIR_WAVE_REPLAYS
+#define TRX_PAIR_WAVE_REPLAYS 2
+#endif
+// ambiguous trees of a wave up to which the whole wave replays them one at a time
+// (heap in registers); above it every pair leader replays its own tree at once
+constexpr int kWaveReplays = TRX_PAIR_WAVE_REPLAYS;
 
 struct SmemW {
     uint32_t flow, cap, dmg, goal, t, aux, dprev;  // [EPW*E] f32 (aux: u32 AON link loads during an iteration)
@@ -250,6 +256,60 @@ __device__ __forceinline__ void replay_tree_pair(int N, const uint64_t* oc, int 
                 } else if (h->val[jc] > nv) {
                     fh_decrease(H, jc, nv);
                     if (lane == 0) pl[jc] = (uint8_t)v;
+                }
+            }
+        }
+    }
+}
+
+// Fibonacci-heap storage of one per-lane replay sized for NPX nodes, carved from
+// the wave's key rows in LDS (dead between the Dijkstra and the subtree pass).
+template <int NPX>
+struct FibSmallW {
+    using idx_t = int8_t;
+    double val[NPX];
+    int8_t parent[NPX], left[NPX], right[NPX], child[NPX];
+    uint8_t rank[NPX], state[NPX];
+    int8_t roots[32];
+};
+
+// The exact scipy-heap replay of one ambiguous tree by ONE lane (its pair leader),
+// the heap in LDS: many of a wave's trees replay concurrently (cold resets with
+// random damage are tie-heavy), where replay_tree_pair takes them one at a time.
+// Same loop, same adjacency and costs.
+template <int NP, int RS>
+__device__ __noinline__ void replay_tree_lane(int N, const uint64_t* oc, int origin, FibSmallW<NP>* h, uint8_t* ol,
+                                              uint8_t* pl) {
+    for (int k = 0; k < N; ++k) {
+        h->val[k] = 0.0;
+        h->parent[k] = h->left[k] = h->right[k] = h->child[k] = -1;
+        h->rank[k] = 0;
+        h->state[k] = 0;
+        pl[k] = kNoPred;
+    }
+    Heap<FibSmallW<NP>> H{h, -1};
+    fh_insert(H, origin);
+    int k = 0;
+    while (H.min >= 0) {
+        const int v = fh_remove_min(H);
+        h->state[v] = 2;
+        ol[k++] = (uint8_t)v;
+        const double vv = h->val[v];
+        for (int q = 0; q < 2 * RS; ++q) {
+            const uint64_t en = oc[(v * 2 + (q & 1)) * RS + (q >> 1)];
+            const int jc = (int)((uint32_t)en & 31u);
+            if (jc == v) break;  // no more out-links
+            const int st = h->state[jc];
+            if (st != 2) {
+                const double nv = vv + bitsd_w(en & ~31ull);
+                if (st == 0) {
+                    h->state[jc] = 1;
+                    h->val[jc] = nv;
+                    fh_insert(H, jc);
+                    pl[jc] = (uint8_t)v;
+                } else if (h->val[jc] > nv) {
+                    fh_decrease(H, jc, nv);
+                    pl[jc] = (uint8_t)v;
                 }
             }
         }
@@ -512,13 +572,38 @@ env_kernel_pair(const DevGraph g, const trx_params p, const trx_state s, int B, 
                 for (int q = 0; q < NQ; ++q) reinterpret_cast<uint32_t*>(ol)[q] = ow[q];
             }
             wave_sync_w();
-            uint64_t pend = need;
-            while (pend) {
-                const int bit = __builtin_ctzll(pend);
-                pend &= pend - 1;
-                const int t = (int)(tid >> 6) * 32 + (bit >> 1);  // the tree of pair leader `bit`
-                const int le = t / Z, zt = t - le * Z;
-                replay_tree_pair<RS>(N, soc + le * ENV_SLOTS, g.origins[zt], sord + t * NP, spred + t * NP);
+            if (__popcll(need) <= kWaveReplays) {  // few: one at a time, the whole wave, heap in registers
+                uint64_t pend = need;
+                while (pend) {
+                    const int bit = __builtin_ctzll(pend);
+                    pend &= pend - 1;
+                    const int t = (int)(tid >> 6) * 32 + (bit >> 1);  // the tree of pair leader `bit`
+                    const int le = t / Z, zt = t - le * Z;
+                    replay_tree_pair<RS>(N, soc + le * ENV_SLOTS, g.origins[zt], sord + t * NP, spred + t * NP);
+                }
+            } else {  // many: each pair leader replays its own tree, kSlots heaps at a time in the
+                      // wave's key rows
+                constexpr int kHeapBytes = (int)((sizeof(FibSmallW<NP>) + 15) & ~(size_t)15);
+                constexpr int kSlots = (32 * KR * 8) / kHeapBytes;
+                static_assert(kSlots >= 1, "replay heap does not fit the wave's key rows");
+                unsigned char* const area = reinterpret_cast<unsigned char*>(skeys + (size_t)(tid >> 6) * 32 * KR);
+                const int lane = tid & 63;
+                uint64_t pend = need;
+                while (pend) {  // wave-uniform
+                    uint64_t batch = 0, mm = pend;
+                    for (int c = 0; c < kSlots && mm; ++c) {
+                        const uint64_t bb = mm & (~mm + 1);
+                        batch |= bb;
+                        mm ^= bb;
+                    }
+                    pend &= ~batch;
+                    if ((batch >> lane) & 1ull) {  // my tree (I am its pair leader)
+                        const int slot = __popcll(batch & ((1ull << lane) - 1ull));
+                        replay_tree_lane<NP, RS>(N, soc + lenv * ENV_SLOTS, origin,
+                                                 reinterpret_cast<FibSmallW<NP>*>(area + slot * kHeapBytes), ol, pl);
+                    }
+                    wave_sync_w();
+                }
             }
             wave_sync_w();
             if (tree_on) {

@@ -46,8 +46,10 @@ def _run(tmp, sync, method="fw", iters=12, world=2, extra=None, timeout=240):
                 q.kill()
             raise
         outs.append(o.decode(errors="replace"))
-    for p, o in zip(procs, outs):
-        assert p.returncode == 0, o[-3000:]
+    bad = [(r, o) for r, (p, o) in enumerate(zip(procs, outs)) if p.returncode != 0]
+    # the rank that failed first, not its peers' "connection closed"
+    bad.sort(key=lambda ro: "Connection closed" in ro[1])
+    assert not bad, "\n".join(f"--- rank {r}:\n{o[-2500:]}" for r, o in bad[:2])
     return [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
 
 
@@ -114,10 +116,11 @@ def test_eight_ranks_config4_sharding(tmp_path):
     Unmeasured on hardware: RCCL over xGMI needs the 8-GPU node."""
     extra = {"TRX_WORKER_HIDDEN": "256", "TRX_WORKER_ENVS": "4096", "TRX_WORKER_BATCH": "256",
              "TRX_WORKER_BUFFER": "200000", "TRX_WORKER_AMP": "bf16", "TRX_WORKER_ITERS": "30",
-             "TRX_WORKER_UNIT": "iterations", "TRX_WORKER_EVERY": "4", "TRX_WORKER_ORACLE": "1"}
-    res = _run(tmp_path, sync=True, method="msa", iters=12, world=8, extra=extra, timeout=600)
+             "TRX_WORKER_UNIT": "iterations", "TRX_WORKER_EVERY": "2", "TRX_WORKER_ORACLE": "1"}
+    # 3 eager warm-up updates, then the captured graphs (every 2nd iteration: 10 updates)
+    res = _run(tmp_path, sync=True, method="msa", iters=20, world=8, extra=extra, timeout=600)
     assert all(r["graphed"] and r["split"] for r in res), [(r["graphed"], r["split"]) for r in res]
-    assert len({r["updates"] for r in res}) == 1 and res[0]["updates"] >= 3, [r["updates"] for r in res]
+    assert len({r["updates"] for r in res}) == 1 and res[0]["updates"] >= 6, [r["updates"] for r in res]
     assert len({r["episodes"] for r in res}) == 1
     assert all(r["reduce_calls"]["flat"] > 0 for r in res)
     assert all(r["oracle_rows"] for r in res)
