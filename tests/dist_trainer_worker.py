@@ -6,9 +6,10 @@ TRX_WORKER_UNIT / TRX_WORKER_EVERY set update_unit / update_every
 ("transitions" with random damage: per-env episode lengths differ, so the
 ranks' due-update counts differ and train.updates_due must deal them out).
 TRX_WORKER_ENVS / TRX_WORKER_BATCH / TRX_WORKER_BUFFER / TRX_WORKER_AMP /
-TRX_WORKER_ITERS set envs per rank, SAC batch, replay capacity, autocast dtype
-and assignment iterations (config #4's shard: 4096 envs, batch 256, bf16,
-MSA-30); TRX_WORKER_ORACLE=1 re-runs one warm-started assignment of the whole
+TRX_WORKER_ITERS / TRX_WORKER_SP set envs per rank, SAC batch, replay capacity,
+autocast dtype, assignment iterations and shortest-path rule (config #4's shard:
+4096 envs, batch 256, bf16, MSA-30, the bench's scipy rule; the trainer's own
+default is the reference config's torch rule); TRX_WORKER_ORACLE=1 re-runs one warm-started assignment of the whole
 shard after training and checks sampled rows against the C oracle
 (oracle/trx_oracle.c) bit for bit.
 
@@ -48,6 +49,7 @@ def main():
                update_unit=os.environ.get("TRX_WORKER_UNIT", "iterations"),
                her_ratio=0.5, assignment_method=method,
                assignment_iters=int(os.environ.get("TRX_WORKER_ITERS", "10")), fixed_damage=False,
+               sp_backend=os.environ.get("TRX_WORKER_SP", cfg["sp_backend"]),
                early_stop_patience=10 ** 6, episodes=10 ** 6, max_steps=0)
     tr = Trainer(cfg, device="cuda:0", rank=rank, world=world if sync else 1, log=False)
     if not sync:
@@ -95,8 +97,10 @@ def check_rows_vs_oracle(env, method, iters, rank):
     flow0 = env.flow[rows].cpu().numpy()
     env.assign()
     torch.cuda.synchronize()
+    from trafficrl import _lib
+    sp = "torch" if env.params.sp_rule == _lib.SP_TORCH else "scipy"   # the env's own rule
     f_o, t_o, ts_o, _ = og.assign(cap, dmg, flow0, method=method, iters=iters, nthreads=4,
-                                  penalty=float(env.params.unassigned_penalty))
+                                  penalty=float(env.params.unassigned_penalty), sp=sp)
     np.testing.assert_array_equal(env.flow[rows].cpu().numpy(), f_o)
     np.testing.assert_array_equal(env.t[rows].cpu().numpy(), t_o)
     np.testing.assert_array_equal(env.tstt[rows].cpu().numpy(), ts_o)

@@ -116,7 +116,8 @@ def test_eight_ranks_config4_sharding(tmp_path):
     Unmeasured on hardware: RCCL over xGMI needs the 8-GPU node."""
     extra = {"TRX_WORKER_HIDDEN": "256", "TRX_WORKER_ENVS": "4096", "TRX_WORKER_BATCH": "256",
              "TRX_WORKER_BUFFER": "200000", "TRX_WORKER_AMP": "bf16", "TRX_WORKER_ITERS": "30",
-             "TRX_WORKER_UNIT": "iterations", "TRX_WORKER_EVERY": "2", "TRX_WORKER_ORACLE": "1"}
+             "TRX_WORKER_UNIT": "iterations", "TRX_WORKER_EVERY": "2", "TRX_WORKER_ORACLE": "1",
+             "TRX_WORKER_SP": "scipy"}
     # 3 eager warm-up updates, then the captured graphs (every 2nd iteration: 10 updates)
     res = _run(tmp_path, sync=True, method="msa", iters=20, world=8, extra=extra, timeout=600)
     assert all(r["graphed"] and r["split"] for r in res), [(r["graphed"], r["split"]) for r in res]
@@ -128,15 +129,3 @@ def test_eight_ranks_config4_sharding(tmp_path):
         for k in res[0]["params"]:
             assert torch.equal(res[0]["params"][k], r["params"][k]), k
 
-
-def test_eight_ranks_transition_schedule(tmp_path):
-    """update_unit "transitions" over 8 ranks with random damage: the per-rank due
-    counts differ every iteration; train.updates_due deals the global sum out, so
-    all eight ranks run the same number of updates and end bit-identical."""
-    extra = {"TRX_WORKER_UNIT": "transitions", "TRX_WORKER_EVERY": "4"}
-    res = _run(tmp_path, sync=True, iters=12, world=8, extra=extra, timeout=600)
-    ups = [r["updates"] for r in res]
-    assert len(set(ups)) == 1 and ups[0] > 20, ups
-    for r in res[1:]:
-        for k in res[0]["params"]:
-            assert torch.equal(res[0]["params"][k], r["params"][k]), k
