@@ -5,7 +5,8 @@ warm-started assignment (trx_assign) of the whole batch from its state and
 compares every row with oracle/trx_oracle.c.  Mismatching rows' inputs and both
 results go to gpurun_out/trainer_mismatch_<kernel>.npz.
 
-usage: python tools/trainer_oracle_check.py [iters] [envs]   (TRX_KERNEL=sparse: the quad kernel)"""
+usage: python tools/trainer_oracle_check.py [iters] [envs]   (TRX_KERNEL=sparse: the quad kernel;
+TRX_CHECK_SP=scipy|torch: the shortest-path rule, default the trainer config's)"""
 import os
 import sys
 
@@ -23,7 +24,7 @@ def main():
     import oracle as O
     from trafficrl.train import Trainer, sf_config
     cfg = sf_config()
-    cfg.update(num_envs=envs, batch_start=64, batch_size=32, hidden_dim=32, embed_dim=32, eval_every=0,
+    cfg.update(sp_backend=os.environ.get("TRX_CHECK_SP", cfg["sp_backend"]), num_envs=envs, batch_start=64, batch_size=32, hidden_dim=32, embed_dim=32, eval_every=0,
                output_dir="/tmp/trx_oracle_check", update_every=4, update_unit="iterations", her_ratio=0.5,
                assignment_method="msa", assignment_iters=30, fixed_damage=False, early_stop_patience=10 ** 6,
                episodes=10 ** 6, max_steps=0)
@@ -39,8 +40,10 @@ def main():
     torch.cuda.synchronize()
     f_d, t_d, ts_d = env.flow.cpu().numpy(), env.t.cpu().numpy(), env.tstt.cpu().numpy()
     og = O.OracleGraph.from_npz(os.path.join(ROOT, "tests", "golden", "sf_graph.npz"))
+    from trafficrl import _lib
+    sp = "torch" if env.params.sp_rule == _lib.SP_TORCH else "scipy"   # the env's own rule
     f_o, t_o, ts_o, _ = og.assign(cap, dmg, flow0, method="msa", iters=30, nthreads=16,
-                                  penalty=float(env.params.unassigned_penalty))
+                                  penalty=float(env.params.unassigned_penalty), sp=sp)
     bad = np.nonzero(np.any(f_d != f_o, axis=1) | (ts_d != ts_o))[0]
     print(f"{kname}: {len(bad)} of {envs} rows differ from the oracle after {iters} training iterations"
           f"{' (first: ' + str(bad[:8].tolist()) + ')' if len(bad) else ''}", flush=True)
