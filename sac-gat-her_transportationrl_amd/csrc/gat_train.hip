@@ -123,7 +123,9 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(const NetList<trx_gat
     // which unpadded 2 KB / 4 KB strides put on the same LDS banks
     constexpr int XS = HC + EV, GS = HC + 4;
     XE* xs = reinterpret_cast<XE*>(smem);                      // [n][XS] bf16 lin output (exact: float; XG: none)
-    float* gv = reinterpret_cast<float*>(xs + (XG ? 0 : n * XS));  // [n][GS] dL/d(aggregate + bias)
+    float* w0s = reinterpret_cast<float*>(smem);               // XG, layer 0: [HC][IN] lin.weight (for the xh recompute)
+    float* gv = XG ? w0s + (IN > 0 ? HC * IN : 0)
+                   : reinterpret_cast<float*>(xs + n * XS);    // [n][GS] dL/d(aggregate + bias)
     float* al = gv + n * GS;                                   // [me*H] attention weights
     float* ge = al + a.max_graph_edges * H;                    // [me*H] dL/dalpha, then dL/de
     float* asd = ge + a.max_graph_edges * H;                   // [n][2H] a_src | a_dst
@@ -157,6 +159,8 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(const NetList<trx_gat
             x0l[v] = XF ? a.x0[(size_t)node0 * IN + v] : rbf(a.x0[(size_t)node0 * IN + v]);
             gx0[v] = 0.0f;
         }
+    if (XG && IN > 0)  // every xh recompute below reads the weights from LDS, not per term from global memory
+        for (int v = tid; v < HC * IN; v += kT) w0s[v] = a.w0[v];
     if (IN == 0 && !XG) {
         const uint4* src = reinterpret_cast<const uint4*>(static_cast<const XE*>(a.xh) + (size_t)node0 * HC);
         constexpr int Q8 = HC / EV;
@@ -197,7 +201,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(const NetList<trx_gat
             for (int r = 0; r < 4; ++r) {
                 acc[r] = 0.0f;
 #pragma unroll
-                for (int j = 0; j < INR; ++j) acc[r] += x0l[i * IN + j] * a.w0[(size_t)(col + r) * IN + j];
+                for (int j = 0; j < INR; ++j) acc[r] += x0l[i * IN + j] * w0s[(col + r) * IN + j];
             }
             return make_float4(acc[0], acc[1], acc[2], acc[3]);
         }
@@ -449,7 +453,8 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(const NetList<trx_gat
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
-                    for (int jj = 0; jj < INR; ++jj) rx[jj] += ob[r] * a.w0[(size_t)(f0 + r) * IN + jj];
+                    for (int jj = 0; jj < INR; ++jj)
+                        rx[jj] += ob[r] * (XG ? w0s[(f0 + r) * IN + jj] : a.w0[(size_t)(f0 + r) * IN + jj]);
             }
         }
         if (IN > 0) {
@@ -517,7 +522,7 @@ __global__ void __launch_bounds__(NT) gat_layer_bwd_kernel(const NetList<trx_gat
 
 size_t gat_layer_bwd_smem(const trx_gat_layer_bwd_args& a) {
     const size_t HC = (size_t)a.heads * a.channels, n = a.nodes_per_graph, H = a.heads, me = a.max_graph_edges;
-    return (a.exact ? (HC > 512 ? 0 : n * (HC + 4) * 4) : n * (HC + 8) * 2) + n * (HC + 4) * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
+    return (a.exact ? (HC > 512 ? (a.in_dim > 0 ? HC * a.in_dim * 4 : 0) : n * (HC + 4) * 4) : n * (HC + 8) * 2) + n * (HC + 4) * 4 + 2 * me * H * 4 + 2 * n * H * 4 + 2 * n * H * 4 + 2 * n * 4 + 8 * n * 4 +
            (a.g_pool ? 2 * HC * 4 : 0) + (2 * me + 2 * (n + 1) + me) * 4;
 }
 
